@@ -1,0 +1,83 @@
+/* duck.h — C ABI of the MI355X Open Duck Joystick simulator (libduck.so).
+ *
+ * This is the drop-in boundary for the reference's hot path. Each entry point replaces
+ * one reference interface (file:line under /root/reference):
+ *
+ *   duck_create        OpenDuckMiniV2Env.__init__ + Joystick._post_init
+ *                        (playground/open_duck_mini_v2/base.py:44-132, joystick.py:121-204);
+ *                        the model arrives pre-compiled (duck_model.h), like mjx.put_model (base.py:61)
+ *   duck_reset         Joystick.reset(rng) -> State          (joystick.py:206-321)
+ *   duck_step          Joystick.step(state, action) -> State (joystick.py:323-481), optionally
+ *                        wrapped by EpisodeWrapper + BraxAutoResetWrapper (common/runner.py:117)
+ *   duck_randomize     randomize.domain_randomize(model, rng) (common/randomize.py:26-146)
+ *   duck_physics_step  mjx_env.step(model, data, ctrl, n_substeps) (joystick.py:420);
+ *                        n_substeps = 0 is mjx_env.init's mjx.forward (joystick.py:258)
+ *
+ * Conventions: all array arguments are DEVICE pointers (HIP/torch allocations on the
+ * handle's device), float32 unless stated, `stream` is a hipStream_t (NULL = default).
+ * Per-env state is struct-of-arrays with the layout of duck_env.h (fstate/istate);
+ * obs/priv/action are row-major [n_envs][k]. The caller owns every buffer; the handle owns
+ * only device-resident model constants. No call allocates, synchronises or throws; errors
+ * are returned as negative codes with a thread-local message in duck_last_error().
+ * Calls on one handle are not thread-safe; work is ordered on `stream`.
+ */
+#ifndef DUCK_H_
+#define DUCK_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "duck_env.h"
+#include "duck_model.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct duck_sim duck_sim;
+
+enum { DUCK_OK = 0, DUCK_EINVAL = -1, DUCK_EUNSUPPORTED = -2, DUCK_EHIP = -3 };
+
+/* library version (major*10000 + minor*100 + patch) */
+int duck_version(void);
+/* message of the last failing call on this thread ("" if none) */
+const char* duck_last_error(void);
+/* per-env state layout for a model/config (same as duck_layout_make) */
+int duck_layout_get(int nq, int nv, int nu, int imitation, duck_layout* out);
+/* size in floats of the per-env debug record written by duck_physics_step(aux) */
+int duck_aux_size(const duck_sim* sim);
+
+/* Create a simulator for `model` (one of the Open Duck scenes; the kernel is specialised
+ * on the model structure and rejects others with DUCK_EUNSUPPORTED). `ref` may be NULL
+ * when cfg->use_imitation == 0. `device` is the HIP device ordinal. */
+int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const duck_refmotion* ref, int device,
+                duck_sim** out);
+void duck_destroy(duck_sim* sim);
+
+/* Joystick.reset for envs [env_offset, env_offset + n_envs): key derived from
+ * (seed, global env id). `mask` (uint8 [n_envs], nullable) restricts the reset to envs
+ * with mask != 0. Writes fstate/istate/obs/priv. */
+int duck_reset(duck_sim* sim, int n_envs, float* fstate, int32_t* istate, const uint8_t* mask, uint64_t seed,
+               int64_t env_offset, const float* dr, float* obs, float* priv, void* stream);
+
+/* Joystick.step (+ wrappers if cfg->auto_reset). `dr` (nullable) = per-env randomised
+ * model values (duck_dr_layout, SoA [k][n_envs]) written by duck_randomize. `reward`,
+ * `done` are [n_envs]. `scratch` (nullable unless feet can collide) = n_envs*nv*nv floats
+ * for the rare dense-Hessian path. */
+int duck_step(duck_sim* sim, int n_envs, float* fstate, int32_t* istate, const float* dr, const float* action,
+              float* obs, float* priv, float* reward, float* done, float* scratch, void* stream);
+
+/* domain_randomize: fill dr (SoA [duck_dr_layout.nfloat][n_envs]) for global env ids
+ * [env_offset, env_offset + n_envs). */
+int duck_randomize(duck_sim* sim, int n_envs, float* dr, uint64_t seed, int64_t env_offset, void* stream);
+
+/* mjx_env.step on raw physics state (SoA [k][n_envs]): qpos [nq], qvel/qacc_warmstart [nv],
+ * ctrl [nu]. n_substeps = 0 runs one forward pass without integration. `aux` (nullable)
+ * receives the last substep's forward record (duck_aux_size floats per env, SoA). */
+int duck_physics_step(duck_sim* sim, int n_envs, float* qpos, float* qvel, float* qacc_warmstart, const float* ctrl,
+                      const float* dr, int n_substeps, float* aux, float* scratch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DUCK_H_ */

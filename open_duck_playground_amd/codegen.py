@@ -1,0 +1,253 @@
+"""Emit the constexpr model header the HIP kernels are specialised on.
+
+MJX specialises its XLA program on the model structure at ``jit`` time (tree topology,
+joint types, collision pairs); the MI355X path does the same at build time: the model
+compiler (``mjcf.py``) output is written as a C++ struct of ``static constexpr`` tables,
+the kernels are templates over that struct, and every loop over bodies/dofs is fully
+unrolled with compile-time indices (registers and immediate LDS offsets instead of
+indirect loads). Per-env domain-randomised fields are read from the DR buffer instead
+of these constants (``csrc/duck_kernels.hip``).
+
+Usage: ``python -m open_duck_playground_amd.codegen`` (reads the committed assets).
+"""
+
+from __future__ import annotations
+
+import os
+from typing import List
+
+import numpy as np
+
+from .mjcf import JNT_FREE, Model, quat2mat
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _f(x) -> str:
+    x = float(x)
+    if x == 0.0:
+        return "0.0f"
+    r = repr(float(np.float32(x)))
+    if "e" not in r and "." not in r and "inf" not in r:
+        r += ".0"
+    return r + "f"
+
+
+def _arr(name: str, a, ctype: str) -> str:
+    a = np.asarray(a)
+    dims = "".join(f"[{d}]" for d in a.shape)
+    if a.size == 0:
+        dims = "[1]"
+        body = "{0}"
+        return f"  static constexpr {ctype} {name}{dims} = {body};\n"
+    fmt = _f if ctype == "float" else (lambda v: str(int(v)))
+
+    def rec(x):
+        if np.ndim(x) == 0:
+            return fmt(x)
+        return "{" + ", ".join(rec(y) for y in x) + "}"
+
+    return f"  static constexpr {ctype} {name}{dims} = {rec(a)};\n"
+
+
+def sparse_pattern(m: Model):
+    """Row i of M holds its ancestor dofs (incl. itself) in increasing order."""
+    rows: List[List[int]] = []
+    for i in range(m.nv):
+        anc = []
+        j = i
+        while j >= 0:
+            anc.append(j)
+            j = m.dof_parentid[j]
+        rows.append(sorted(anc))
+    adr = np.zeros((m.nv, m.nv), dtype=np.int64) - 1
+    k = 0
+    for i, r in enumerate(rows):
+        for j in r:
+            adr[i, j] = k
+            k += 1
+    return rows, adr, k
+
+
+def _ancestors(m: Model, k: int, include_self: bool):
+    out = [k] if include_self else []
+    j = m.dof_parentid[k]
+    while j >= 0:
+        out.append(j)
+        j = m.dof_parentid[j]
+    return out
+
+
+def sparse_code(m: Model, adr) -> str:
+    """Straight-line sparse LDL'/solve/matvec on the tree pattern of M (MuJoCo's
+    mj_factorM / mj_solveLD / mj_mulM). ``L`` is an accessor (per-thread LDS slice)."""
+    nv = m.nv
+    o = ["  // M = L' D L, in place: diag holds D, off-diagonals hold L (mj_factorM order)\n",
+         "  template <class A> static __device__ __forceinline__ void ldl_factor(const A& L) {\n"]
+    for k in range(nv - 1, -1, -1):
+        for i in _ancestors(m, k, False):
+            o.append(f"    {{ const float t = L[{adr[k, i]}] / L[{adr[k, k]}];")
+            for j in _ancestors(m, i, True):
+                o.append(f" L[{adr[i, j]}] -= t * L[{adr[k, j]}];")
+            o.append(f" L[{adr[k, i]}] = t; }}\n")
+        # bound live ranges: the compiler may not carry LDS values in registers across rows
+        o.append("    asm volatile(\"\" ::: \"memory\");\n")
+    o.append("  }\n")
+    o.append("  template <class A> static __device__ __forceinline__ void ldl_solve(const A& L, float* x) {\n")
+    for k in range(nv - 1, -1, -1):
+        for i in _ancestors(m, k, False):
+            o.append(f"    x[{i}] -= L[{adr[k, i]}] * x[{k}];\n")
+    for k in range(nv):
+        o.append(f"    x[{k}] = x[{k}] / L[{adr[k, k]}];\n")
+    for k in range(nv):
+        for i in _ancestors(m, k, False):
+            o.append(f"    x[{k}] -= L[{adr[k, i]}] * x[{i}];\n")
+    o.append("  }\n")
+    o.append("  template <class A> static __device__ __forceinline__ void mul_sym(const A& M, const float* x, float* y) {\n")
+    for i in range(nv):
+        o.append(f"    y[{i}] = 0.0f;\n")
+    for i in range(nv):
+        for j in sorted(_ancestors(m, i, True)):
+            if j == i:
+                o.append(f"    y[{i}] += M[{adr[i, i]}] * x[{i}];\n")
+            else:
+                o.append(f"    {{ const float v = M[{adr[i, j]}]; y[{i}] += v * x[{j}]; y[{j}] += v * x[{i}]; }}\n")
+    o.append("  }\n")
+    return "".join(o)
+
+
+def model_header(m: Model, variant: str) -> str:
+    nb, nv, nq, nu, nj = m.nbody, m.nv, m.nq, m.nu, m.njnt
+    rows, adr, nm = sparse_pattern(m)
+    # chains: for each body, its dof ancestors (ordered increasing)
+    chain = []
+    for b in range(nb):
+        wb = m.body_weldid[b]
+        c = []
+        if wb > 0:
+            j = m.body_dofadr[wb] + m.body_dofnum[wb] - 1
+            while j >= 0:
+                c.append(j)
+                j = m.dof_parentid[j]
+        chain.append(sorted(c))
+    maxchain = max(len(c) for c in chain)
+    chain_arr = np.full((nb, maxchain), -1)
+    for b, c in enumerate(chain):
+        chain_arr[b, :len(c)] = c
+    hull = m.hulls[0]
+    floor = m.id("geom", "floor")
+    lfoot = m.id("geom", "left_foot_bottom_tpu")
+    rfoot = m.id("geom", "right_foot_bottom_tpu")
+    body_imat = np.array([quat2mat(q) for q in m.body_iquat])
+    site_mat = np.array([quat2mat(q) for q in m.site_quat])
+    geom_mat = np.array([quat2mat(q) for q in m.geom_quat])
+    free = [j for j in range(nj) if m.jnt_type[j] == JNT_FREE]
+    assert free == [0] and m.body_jntadr[1] == 0, "kernel assumes body 1 carries the free joint"
+    for j in range(nj):
+        if j not in free:
+            assert np.allclose(m.jnt_pos[j], 0), "kernel assumes hinge anchors at the body origin"
+            assert np.allclose(m.jnt_axis[j], m.jnt_axis[m.body_jntadr[m.jnt_bodyid[j]]]), "same-axis joints per body"
+    assert m.nsite <= 8 and len(m.hulls) == 1
+    hc = hull.vert.mean(axis=0)
+    hr = float(np.max(np.linalg.norm(hull.vert - hc, axis=1)))
+    pre = f"DuckModel_{variant}"
+    dev = [f"__device__ const float {pre}_hull_vert_d[{len(hull.vert)}][3] = {_arr('x', hull.vert, 'float').split('= ', 1)[1]}",
+           f"__device__ const float {pre}_hull_face_normal_d[{len(hull.face_normal)}][3] = {_arr('x', hull.face_normal, 'float').split('= ', 1)[1]}",
+           f"__device__ const float {pre}_hull_face_offset_d[{len(hull.face_offset)}] = {_arr('x', hull.face_offset, 'float').split('= ', 1)[1]}",
+           f"__device__ const int {pre}_hull_edge_d[{len(hull.edge)}][2] = {_arr('x', hull.edge, 'int').split('= ', 1)[1]}",
+           f"__device__ const int {pre}_chain_d[{nb}][{maxchain}] = {_arr('x', chain_arr, 'int').split('= ', 1)[1]}"]
+    acc = [f"  static __device__ __forceinline__ const float (*hull_vert_d())[3] {{ return {pre}_hull_vert_d; }}\n",
+           f"  static __device__ __forceinline__ const float (*hull_face_normal_d())[3] {{ return {pre}_hull_face_normal_d; }}\n",
+           f"  static __device__ __forceinline__ const float* hull_face_offset_d() {{ return {pre}_hull_face_offset_d; }}\n",
+           f"  static __device__ __forceinline__ const int (*hull_edge_d())[2] {{ return {pre}_hull_edge_d; }}\n",
+           f"  static __device__ __forceinline__ const int (*chain_d())[{maxchain}] {{ return {pre}_chain_d; }}\n"]
+    out = [f"// generated by open_duck_playground_amd/codegen.py from assets/{m.name} — do not edit\n",
+           "#pragma once\n\n"] + dev + [
+           f"struct DuckModel_{variant} {{\n"] + acc + [
+           f"  static constexpr int NB = {nb}, NQ = {nq}, NV = {nv}, NU = {nu}, NJ = {nj}, NSITE = {m.nsite};\n",
+           f"  static constexpr int NM = {nm}, MAXCHAIN = {maxchain}, NSENSORDATA = {m.nsensordata};\n",
+           f"  static constexpr int NHV = {len(hull.vert)}, NHF = {len(hull.face_normal)}, NHE = {len(hull.edge)};\n",
+           f"  static constexpr int FLOOR_GEOM = {floor}, LFOOT_GEOM = {lfoot}, RFOOT_GEOM = {rfoot};\n",
+           f"  static constexpr int LFOOT_BODY = {m.geom_bodyid[lfoot]}, RFOOT_BODY = {m.geom_bodyid[rfoot]};\n",
+           f"  static constexpr int FLOOR_TYPE = {m.geom_type[floor]};\n",
+           f"  static constexpr float timestep = {_f(m.opt_timestep)}, impratio = {_f(m.opt_impratio)};\n",
+           f"  static constexpr float tolerance = {_f(m.opt_tolerance)}, ls_tolerance = {_f(m.opt_ls_tolerance)};\n",
+           f"  static constexpr float meaninertia = {_f(m.stat_meaninertia)};\n",
+           f"  static constexpr int iterations = {m.opt_iterations}, ls_iterations = {m.opt_ls_iterations};\n",
+           f"  static constexpr float hull_radius = {_f(hr)};\n",
+           ]
+    out.append(_arr("gravity", m.opt_gravity, "float"))
+    out.append(_arr("hull_center", hc, "float"))
+    for name in ("body_parentid", "body_jntnum", "body_jntadr", "body_dofnum", "body_dofadr", "body_weldid"):
+        out.append(_arr(name, m.arrays[name], "int"))
+    for name in ("body_pos", "body_quat", "body_ipos", "body_mass", "body_inertia", "body_invweight0"):
+        out.append(_arr(name, m.arrays[name], "float"))
+    out.append(_arr("body_imat", body_imat.reshape(nb, 9), "float"))
+    for name in ("jnt_type", "jnt_qposadr", "jnt_dofadr", "jnt_bodyid", "jnt_limited"):
+        out.append(_arr(name, m.arrays[name], "int"))
+    for name in ("jnt_pos", "jnt_axis", "jnt_range", "jnt_margin", "jnt_solref", "jnt_solimp"):
+        out.append(_arr(name, m.arrays[name], "float"))
+    for name in ("dof_bodyid", "dof_jntid", "dof_parentid"):
+        out.append(_arr(name, m.arrays[name], "int"))
+    for name in ("dof_armature", "dof_damping", "dof_frictionloss", "dof_invweight0", "dof_solref", "dof_solimp"):
+        out.append(_arr(name, m.arrays[name], "float"))
+    out.append(_arr("qpos0", m.qpos0, "float"))
+    out.append(_arr("site_bodyid", m.site_bodyid, "int"))
+    out.append(_arr("site_pos", m.site_pos, "float"))
+    out.append(_arr("site_quat", m.site_quat, "float"))
+    out.append(_arr("site_mat", site_mat.reshape(-1, 9), "float"))
+    out.append(_arr("cgeom_body", m.geom_bodyid[[floor, lfoot, rfoot]], "int"))
+    out.append(_arr("geom_pos", m.geom_pos[[floor, lfoot, rfoot]], "float"))
+    out.append(_arr("geom_mat", geom_mat[[floor, lfoot, rfoot]].reshape(3, 9), "float"))
+    out.append(_arr("actuator_trnid", m.actuator_trnid, "int"))
+    for name in ("actuator_kp", "actuator_kv", "actuator_gear", "actuator_ctrlrange", "actuator_forcerange"):
+        out.append(_arr(name, m.arrays[name], "float"))
+    out.append(_arr("actuator_ctrllimited", m.actuator_ctrllimited, "int"))
+    out.append(_arr("actuator_forcelimited", m.actuator_forcelimited, "int"))
+    out.append(_arr("actuator_dof", [m.jnt_dofadr[j] for j in m.actuator_trnid], "int"))
+    out.append(_arr("actuator_qadr", [m.jnt_qposadr[j] for j in m.actuator_trnid], "int"))
+    out.append(f"  static constexpr int NSENSOR = {m.nsensor}, IMU_SITE = {m.id('site', 'imu')};\n")
+    out.append(f"  static constexpr int LFOOT_SITE = {m.id('site', 'left_foot')}, RFOOT_SITE = {m.id('site', 'right_foot')};\n")
+    acc_sites = [m.sensor_objid[i] for i in range(m.nsensor) if m.sensor_type[i] == 2]
+    assert all(m.site_bodyid[s] == 1 for s in acc_sites), "accelerometer must sit on the free body"
+    out.append(_arr("sensor_type", m.sensor_type, "int"))
+    out.append(_arr("sensor_objid", m.sensor_objid, "int"))
+    out.append(_arr("sensor_adr", m.sensor_adr, "int"))
+    # collision pairs in slot order: pair p -> contact slots 4p..4p+3
+    out.append(f"  static constexpr int NPAIR = {m.npair};\n")
+    out.append(_arr("pair_geom1", m.pair_geom1, "int"))
+    out.append(_arr("pair_geom2", m.pair_geom2, "int"))
+    out.append(_arr("pair_friction", m.pair_friction, "float"))
+    out.append(_arr("pair_solref", m.pair_solref, "float"))
+    out.append(_arr("pair_solimp", m.pair_solimp, "float"))
+    out.append(_arr("pair_margin", m.pair_margin, "float"))
+    out.append(_arr("hull_vert", hull.vert, "float"))
+    out.append(_arr("hull_face_normal", hull.face_normal, "float"))
+    out.append(_arr("hull_face_offset", hull.face_offset, "float"))
+    out.append(_arr("hull_edge", hull.edge, "int"))
+    # sparse mass-matrix pattern
+    out.append(_arr("M_adr", adr, "int"))
+    out.append(_arr("M_rowlen", [len(r) for r in rows], "int"))
+    out.append(_arr("chain", chain_arr, "int"))
+    out.append(_arr("chain_len", [len(c) for c in chain], "int"))
+    fric = [i for i in range(nv) if m.dof_frictionloss[i] > 0]
+    lim = [j for j in range(nj) if m.jnt_limited[j]]
+    out.append(f"  static constexpr int NFRIC = {len(fric)}, NLIM = {len(lim)};\n")
+    out.append(_arr("fric_dof", fric, "int"))
+    out.append(_arr("lim_jnt", lim, "int"))
+    out.append(sparse_code(m, adr))
+    out.append("};\n")
+    return "".join(out)
+
+
+def main():
+    gen = os.path.join(HERE, "csrc", "generated")
+    os.makedirs(gen, exist_ok=True)
+    for variant, task in (("flat", "flat_terrain"), ("backlash", "flat_terrain_backlash")):
+        m = Model.load(os.path.join(HERE, "assets", f"{task}.npz"))
+        with open(os.path.join(gen, f"duck_model_{variant}.h"), "w") as f:
+            f.write(model_header(m, variant))
+
+
+if __name__ == "__main__":
+    main()

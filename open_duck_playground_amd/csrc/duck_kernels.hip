@@ -1,0 +1,752 @@
+// duck_kernels.hip — Joystick env kernels + C ABI (include/duck.h) for MI355X (gfx950).
+//
+// One env per lane; one launch per env-step runs the whole of Joystick.step
+// (joystick.py:323-481): imitation phase + reference motion, action delay, push,
+// motor-target rate limit, 10 fused physics substeps (duck_physics.h), contacts, obs,
+// termination, rewards, info bookkeeping, and (optionally) the training wrappers
+// EpisodeWrapper + BraxAutoResetWrapper. Per-env state never leaves the lane between
+// substeps; HBM sees one coalesced read and one write of the state per env-step.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../include/duck.h"
+#include "duck_physics.h"
+#include "generated/duck_model_backlash.h"
+#include "generated/duck_model_flat.h"
+
+#define DUCK_VERSION 100  // 0.1.0
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHECK(x)                                                                      \
+  do {                                                                                   \
+    hipError_t _e = (x);                                                                 \
+    if (_e != hipSuccess) return fail(DUCK_EHIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// per-step RNG slot map (identical to oracle/duck_oracle.c)
+enum { SLOT_ACTION_DELAY = 0, SLOT_PUSH_THETA = 1, SLOT_PUSH_MAG = 2, SLOT_GYRO = 3, SLOT_ACCEL = 6,
+       SLOT_GRAVITY = 9, SLOT_IMU_IDX = 12, SLOT_QPOS = 13, SLOT_QVEL = 29, SLOT_CMD = 45 };
+enum { RSLOT_DXY = 0, RSLOT_YAW = 2, RSLOT_QSCALE = 3, RSLOT_QVEL = 19, RSLOT_CMD = 25, RSLOT_PUSH = 33,
+       RSLOT_OBS = 64 };
+#define KEY_TAG_ENV 0x5EEDu
+#define KEY_TAG_DR 0xD0D0u
+#define PI_F 3.14159265358979323846f
+
+struct RefMeta {
+  int n_dx, n_dy, n_dtheta, n_dim, n_coef, nb;
+  float dxs[16], dys[16], dthetas[16];
+  float dx_range[2], dy_range[2], dtheta_range[2];
+};
+
+struct KArgs {
+  int n;
+  float* fs;
+  int32_t* is;
+  const float* dr;
+  const float* action;
+  float* obs;
+  float* priv;
+  float* reward;
+  float* done;
+  float* scratch;
+  const uint8_t* mask;
+  uint64_t seed;
+  int64_t env_offset;
+  const float* frames;
+  RefMeta ref;
+  duck_env_config cfg;
+  duck_layout lay;
+  duck_dr_layout drl;
+};
+
+template <int WG>
+struct Col {  // SoA accessor for env e
+  float* p;
+  int n;
+  DK float& operator[](int k) const { return p[(size_t)k * n]; }
+};
+
+// PolyReferenceMotion.get_reference_motion (poly_reference_motion.py:148-168)
+DK int nearest(const float* g, int n, float v) {
+  int best = 0;
+  float bd = fabsf(g[0] - v);
+  for (int i = 1; i < 16; i++) {
+    if (i >= n) break;
+    const float d = fabsf(g[i] - v);
+    if (d < bd) { bd = d; best = i; }
+  }
+  return best;
+}
+DK void reference_motion(const KArgs& A, float dx, float dy, float dth, int i, float* out) {
+  const RefMeta& R = A.ref;
+  dx = fminf(fmaxf(dx, R.dx_range[0]), R.dx_range[1]);
+  dy = fminf(fmaxf(dy, R.dy_range[0]), R.dy_range[1]);
+  dth = fminf(fmaxf(dth, R.dtheta_range[0]), R.dtheta_range[1]);
+  const int ix = nearest(R.dxs, R.n_dx, dx), iy = nearest(R.dys, R.n_dy, dy), it = nearest(R.dthetas, R.n_dtheta, dth);
+  // t = (i % nb) / nb takes nb values: the table holds the polynomials pre-evaluated there
+  const int nb = R.nb;
+  const int ph = ((i % nb) + nb) % nb;
+  const float4* f = reinterpret_cast<const float4*>(
+      A.frames + ((size_t)((ix * R.n_dy + iy) * R.n_dtheta + it) * nb + ph) * 40);
+#pragma unroll
+  for (int d = 0; d < 10; d++) {
+    const float4 v = f[d];
+    out[4 * d] = v.x; out[4 * d + 1] = v.y; out[4 * d + 2] = v.z; out[4 * d + 3] = v.w;
+  }
+}
+
+DK float nan_to_num(float x) {
+  if (isnan(x)) return 0.0f;
+  if (isinf(x)) return x > 0 ? 3.4028234663852886e38f : -3.4028234663852886e38f;
+  return x;
+}
+
+DK void sample_command(const duck_env_config& c, const Rng& r, int slot, float* cmd) {
+  const float f = c.head_range_factor;
+  cmd[0] = r.uniform(slot + 0, c.lin_vel_x[0], c.lin_vel_x[1]);
+  cmd[1] = r.uniform(slot + 1, c.lin_vel_y[0], c.lin_vel_y[1]);
+  cmd[2] = r.uniform(slot + 2, c.ang_vel_yaw[0], c.ang_vel_yaw[1]);
+  cmd[3] = r.uniform(slot + 3, c.neck_pitch_range[0] * f, c.neck_pitch_range[1] * f);
+  cmd[4] = r.uniform(slot + 4, c.head_pitch_range[0] * f, c.head_pitch_range[1] * f);
+  cmd[5] = r.uniform(slot + 5, c.head_yaw_range[0] * f, c.head_yaw_range[1] * f);
+  cmd[6] = r.uniform(slot + 6, c.head_roll_range[0] * f, c.head_roll_range[1] * f);
+  if (r.u(slot + 7) < 0.1f)
+    for (int k = 0; k < 7; k++) cmd[k] = 0.0f;
+}
+
+// per-env model values: nominal (constexpr) or this env's domain-randomised record
+template <class Md, int WG>
+DK void load_dyn(const KArgs& A, int e, Slice<WG> L) {
+  using Ly = Lay<Md>;
+  Phys<Md, WG>::set_nominal(L);
+  if (A.dr) {
+    const duck_dr_layout& D = A.drl;
+    const int n = A.n;
+#pragma unroll
+    for (int k = 0; k < 3; k++) L[Ly::DIPOS + k] = A.dr[(size_t)(D.base_ipos + k) * n + e];
+#pragma unroll
+    for (int b = 0; b < Md::NB; b++) L[Ly::DMASS + b] = A.dr[(size_t)(D.body_mass + b) * n + e];
+#pragma unroll
+    for (int a = 0; a < Md::NU; a++) {
+      L[Ly::DFRIC + Md::actuator_dof[a]] = A.dr[(size_t)(D.frictionloss + a) * n + e];
+      L[Ly::DARM + Md::actuator_dof[a]] = A.dr[(size_t)(D.armature + a) * n + e];
+      L[Ly::DQ0 + Md::actuator_qadr[a]] = A.dr[(size_t)(D.qpos0 + a) * n + e];
+      L[Ly::DKP + a] = A.dr[(size_t)(D.kp + a) * n + e];
+    }
+  }
+}
+
+// Joystick._get_obs (joystick.py:487-620); reads the last forward's outputs from the slice
+template <class Md, int WG>
+DK void write_obs(const KArgs& A, int e, Slice<WG> L, const Rng& r, int slot_base,
+                                       int imitation_i) {
+  using Ly = Lay<Md>;
+  const duck_env_config& c = A.cfg;
+  const duck_layout& Lo = A.lay;
+  Col<0> F{A.fs + e, A.n};
+  constexpr int NU = Md::NU;
+  float gyro[3], acc[3], grav[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    gyro[k] = L[Ly::SENS + c.sens_gyro + k];
+    acc[k] = L[Ly::SENS + c.sens_accelerometer + k];
+    grav[k] = -L[Ly::IMUR + k];
+  }
+  float ngrav[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+    ngrav[k] = grav[k] + (2.0f * r.u(slot_base + SLOT_GRAVITY + k) - 1.0f) * c.noise_level * c.noise_gravity;
+  // IMU delay history (joystick.py:521-530); the delayed sample is never emitted
+#pragma unroll
+  for (int k = 8; k >= 3; k--) F[Lo.imu_history + k] = F[Lo.imu_history + k - 3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) F[Lo.imu_history + k] = ngrav[k];
+  float* obs = A.obs + (size_t)e * Lo.obs_size;
+  float* priv = A.priv + (size_t)e * Lo.priv_size;
+  int o = 0;
+  auto put = [&](float v) { obs[o] = v; priv[o] = v; o++; };
+#pragma unroll
+  for (int k = 0; k < 3; k++) put(gyro[k] + (2.0f * r.u(slot_base + SLOT_GYRO + k) - 1.0f) * c.noise_level * c.noise_gyro);
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+    put(acc[k] + (2.0f * r.u(slot_base + SLOT_ACCEL + k) - 1.0f) * c.noise_level * c.noise_accelerometer);
+#pragma unroll
+  for (int k = 0; k < 7; k++) put(F[Lo.command + k]);
+  for (int a = 0; a < NU; a++) {
+    float ja = L[Ly::QPOS + c.actuator_qposadr[a]];
+    if (c.backlash_qposadr[a] >= 0) ja += L[Ly::QPOS + c.backlash_qposadr[a]];
+    put(ja + (2.0f * r.u(slot_base + SLOT_QPOS + a) - 1.0f) * c.noise_level * c.qpos_noise_scale[a] - c.default_actuator[a]);
+  }
+  for (int a = 0; a < NU; a++) {
+    const float jv = L[Ly::QVEL + c.actuator_qveladr[a]];
+    put((jv + (2.0f * r.u(slot_base + SLOT_QVEL + a) - 1.0f) * c.noise_level * c.noise_joint_vel) * c.dof_vel_scale);
+  }
+  for (int a = 0; a < NU; a++) put(F[Lo.last_act + a]);
+  for (int a = 0; a < NU; a++) put(F[Lo.last_last_act + a]);
+  for (int a = 0; a < NU; a++) put(F[Lo.last_last_last_act + a]);
+  for (int a = 0; a < NU; a++) put(F[Lo.motor_targets + a]);
+  put(L[Ly::OCON]);
+  put(L[Ly::OCON + 1]);
+  put(F[Lo.imitation_phase]);
+  put(F[Lo.imitation_phase + 1]);
+  int p = o;
+  auto pp = [&](float v) { priv[p++] = v; };
+#pragma unroll
+  for (int k = 0; k < 3; k++) pp(gyro[k]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) pp(acc[k]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) pp(grav[k]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) pp(L[Ly::SENS + c.sens_local_linvel + k]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) pp(L[Ly::SENS + c.sens_global_angvel + k]);
+  for (int a = 0; a < NU; a++) {
+    float ja = L[Ly::QPOS + c.actuator_qposadr[a]];
+    if (c.backlash_qposadr[a] >= 0) ja += L[Ly::QPOS + c.backlash_qposadr[a]];
+    pp(ja - c.default_actuator[a]);
+  }
+  for (int a = 0; a < NU; a++) pp(L[Ly::QVEL + c.actuator_qveladr[a]]);
+  pp(L[Ly::QPOS + 2]);
+  for (int a = 0; a < NU; a++) pp(L[Ly::AF + a]);
+  pp(L[Ly::OCON]);
+  pp(L[Ly::OCON + 1]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) pp(L[Ly::SENS + c.sens_left_foot_linvel + k]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) pp(L[Ly::SENS + c.sens_right_foot_linvel + k]);
+  pp(F[Lo.feet_air_time]);
+  pp(F[Lo.feet_air_time + 1]);
+  if (Lo.imitation)
+    for (int k = 0; k < 40; k++) pp(F[Lo.ref_motion + k]);
+  pp((float)imitation_i);
+  pp(F[Lo.imitation_phase]);
+  pp(F[Lo.imitation_phase + 1]);
+}
+
+template <class Md, int WG>
+__global__ void __launch_bounds__(WG) reset_kernel(KArgs A) {
+  using Ly = Lay<Md>;
+  const int e = blockIdx.x * WG + threadIdx.x;
+  if (e >= A.n) return;
+  if (A.mask && !A.mask[e]) return;
+  extern __shared__ float lds[];
+  Slice<WG> L{lds + threadIdx.x};
+  const duck_env_config& c = A.cfg;
+  const duck_layout& Lo = A.lay;
+  constexpr int NQ = Md::NQ, NV = Md::NV, NU = Md::NU;
+  Col<0> F{A.fs + e, A.n};
+  auto iset = [&](int k, int32_t v) { A.is[(size_t)k * A.n + e] = v; };
+  for (int k = 0; k < Lo.nfloat; k++) F[k] = 0.0f;
+  for (int k = 0; k < Lo.nint; k++) iset(k, 0);
+  Rng r;
+  derive_key(A.seed, A.env_offset + e, KEY_TAG_ENV, r.k0, r.k1);
+  r.ctr = 0;
+  load_dyn<Md, WG>(A, e, L);
+  // Joystick.reset (joystick.py:206-258)
+  for (int i = 0; i < NQ; i++) L[Ly::QPOS + i] = c.init_qpos[i];
+  for (int i = 0; i < NV; i++) { L[Ly::QVEL + i] = 0.0f; L[Ly::WARM + i] = 0.0f; }
+  L[Ly::QPOS + 0] += r.uniform(RSLOT_DXY + 0, -0.05f, 0.05f);
+  L[Ly::QPOS + 1] += r.uniform(RSLOT_DXY + 1, -0.05f, 0.05f);
+  {
+    const float yaw = r.uniform(RSLOT_YAW, -3.14f, 3.14f);
+    float s, co;
+    sincosf(0.5f * yaw, &s, &co);
+    const float qy[4] = {co, 0.0f, 0.0f, s};
+    float q[4] = {L[Ly::QPOS + 3], L[Ly::QPOS + 4], L[Ly::QPOS + 5], L[Ly::QPOS + 6]};
+    qmul(q, q, qy);
+    for (int k = 0; k < 4; k++) L[Ly::QPOS + 3 + k] = q[k];
+  }
+  for (int a = 0; a < NU; a++) L[Ly::QPOS + c.actuator_qposadr[a]] *= r.uniform(RSLOT_QSCALE + a, 0.5f, 1.5f);
+  for (int k = 0; k < 6; k++) L[Ly::QVEL + k] = r.uniform(RSLOT_QVEL + k, -0.05f, 0.05f);
+  for (int a = 0; a < NU; a++) L[Ly::CTRL + a] = L[Ly::QPOS + c.actuator_qposadr[a]];
+  Phys<Md, WG>::step(L, false, true, nullptr, 0, A.scratch ? A.scratch + e : nullptr, A.n);
+  float cmd[7];
+  sample_command(c, r, RSLOT_CMD, cmd);
+  const float push_interval = r.uniform(RSLOT_PUSH, c.push_interval_range[0], c.push_interval_range[1]);
+  iset(Lo.push_interval, (int32_t)rintf(push_interval / c.ctrl_dt));
+  iset(Lo.rng_key, (int32_t)r.k0);
+  iset(Lo.rng_key + 1, (int32_t)r.k1);
+  iset(Lo.rng_ctr, 1);
+  for (int k = 0; k < 7; k++) F[Lo.command + k] = cmd[k];
+  for (int a = 0; a < NU; a++) F[Lo.motor_targets + a] = c.default_actuator[a];
+  if (Lo.imitation) {
+    float ref[40];
+    reference_motion(A, cmd[0], cmd[1], cmd[2], 0, ref);
+    for (int k = 0; k < 40; k++) F[Lo.ref_motion + k] = ref[k];
+  }
+  for (int i = 0; i < NQ; i++) { F[Lo.qpos + i] = L[Ly::QPOS + i]; F[Lo.first_qpos + i] = L[Ly::QPOS + i]; }
+  for (int i = 0; i < NV; i++) {
+    F[Lo.qvel + i] = L[Ly::QVEL + i]; F[Lo.first_qvel + i] = L[Ly::QVEL + i];
+    F[Lo.qacc_warmstart + i] = L[Ly::WARM + i]; F[Lo.first_qacc_warmstart + i] = L[Ly::WARM + i];
+  }
+  for (int a = 0; a < NU; a++) { F[Lo.ctrl + a] = L[Ly::CTRL + a]; F[Lo.first_ctrl + a] = L[Ly::CTRL + a]; }
+  write_obs<Md, WG>(A, e, L, r, RSLOT_OBS, 0);
+  for (int k = 0; k < Lo.obs_size; k++) F[Lo.first_obs + k] = A.obs[(size_t)e * Lo.obs_size + k];
+  for (int k = 0; k < Lo.priv_size; k++) F[Lo.first_priv + k] = A.priv[(size_t)e * Lo.priv_size + k];
+}
+
+template <class Md, int WG>
+__global__ void __launch_bounds__(WG) step_kernel(KArgs A) {
+  using Ly = Lay<Md>;
+  const int e = blockIdx.x * WG + threadIdx.x;
+  if (e >= A.n) return;
+  extern __shared__ float lds[];
+  Slice<WG> L{lds + threadIdx.x};
+  const duck_env_config& c = A.cfg;
+  const duck_layout& Lo = A.lay;
+  constexpr int NQ = Md::NQ, NV = Md::NV, NU = Md::NU;
+  const int n = A.n;
+  Col<0> F{A.fs + e, n};
+  auto iget = [&](int k) { return A.is[(size_t)k * n + e]; };
+  auto iset = [&](int k, int32_t v) { A.is[(size_t)k * n + e] = v; };
+  const float dt = c.ctrl_dt;
+  int ep_steps = iget(Lo.ep_steps);
+  if (c.auto_reset && F[Lo.done] != 0.0f) ep_steps = 0;
+  Rng r;
+  r.k0 = (uint32_t)iget(Lo.rng_key);
+  r.k1 = (uint32_t)iget(Lo.rng_key + 1);
+  r.ctr = (uint32_t)iget(Lo.rng_ctr);
+  int imitation_i = iget(Lo.imitation_i);
+  if (Lo.imitation) {  // joystick.py:325-355
+    const int nb = A.ref.nb;
+    imitation_i = (imitation_i + 1) % nb;
+    const float ph = ((float)imitation_i / (float)nb) * 2.0f * PI_F;
+    F[Lo.imitation_phase] = cosf(ph);
+    F[Lo.imitation_phase + 1] = sinf(ph);
+    float ref[40];
+    reference_motion(A, F[Lo.command], F[Lo.command + 1], F[Lo.command + 2], imitation_i, ref);
+    for (int k = 0; k < 40; k++) F[Lo.ref_motion + k] = ref[k];
+  } else {
+    imitation_i = 0;
+  }
+  // action delay (joystick.py:362-376): history = [a_t, a_{t-1}, a_{t-2}]
+  const int didx = r.randint(SLOT_ACTION_DELAY, c.action_min_delay, c.action_max_delay);
+  float arate = 0.0f;
+  for (int a = 0; a < NU; a++) {
+    const float act = A.action[(size_t)e * NU + a];
+    const float h1 = F[Lo.action_history + a], h2 = F[Lo.action_history + NU + a];
+    F[Lo.action_history + a] = act;
+    F[Lo.action_history + NU + a] = h1;
+    F[Lo.action_history + 2 * NU + a] = h2;
+    const float ad = didx == 0 ? act : (didx == 1 ? h1 : h2);
+    float mt = c.default_actuator[a] + ad * c.action_scale;  // joystick.py:404-417
+    if (c.use_motor_speed_limits) {
+      const float prev = F[Lo.motor_targets + a], lim = c.max_motor_velocity * dt;
+      mt = fminf(fmaxf(mt, prev - lim), prev + lim);
+    }
+    L[Ly::CTRL + a] = mt;
+    const float la = F[Lo.last_act + a];
+    arate += (act - la) * (act - la);
+  }
+  // push (joystick.py:381-400)
+  const float theta = r.uniform(SLOT_PUSH_THETA, 0.0f, 2.0f * PI_F);
+  const float mag = r.uniform(SLOT_PUSH_MAG, c.push_magnitude_range[0], c.push_magnitude_range[1]);
+  const int push_step = iget(Lo.push_step), push_interval = iget(Lo.push_interval);
+  const float gate = ((push_step + 1) % push_interval == 0) ? 1.0f : 0.0f;
+  const float push[2] = {cosf(theta) * gate * (float)c.push_enable, sinf(theta) * gate * (float)c.push_enable};
+  for (int i = 0; i < NQ; i++) L[Ly::QPOS + i] = F[Lo.qpos + i];
+  for (int i = 0; i < NV; i++) { L[Ly::QVEL + i] = F[Lo.qvel + i]; L[Ly::WARM + i] = F[Lo.qacc_warmstart + i]; }
+  L[Ly::QVEL + 0] += push[0] * mag;
+  L[Ly::QVEL + 1] += push[1] * mag;
+  load_dyn<Md, WG>(A, e, L);
+  // physics (joystick.py:420)
+  float* scr = A.scratch ? A.scratch + e : nullptr;
+  for (int s = 0; s < c.n_substeps; s++) Phys<Md, WG>::step(L, true, s == c.n_substeps - 1, nullptr, 0, scr, n);
+  for (int a = 0; a < NU; a++) { F[Lo.motor_targets + a] = L[Ly::CTRL + a]; F[Lo.ctrl + a] = L[Ly::CTRL + a]; }
+  const float con[2] = {L[Ly::OCON], L[Ly::OCON + 1]};
+  // feet bookkeeping (joystick.py:424-435)
+  for (int k = 0; k < 2; k++) {
+    F[Lo.feet_air_time + k] = F[Lo.feet_air_time + k] + dt;
+    F[Lo.swing_peak + k] = fmaxf(F[Lo.swing_peak + k], L[Ly::FOOTZ + k]);
+  }
+  write_obs<Md, WG>(A, e, L, r, 0, imitation_i);
+  // termination (joystick.py:483-485)
+  bool nan = false;
+  for (int i = 0; i < NQ; i++) nan = nan || isnan(L[Ly::QPOS + i]);
+  for (int i = 0; i < NV; i++) nan = nan || isnan(L[Ly::QVEL + i]);
+  float done = (L[Ly::SENS + c.sens_upvector + 2] < 0.0f || nan) ? 1.0f : 0.0f;
+  // rewards (joystick.py:622-669, common/rewards.py:11-125, custom_rewards.py:4-148)
+  float cmd[7];
+  for (int k = 0; k < 7; k++) cmd[k] = F[Lo.command + k];
+  const float lv0 = L[Ly::SENS + c.sens_local_linvel], lv1 = L[Ly::SENS + c.sens_local_linvel + 1];
+  const float gz = L[Ly::SENS + c.sens_gyro + 2];
+  const float sigma = c.tracking_sigma;
+  const float ex = (cmd[0] - lv0) * (cmd[0] - lv0);
+  const float ey = fmaxf(fabsf(lv1 - cmd[1]) - 0.1f, 0.0f);
+  const float r_lin = nan_to_num(expf(-(ex + ey * ey) / sigma));
+  const float r_ang = nan_to_num(expf(-((cmd[2] - gz) * (cmd[2] - gz)) / sigma));
+  float torq = 0.0f, pc = 0.0f, vc = 0.0f;
+  for (int a = 0; a < NU; a++) {
+    const float f = L[Ly::AF + a];
+    torq += f * f;
+    pc += fabsf(L[Ly::QPOS + c.actuator_qposadr[a]] - c.default_actuator[a]);
+    vc += fabsf(L[Ly::QVEL + c.actuator_qveladr[a]]);
+  }
+  const float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1] + cmd[2] * cmd[2]);
+  const float r_still = nan_to_num(pc + vc) * (cn < 0.01f ? 1.0f : 0.0f);
+  float imit = 0.0f;
+  if (Lo.imitation) {
+    const int R0 = Lo.ref_motion;
+    float lxy = 0.0f, axy = 0.0f;
+    for (int k = 0; k < 2; k++) {
+      const float dv = L[Ly::QVEL + k] - F[R0 + 34 + k], dw = L[Ly::QVEL + 3 + k] - F[R0 + 37 + k];
+      lxy += dv * dv;
+      axy += dw * dw;
+    }
+    const float dz = L[Ly::QVEL + 2] - F[R0 + 36], dwz = L[Ly::QVEL + 5] - F[R0 + 39];
+    const float lin_xy = expf(-8.0f * lxy), lin_z = expf(-8.0f * dz * dz);
+    const float ang_xy = expf(-2.0f * axy) * 0.5f, ang_z = expf(-2.0f * dwz * dwz) * 0.5f;
+    float jp = 0.0f, jv = 0.0f;
+    for (int k = 0; k < 5; k++) {
+      const float q1 = L[Ly::QPOS + c.actuator_qposadr[k]] - F[R0 + k];
+      const float q2 = L[Ly::QPOS + c.actuator_qposadr[NU - 5 + k]] - F[R0 + 11 + k];
+      const float v1 = L[Ly::QVEL + c.actuator_qveladr[k]] - F[R0 + 16 + k];
+      const float v2 = L[Ly::QVEL + c.actuator_qveladr[NU - 5 + k]] - F[R0 + 27 + k];
+      jp += q1 * q1 + q2 * q2;
+      jv += v1 * v1 + v2 * v2;
+    }
+    float contact_r = 0.0f;
+    for (int k = 0; k < 2; k++) contact_r += (con[k] == (F[R0 + 32 + k] > 0.5f ? 1.0f : 0.0f)) ? 1.0f : 0.0f;
+    float rr = lin_xy + lin_z + ang_xy + ang_z + (-jp * 15.0f) + (-jv * 1e-3f) + contact_r;
+    rr *= cn > 0.01f ? 1.0f : 0.0f;
+    imit = nan_to_num(rr);
+  }
+  const float terms[7] = {r_lin * c.scale_tracking_lin_vel, r_ang * c.scale_tracking_ang_vel,
+                          nan_to_num(torq) * c.scale_torques, nan_to_num(arate) * c.scale_action_rate,
+                          1.0f * c.scale_alive, imit * c.scale_imitation, r_still * c.scale_stand_still};
+  float sum = 0.0f;
+  for (int k = 0; k < 7; k++) sum += terms[k];
+  const float reward = fminf(fmaxf(sum * dt, 0.0f), 10000.0f);
+  // info bookkeeping (joystick.py:449-477)
+  F[Lo.push] = push[0];
+  F[Lo.push + 1] = push[1];
+  int step = iget(Lo.step) + 1;
+  iset(Lo.push_step, push_step + 1);
+  for (int a = 0; a < NU; a++) {
+    F[Lo.last_last_last_act + a] = F[Lo.last_last_act + a];
+    F[Lo.last_last_act + a] = F[Lo.last_act + a];
+    F[Lo.last_act + a] = A.action[(size_t)e * NU + a];
+  }
+  if (step > 500) {
+    float nc[7];
+    sample_command(c, r, SLOT_CMD, nc);
+    for (int k = 0; k < 7; k++) F[Lo.command + k] = nc[k];
+  }
+  if (done != 0.0f || step > 500) step = 0;
+  iset(Lo.step, step);
+  iset(Lo.imitation_i, imitation_i);
+  for (int k = 0; k < 2; k++) {
+    F[Lo.feet_air_time + k] = F[Lo.feet_air_time + k] * (con[k] != 0.0f ? 0.0f : 1.0f);
+    F[Lo.last_contact + k] = con[k];
+    F[Lo.swing_peak + k] = F[Lo.swing_peak + k] * (con[k] != 0.0f ? 0.0f : 1.0f);
+  }
+  const float scales[7] = {c.scale_tracking_lin_vel, c.scale_tracking_ang_vel, c.scale_torques, c.scale_action_rate,
+                           c.scale_alive, c.scale_imitation, c.scale_stand_still};
+  for (int k = 0; k < 7; k++) F[Lo.metrics + k] = scales[k] > 0.0f ? terms[k] : -terms[k];
+  F[Lo.metrics + DUCK_M_SWING_PEAK] = 0.5f * (F[Lo.swing_peak] + F[Lo.swing_peak + 1]);
+  iset(Lo.rng_ctr, (int32_t)(r.ctr + 1));
+  // training wrappers: EpisodeWrapper + BraxAutoResetWrapper
+  float trunc = 0.0f;
+  bool restore = false;
+  if (c.auto_reset) {
+    ep_steps += 1;
+    if (ep_steps >= c.episode_length) { trunc = 1.0f - done; done = 1.0f; }
+    restore = done != 0.0f;
+    iset(Lo.ep_steps, ep_steps);
+  }
+  if (restore) {
+    for (int i = 0; i < NQ; i++) F[Lo.qpos + i] = F[Lo.first_qpos + i];
+    for (int i = 0; i < NV; i++) { F[Lo.qvel + i] = F[Lo.first_qvel + i]; F[Lo.qacc_warmstart + i] = F[Lo.first_qacc_warmstart + i]; }
+    for (int a = 0; a < NU; a++) F[Lo.ctrl + a] = F[Lo.first_ctrl + a];
+    for (int k = 0; k < Lo.obs_size; k++) A.obs[(size_t)e * Lo.obs_size + k] = F[Lo.first_obs + k];
+    for (int k = 0; k < Lo.priv_size; k++) A.priv[(size_t)e * Lo.priv_size + k] = F[Lo.first_priv + k];
+  } else {
+    for (int i = 0; i < NQ; i++) F[Lo.qpos + i] = L[Ly::QPOS + i];
+    for (int i = 0; i < NV; i++) { F[Lo.qvel + i] = L[Ly::QVEL + i]; F[Lo.qacc_warmstart + i] = L[Ly::WARM + i]; }
+  }
+  F[Lo.reward] = reward;
+  F[Lo.done] = done;
+  F[Lo.truncation] = trunc;
+  A.reward[e] = reward;
+  A.done[e] = done;
+}
+
+template <class Md, int WG>
+__global__ void __launch_bounds__(WG) physics_kernel(KArgs A, float* qpos_g, float* qvel_g, float* warm_g,
+                                                     const float* ctrl_g, int nsub, float* aux) {
+  using Ly = Lay<Md>;
+  const int e = blockIdx.x * WG + threadIdx.x;
+  const int n = A.n;
+  if (e >= n) return;
+  extern __shared__ float lds[];
+  Slice<WG> L{lds + threadIdx.x};
+  for (int i = 0; i < Md::NQ; i++) L[Ly::QPOS + i] = qpos_g[(size_t)i * n + e];
+  for (int i = 0; i < Md::NV; i++) { L[Ly::QVEL + i] = qvel_g[(size_t)i * n + e]; L[Ly::WARM + i] = warm_g[(size_t)i * n + e]; }
+  for (int a = 0; a < Md::NU; a++) L[Ly::CTRL + a] = ctrl_g[(size_t)a * n + e];
+  load_dyn<Md, WG>(A, e, L);
+  float* ax = aux ? aux + e : nullptr;
+  float* scr = A.scratch ? A.scratch + e : nullptr;
+  if (nsub == 0) {
+    Phys<Md, WG>::step(L, false, true, ax, n, scr, n);
+  } else {
+    for (int s = 0; s < nsub; s++) Phys<Md, WG>::step(L, true, s == nsub - 1, ax, n, scr, n);
+  }
+  for (int i = 0; i < Md::NQ; i++) qpos_g[(size_t)i * n + e] = L[Ly::QPOS + i];
+  for (int i = 0; i < Md::NV; i++) { qvel_g[(size_t)i * n + e] = L[Ly::QVEL + i]; warm_g[(size_t)i * n + e] = L[Ly::WARM + i]; }
+}
+
+// domain_randomize (randomize.py:39-106), absolute randomised values per env
+template <class Md>
+__global__ void randomize_kernel(int n, float* dr, duck_dr_layout D, uint64_t seed, int64_t env_offset) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  Rng r;
+  derive_key(seed, env_offset + e, KEY_TAG_DR, r.k0, r.k1);
+  r.ctr = 0;
+  int slot = 0;
+  auto W = [&](int k, float v) { dr[(size_t)k * n + e] = v; };
+  W(D.floor_friction, r.uniform(slot++, 0.5f, 1.0f));
+  float fl[Md::NU], arm[Md::NU], ip[3], ms[Md::NB], q0[Md::NU], kp[Md::NU];
+  for (int a = 0; a < Md::NU; a++) fl[a] = r.uniform(slot++, 0.9f, 1.1f);
+  for (int a = 0; a < Md::NU; a++) arm[a] = r.uniform(slot++, 1.0f, 1.05f);
+  for (int k = 0; k < 3; k++) ip[k] = r.uniform(slot++, -0.05f, 0.05f);
+  for (int b = 0; b < Md::NB; b++) ms[b] = r.uniform(slot++, 0.9f, 1.1f);
+  const float dmass = r.uniform(slot++, -0.1f, 0.1f);
+  for (int a = 0; a < Md::NU; a++) q0[a] = r.uniform(slot++, -0.03f, 0.03f);
+  for (int a = 0; a < Md::NU; a++) kp[a] = r.uniform(slot++, 0.9f, 1.1f);
+  for (int a = 0; a < Md::NU; a++) {
+    W(D.frictionloss + a, fl[a] * Md::dof_frictionloss[Md::actuator_dof[a]]);
+    W(D.armature + a, arm[a] * Md::dof_armature[Md::actuator_dof[a]]);
+    W(D.qpos0 + a, q0[a] + Md::qpos0[Md::actuator_qadr[a]]);
+    W(D.kp + a, kp[a] * Md::actuator_kp[a]);
+  }
+  for (int k = 0; k < 3; k++) W(D.base_ipos + k, ip[k] + Md::body_ipos[1][k]);
+  for (int b = 0; b < Md::NB; b++) W(D.body_mass + b, ms[b] * Md::body_mass[b] + (b == 1 ? dmass : 0.0f));
+}
+
+// --------------------------------------------------------------------------------------
+// host side
+// --------------------------------------------------------------------------------------
+enum Variant { V_FLAT = 0, V_BACKLASH = 1 };
+constexpr int WG = 16;  // one 16-lane wave per workgroup: 4096 envs fill all 256 CUs
+
+struct duck_sim {
+  int device;
+  Variant variant;
+  duck_env_config cfg;
+  duck_layout lay;
+  duck_dr_layout drl;
+  RefMeta ref;
+  float* frames_d;
+  int nq, nv, nu;
+};
+
+template <class Md>
+static bool matches(const duck_model_desc* m) {
+  if (m->nq != Md::NQ || m->nv != Md::NV || m->nu != Md::NU || m->nbody != Md::NB || m->njnt != Md::NJ) return false;
+  if (m->npair != Md::NPAIR || m->hull_nvert != Md::NHV) return false;
+  auto close = [](double a, float b) { return fabs(a - (double)b) <= 1e-6 * (1.0 + fabs(a)); };
+  for (int b = 0; b < Md::NB; b++) {
+    if (m->body_parentid[b] != Md::body_parentid[b]) return false;
+    if (!close(m->body_mass[b], Md::body_mass[b])) return false;
+    for (int k = 0; k < 3; k++)
+      if (!close(m->body_pos[3 * b + k], Md::body_pos[b][k])) return false;
+  }
+  for (int a = 0; a < Md::NU; a++)
+    if (!close(m->actuator_kp[a], Md::actuator_kp[a])) return false;
+  for (int p = 0; p < Md::NPAIR; p++)
+    if (m->pair_geom1[p] != Md::pair_geom1[p] || m->pair_geom2[p] != Md::pair_geom2[p] ||
+        !close(m->pair_friction[5 * p], Md::pair_friction[p][0]))
+      return false;
+  if (m->geom_type[m->pair_geom1[1]] != 0) return false;  // plane floor (hfield: not yet supported)
+  return true;
+}
+
+template <class Md>
+static size_t lds_bytes() {
+  return (size_t)Lay<Md>::TOTAL * WG * sizeof(float);
+}
+
+static KArgs make_args(duck_sim* s, int n) {
+  KArgs A;
+  memset(&A, 0, sizeof(A));
+  A.n = n;
+  A.cfg = s->cfg;
+  A.lay = s->lay;
+  A.drl = s->drl;
+  A.ref = s->ref;
+  A.frames = s->frames_d;
+  return A;
+}
+
+template <class Md>
+static int launch_reset(duck_sim* s, KArgs& A, hipStream_t st) {
+  const dim3 grid((A.n + WG - 1) / WG), block(WG);
+  hipLaunchKernelGGL((reset_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A);
+  HIPCHECK(hipGetLastError());
+  return DUCK_OK;
+}
+
+template <class Md>
+static int launch_step(duck_sim* s, KArgs& A, hipStream_t st) {
+  const dim3 grid((A.n + WG - 1) / WG), block(WG);
+  hipLaunchKernelGGL((step_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A);
+  HIPCHECK(hipGetLastError());
+  return DUCK_OK;
+}
+
+template <class Md>
+static int launch_physics(duck_sim* s, int n, float* qpos, float* qvel, float* warm, const float* ctrl, const float* dr,
+                          int nsub, float* aux, float* scratch, hipStream_t st) {
+  const dim3 grid((n + WG - 1) / WG), block(WG);
+  KArgs A = make_args(s, n);
+  A.dr = dr;
+  A.scratch = scratch;
+  hipLaunchKernelGGL((physics_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A, qpos, qvel, warm, ctrl, nsub, aux);
+  HIPCHECK(hipGetLastError());
+  return DUCK_OK;
+}
+
+extern "C" {
+
+int duck_version(void) { return DUCK_VERSION; }
+const char* duck_last_error(void) { return g_err.c_str(); }
+
+int duck_layout_get(int nq, int nv, int nu, int imitation, duck_layout* out) {
+  if (!out) return fail(DUCK_EINVAL, "null out");
+  *out = duck_layout_make(nq, nv, nu, imitation);
+  return DUCK_OK;
+}
+
+int duck_aux_size(const duck_sim* sim) {
+  if (!sim) return fail(DUCK_EINVAL, "null sim");
+  return sim->variant == V_FLAT ? aux_size<DuckModel_flat>() : aux_size<DuckModel_backlash>();
+}
+
+int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const duck_refmotion* ref, int device,
+                duck_sim** out) {
+  g_err.clear();
+  if (!model || !cfg || !out) return fail(DUCK_EINVAL, "null argument");
+  Variant v;
+  if (matches<DuckModel_flat>(model)) v = V_FLAT;
+  else if (matches<DuckModel_backlash>(model)) v = V_BACKLASH;
+  else return fail(DUCK_EUNSUPPORTED, "model does not match a compiled Open Duck variant (flat / flat_backlash)");
+  if (cfg->use_imitation && !ref) return fail(DUCK_EINVAL, "use_imitation requires a reference-motion table");
+  if (cfg->n_substeps < 1 || cfg->action_max_delay < 1 || cfg->action_max_delay > 3)
+    return fail(DUCK_EINVAL, "bad config (n_substeps >= 1, 1 <= action_max_delay <= 3)");
+  HIPCHECK(hipSetDevice(device));
+  duck_sim* s = new duck_sim();
+  s->device = device;
+  s->variant = v;
+  s->cfg = *cfg;
+  s->nq = model->nq; s->nv = model->nv; s->nu = model->nu;
+  s->lay = duck_layout_make(model->nq, model->nv, model->nu, cfg->use_imitation);
+  s->drl = duck_dr_layout_make(model->nbody, model->nu);
+  memset(&s->ref, 0, sizeof(s->ref));
+  s->frames_d = nullptr;
+  if (ref) {
+    if (ref->n_dim != 40 || ref->n_dx > 16 || ref->n_dy > 16 || ref->n_dtheta > 16 || ref->nb_steps_in_period < 1 ||
+        !ref->frames) {
+      delete s;
+      return fail(DUCK_EINVAL, "reference-motion table must be [<=16][<=16][<=16][nb][40] frames");
+    }
+    s->ref.n_dx = ref->n_dx; s->ref.n_dy = ref->n_dy; s->ref.n_dtheta = ref->n_dtheta;
+    s->ref.n_dim = ref->n_dim; s->ref.n_coef = ref->n_coef; s->ref.nb = ref->nb_steps_in_period;
+    memcpy(s->ref.dxs, ref->dxs, sizeof(ref->dxs)); memcpy(s->ref.dys, ref->dys, sizeof(ref->dys));
+    memcpy(s->ref.dthetas, ref->dthetas, sizeof(ref->dthetas));
+    memcpy(s->ref.dx_range, ref->dx_range, 8); memcpy(s->ref.dy_range, ref->dy_range, 8);
+    memcpy(s->ref.dtheta_range, ref->dtheta_range, 8);
+    const size_t nbytes =
+        sizeof(float) * (size_t)ref->n_dx * ref->n_dy * ref->n_dtheta * ref->nb_steps_in_period * ref->n_dim;
+    hipError_t e = hipMalloc(&s->frames_d, nbytes);
+    if (e == hipSuccess) e = hipMemcpy(s->frames_d, ref->frames, nbytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      if (s->frames_d) (void)hipFree(s->frames_d);
+      delete s;
+      return fail(DUCK_EHIP, std::string("reference table upload: ") + hipGetErrorString(e));
+    }
+  }
+  // LDS budget
+  const size_t need = v == V_FLAT ? lds_bytes<DuckModel_flat>() : lds_bytes<DuckModel_backlash>();
+  if (need > 160 * 1024) {
+    duck_destroy(s);
+    return fail(DUCK_EUNSUPPORTED, "per-workgroup LDS over 160 KiB");
+  }
+  *out = s;
+  return DUCK_OK;
+}
+
+void duck_destroy(duck_sim* s) {
+  if (!s) return;
+  if (s->frames_d) (void)hipFree(s->frames_d);
+  delete s;
+}
+
+
+
+
+int duck_reset(duck_sim* s, int n, float* fstate, int32_t* istate, const uint8_t* mask, uint64_t seed,
+               int64_t env_offset, const float* dr, float* obs, float* priv, void* stream) {
+  g_err.clear();
+  if (!s || n < 0 || !fstate || !istate || !obs || !priv) return fail(DUCK_EINVAL, "bad argument");
+  if (n == 0) return DUCK_OK;
+  HIPCHECK(hipSetDevice(s->device));
+  KArgs A = make_args(s, n);
+  A.fs = fstate; A.is = istate; A.mask = mask; A.seed = seed; A.env_offset = env_offset; A.dr = dr;
+  A.obs = obs; A.priv = priv;
+  hipStream_t st = (hipStream_t)stream;
+  return s->variant == V_FLAT ? launch_reset<DuckModel_flat>(s, A, st) : launch_reset<DuckModel_backlash>(s, A, st);
+}
+
+int duck_step(duck_sim* s, int n, float* fstate, int32_t* istate, const float* dr, const float* action, float* obs,
+              float* priv, float* reward, float* done, float* scratch, void* stream) {
+  g_err.clear();
+  if (!s || n < 0 || !fstate || !istate || !action || !obs || !priv || !reward || !done)
+    return fail(DUCK_EINVAL, "bad argument");
+  if (n == 0) return DUCK_OK;
+  HIPCHECK(hipSetDevice(s->device));
+  KArgs A = make_args(s, n);
+  A.fs = fstate; A.is = istate; A.dr = dr; A.action = action; A.obs = obs; A.priv = priv;
+  A.reward = reward; A.done = done; A.scratch = scratch;
+  hipStream_t st = (hipStream_t)stream;
+  return s->variant == V_FLAT ? launch_step<DuckModel_flat>(s, A, st) : launch_step<DuckModel_backlash>(s, A, st);
+}
+
+int duck_randomize(duck_sim* s, int n, float* dr, uint64_t seed, int64_t env_offset, void* stream) {
+  g_err.clear();
+  if (!s || n < 0 || !dr) return fail(DUCK_EINVAL, "bad argument");
+  if (n == 0) return DUCK_OK;
+  HIPCHECK(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((n + 255) / 256), block(256);
+  if (s->variant == V_FLAT)
+    hipLaunchKernelGGL((randomize_kernel<DuckModel_flat>), grid, block, 0, st, n, dr, s->drl, seed, env_offset);
+  else
+    hipLaunchKernelGGL((randomize_kernel<DuckModel_backlash>), grid, block, 0, st, n, dr, s->drl, seed, env_offset);
+  HIPCHECK(hipGetLastError());
+  return DUCK_OK;
+}
+
+
+int duck_physics_step(duck_sim* s, int n, float* qpos, float* qvel, float* warm, const float* ctrl, const float* dr,
+                      int nsub, float* aux, float* scratch, void* stream) {
+  g_err.clear();
+  if (!s || n < 0 || !qpos || !qvel || !warm || !ctrl || nsub < 0) return fail(DUCK_EINVAL, "bad argument");
+  if (n == 0) return DUCK_OK;
+  HIPCHECK(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  return s->variant == V_FLAT
+             ? launch_physics<DuckModel_flat>(s, n, qpos, qvel, warm, ctrl, dr, nsub, aux, scratch, st)
+             : launch_physics<DuckModel_backlash>(s, n, qpos, qvel, warm, ctrl, dr, nsub, aux, scratch, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,84 @@
+"""Loader for the MI355X C-ABI library (``libduck.so``, ``include/duck.h``).
+
+The product path only ever calls into this library; there is no CPU fallback. If the
+shared object is missing or fails to load, every entry point raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+from .cabi import DuckEnvConfig, DuckModelDesc, DuckRefMotion
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libduck.so")
+CSRC = os.path.join(HERE, "csrc")
+ROOT = os.path.dirname(HERE)
+
+EXPORTS = ["duck_version", "duck_last_error", "duck_layout_get", "duck_aux_size", "duck_create", "duck_destroy",
+           "duck_reset", "duck_step", "duck_randomize", "duck_physics_step"]
+
+
+class DuckError(RuntimeError):
+    pass
+
+
+class DuckLayout(C.Structure):
+    _fields_ = [(k, C.c_int) for k in (
+        "nq", "nv", "nu", "imitation", "obs_size", "priv_size",
+        "qpos", "qvel", "qacc_warmstart", "ctrl", "command", "last_act", "last_last_act", "last_last_last_act",
+        "motor_targets", "feet_air_time", "last_contact", "swing_peak", "push", "action_history", "imu_history",
+        "ref_motion", "imitation_phase", "metrics", "reward", "done", "truncation", "first_qpos", "first_qvel",
+        "first_qacc_warmstart", "first_ctrl", "first_obs", "first_priv", "nfloat",
+        "rng_key", "rng_ctr", "step", "push_step", "push_interval", "imitation_i", "ep_steps", "nint")]
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libduck.so for gfx950 with hipcc (in-tree, so it travels with the repo)."""
+    srcs = [os.path.join(CSRC, "duck_kernels.hip")]
+    deps = srcs + [os.path.join(CSRC, f) for f in ("duck_physics.h", "duck_math.h")] + \
+        [os.path.join(CSRC, "generated", f) for f in os.listdir(os.path.join(CSRC, "generated"))] + \
+        [os.path.join(ROOT, "include", f) for f in ("duck.h", "duck_env.h", "duck_model.h")]
+    if os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= max(os.path.getmtime(d) for d in deps):
+        return LIB_PATH
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", LIB_PATH + ".tmp"] + srcs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd, cwd=CSRC)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    """Load libduck.so (raises if it is missing: no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DuckError(f"{LIB_PATH} not built; run __graft_entry__.build() or native.build()")
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.duck_version.restype = C.c_int
+        L.duck_last_error.restype = C.c_char_p
+        L.duck_layout_get.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(DuckLayout)]
+        L.duck_aux_size.argtypes = [vp]
+        L.duck_create.argtypes = [C.POINTER(DuckModelDesc), C.POINTER(DuckEnvConfig), C.POINTER(DuckRefMotion), C.c_int,
+                                  C.POINTER(vp)]
+        L.duck_destroy.argtypes = [vp]
+        L.duck_destroy.restype = None
+        L.duck_reset.argtypes = [vp, C.c_int, vp, vp, vp, C.c_uint64, C.c_int64, vp, vp, vp, vp]
+        L.duck_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.duck_randomize.argtypes = [vp, C.c_int, vp, C.c_uint64, C.c_int64, vp]
+        L.duck_physics_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def check(rc: int):
+    if rc != 0:
+        raise DuckError(f"libduck error {rc}: {lib().duck_last_error().decode()}")
+    return rc

@@ -1,0 +1,1712 @@
+/* duck_oracle.c — CPU (fp64) restatement of the Open Duck Joystick hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline). See duck_oracle.h for the
+ * scope and DESIGN.md for what is pinned and what is not. Every block cites the
+ * reference file:line it restates; physics blocks name the upstream MuJoCo/MJX stage.
+ */
+#include "duck_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define MINVAL 1e-15
+#define PI 3.14159265358979323846
+#define MINIMP 0.0001
+#define MAXIMP 0.9999
+#define MAXEFC 128
+#define NV DUCK_MAXV
+
+struct oracle_model {
+  int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
+  double timestep, gravity[3], impratio, tolerance, ls_tolerance, meaninertia;
+  int iterations, ls_iterations, eulerdamp;
+  int body_parentid[DUCK_MAXBODY], body_rootid[DUCK_MAXBODY], body_weldid[DUCK_MAXBODY],
+      body_jntnum[DUCK_MAXBODY], body_jntadr[DUCK_MAXBODY], body_dofnum[DUCK_MAXBODY], body_dofadr[DUCK_MAXBODY];
+  double body_pos[DUCK_MAXBODY][3], body_quat[DUCK_MAXBODY][4], body_ipos[DUCK_MAXBODY][3],
+      body_iquat[DUCK_MAXBODY][4], body_mass[DUCK_MAXBODY], body_inertia[DUCK_MAXBODY][3],
+      body_invweight0[DUCK_MAXBODY][2];
+  int jnt_type[DUCK_MAXJNT], jnt_qposadr[DUCK_MAXJNT], jnt_dofadr[DUCK_MAXJNT], jnt_bodyid[DUCK_MAXJNT],
+      jnt_limited[DUCK_MAXJNT];
+  double jnt_pos[DUCK_MAXJNT][3], jnt_axis[DUCK_MAXJNT][3], jnt_range[DUCK_MAXJNT][2], jnt_margin[DUCK_MAXJNT],
+      jnt_solref[DUCK_MAXJNT][2], jnt_solimp[DUCK_MAXJNT][5];
+  int dof_bodyid[NV], dof_jntid[NV], dof_parentid[NV];
+  double dof_armature[NV], dof_damping[NV], dof_frictionloss[NV], dof_invweight0[NV], dof_solref[NV][2],
+      dof_solimp[NV][5];
+  int dof_has_friction[NV]; /* row selection from the nominal model (MJX: static) */
+  int geom_type[DUCK_MAXGEOM], geom_bodyid[DUCK_MAXGEOM], geom_dataid[DUCK_MAXGEOM];
+  double geom_pos[DUCK_MAXGEOM][3], geom_quat[DUCK_MAXGEOM][4], geom_rbound[DUCK_MAXGEOM], geom_size[DUCK_MAXGEOM][3];
+  int pair_geom1[DUCK_MAXPAIR], pair_geom2[DUCK_MAXPAIR], pair_condim[DUCK_MAXPAIR];
+  double pair_friction[DUCK_MAXPAIR][5], pair_solref[DUCK_MAXPAIR][2], pair_solimp[DUCK_MAXPAIR][5],
+      pair_margin[DUCK_MAXPAIR];
+  int hull_nvert, hull_nface, hull_nedge;
+  double hull_vert[DUCK_MAXHULLV][3], hull_face_normal[DUCK_MAXHULLF][3], hull_face_offset[DUCK_MAXHULLF];
+  int hull_edge[DUCK_MAXHULLE][2];
+  double hull_center[3], hull_radius;
+  int hfield_nrow, hfield_ncol;
+  double hfield_size[4];
+  double* hfield_data;
+  int site_bodyid[DUCK_MAXSITE];
+  double site_pos[DUCK_MAXSITE][3], site_quat[DUCK_MAXSITE][4];
+  int actuator_trnid[DUCK_MAXU], actuator_ctrllimited[DUCK_MAXU], actuator_forcelimited[DUCK_MAXU];
+  double actuator_kp[DUCK_MAXU], actuator_kv[DUCK_MAXU], actuator_gear[DUCK_MAXU], actuator_ctrlrange[DUCK_MAXU][2],
+      actuator_forcerange[DUCK_MAXU][2];
+  int sensor_type[DUCK_MAXSENSOR], sensor_objid[DUCK_MAXSENSOR], sensor_adr[DUCK_MAXSENSOR],
+      sensor_dim[DUCK_MAXSENSOR];
+  double qpos0[DUCK_MAXQ];
+};
+
+/* ------------------------------------------------------------------------------------ */
+/* model                                                                                */
+/* ------------------------------------------------------------------------------------ */
+
+#define CP(dst, src, n) memcpy((dst), (src), sizeof(*(src)) * (size_t)(n))
+
+oracle_model* oracle_model_create(const duck_model_desc* s) {
+  if (s->nbody > DUCK_MAXBODY || s->nv > DUCK_MAXV || s->nq > DUCK_MAXQ || s->nu > DUCK_MAXU ||
+      s->njnt > DUCK_MAXJNT || s->ngeom > DUCK_MAXGEOM || s->npair > DUCK_MAXPAIR ||
+      s->hull_nvert > DUCK_MAXHULLV || s->hull_nface > DUCK_MAXHULLF || s->hull_nedge > DUCK_MAXHULLE)
+    return NULL;
+  oracle_model* m = (oracle_model*)calloc(1, sizeof(oracle_model));
+  m->nq = s->nq; m->nv = s->nv; m->nu = s->nu; m->nbody = s->nbody; m->njnt = s->njnt; m->ngeom = s->ngeom;
+  m->nsite = s->nsite; m->nsensor = s->nsensor; m->nsensordata = s->nsensordata; m->npair = s->npair;
+  m->timestep = s->timestep; CP(m->gravity, s->gravity, 3); m->impratio = s->impratio;
+  m->tolerance = s->tolerance; m->ls_tolerance = s->ls_tolerance; m->meaninertia = s->meaninertia;
+  m->iterations = s->iterations; m->ls_iterations = s->ls_iterations; m->eulerdamp = s->eulerdamp;
+  int nb = s->nbody;
+  for (int i = 0; i < nb; i++) {
+    m->body_parentid[i] = s->body_parentid[i]; m->body_rootid[i] = s->body_rootid[i];
+    m->body_weldid[i] = s->body_weldid[i]; m->body_jntnum[i] = s->body_jntnum[i];
+    m->body_jntadr[i] = s->body_jntadr[i]; m->body_dofnum[i] = s->body_dofnum[i];
+    m->body_dofadr[i] = s->body_dofadr[i]; m->body_mass[i] = s->body_mass[i];
+    CP(m->body_pos[i], s->body_pos + 3 * i, 3); CP(m->body_quat[i], s->body_quat + 4 * i, 4);
+    CP(m->body_ipos[i], s->body_ipos + 3 * i, 3); CP(m->body_iquat[i], s->body_iquat + 4 * i, 4);
+    CP(m->body_inertia[i], s->body_inertia + 3 * i, 3); CP(m->body_invweight0[i], s->body_invweight0 + 2 * i, 2);
+  }
+  for (int j = 0; j < s->njnt; j++) {
+    m->jnt_type[j] = s->jnt_type[j]; m->jnt_qposadr[j] = s->jnt_qposadr[j]; m->jnt_dofadr[j] = s->jnt_dofadr[j];
+    m->jnt_bodyid[j] = s->jnt_bodyid[j]; m->jnt_limited[j] = s->jnt_limited[j]; m->jnt_margin[j] = s->jnt_margin[j];
+    CP(m->jnt_pos[j], s->jnt_pos + 3 * j, 3); CP(m->jnt_axis[j], s->jnt_axis + 3 * j, 3);
+    CP(m->jnt_range[j], s->jnt_range + 2 * j, 2); CP(m->jnt_solref[j], s->jnt_solref + 2 * j, 2);
+    CP(m->jnt_solimp[j], s->jnt_solimp + 5 * j, 5);
+  }
+  for (int i = 0; i < s->nv; i++) {
+    m->dof_bodyid[i] = s->dof_bodyid[i]; m->dof_jntid[i] = s->dof_jntid[i]; m->dof_parentid[i] = s->dof_parentid[i];
+    m->dof_armature[i] = s->dof_armature[i]; m->dof_damping[i] = s->dof_damping[i];
+    m->dof_frictionloss[i] = s->dof_frictionloss[i]; m->dof_invweight0[i] = s->dof_invweight0[i];
+    m->dof_has_friction[i] = s->dof_frictionloss[i] > 0;
+    CP(m->dof_solref[i], s->dof_solref + 2 * i, 2); CP(m->dof_solimp[i], s->dof_solimp + 5 * i, 5);
+  }
+  for (int g = 0; g < s->ngeom; g++) {
+    m->geom_type[g] = s->geom_type[g]; m->geom_bodyid[g] = s->geom_bodyid[g]; m->geom_dataid[g] = s->geom_dataid[g];
+    m->geom_rbound[g] = s->geom_rbound[g];
+    CP(m->geom_pos[g], s->geom_pos + 3 * g, 3); CP(m->geom_quat[g], s->geom_quat + 4 * g, 4);
+    CP(m->geom_size[g], s->geom_size + 3 * g, 3);
+  }
+  for (int p = 0; p < s->npair; p++) {
+    m->pair_geom1[p] = s->pair_geom1[p]; m->pair_geom2[p] = s->pair_geom2[p]; m->pair_condim[p] = s->pair_condim[p];
+    CP(m->pair_friction[p], s->pair_friction + 5 * p, 5); CP(m->pair_solref[p], s->pair_solref + 2 * p, 2);
+    CP(m->pair_solimp[p], s->pair_solimp + 5 * p, 5); m->pair_margin[p] = s->pair_margin[p];
+  }
+  m->hull_nvert = s->hull_nvert; m->hull_nface = s->hull_nface; m->hull_nedge = s->hull_nedge;
+  double c[3] = {0, 0, 0};
+  for (int k = 0; k < s->hull_nvert; k++) {
+    CP(m->hull_vert[k], s->hull_vert + 3 * k, 3);
+    for (int a = 0; a < 3; a++) c[a] += m->hull_vert[k][a] / s->hull_nvert;
+  }
+  double r = 0;
+  for (int k = 0; k < s->hull_nvert; k++) {
+    double dx = m->hull_vert[k][0] - c[0], dy = m->hull_vert[k][1] - c[1], dz = m->hull_vert[k][2] - c[2];
+    double rr = sqrt(dx * dx + dy * dy + dz * dz);
+    if (rr > r) r = rr;
+  }
+  CP(m->hull_center, c, 3); m->hull_radius = r;
+  for (int f = 0; f < s->hull_nface; f++) {
+    CP(m->hull_face_normal[f], s->hull_face_normal + 3 * f, 3);
+    m->hull_face_offset[f] = s->hull_face_offset[f];
+  }
+  for (int e = 0; e < s->hull_nedge; e++) { m->hull_edge[e][0] = s->hull_edge[2 * e]; m->hull_edge[e][1] = s->hull_edge[2 * e + 1]; }
+  m->hfield_nrow = s->hfield_nrow; m->hfield_ncol = s->hfield_ncol; CP(m->hfield_size, s->hfield_size, 4);
+  if (s->hfield_nrow > 0) {
+    m->hfield_data = (double*)malloc(sizeof(double) * (size_t)s->hfield_nrow * s->hfield_ncol);
+    CP(m->hfield_data, s->hfield_data, (size_t)s->hfield_nrow * s->hfield_ncol);
+  }
+  for (int i = 0; i < s->nsite; i++) {
+    m->site_bodyid[i] = s->site_bodyid[i];
+    CP(m->site_pos[i], s->site_pos + 3 * i, 3); CP(m->site_quat[i], s->site_quat + 4 * i, 4);
+  }
+  for (int a = 0; a < s->nu; a++) {
+    m->actuator_trnid[a] = s->actuator_trnid[a]; m->actuator_ctrllimited[a] = s->actuator_ctrllimited[a];
+    m->actuator_forcelimited[a] = s->actuator_forcelimited[a]; m->actuator_kp[a] = s->actuator_kp[a];
+    m->actuator_kv[a] = s->actuator_kv[a]; m->actuator_gear[a] = s->actuator_gear[a];
+    CP(m->actuator_ctrlrange[a], s->actuator_ctrlrange + 2 * a, 2);
+    CP(m->actuator_forcerange[a], s->actuator_forcerange + 2 * a, 2);
+  }
+  for (int i = 0; i < s->nsensor; i++) {
+    m->sensor_type[i] = s->sensor_type[i]; m->sensor_objid[i] = s->sensor_objid[i];
+    m->sensor_adr[i] = s->sensor_adr[i]; m->sensor_dim[i] = s->sensor_dim[i];
+  }
+  CP(m->qpos0, s->qpos0, s->nq);
+  return m;
+}
+
+void oracle_model_destroy(oracle_model* m) {
+  if (!m) return;
+  free(m->hfield_data);
+  free(m);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* small math                                                                           */
+/* ------------------------------------------------------------------------------------ */
+
+static double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void cross3(double* r, const double* a, const double* b) {
+  double t[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+  r[0] = t[0]; r[1] = t[1]; r[2] = t[2];
+}
+static double norm3(const double* a) { return sqrt(dot3(a, a)); }
+static void mulmv3(double* r, const double* M, const double* v) {
+  double t[3] = {M[0] * v[0] + M[1] * v[1] + M[2] * v[2], M[3] * v[0] + M[4] * v[1] + M[5] * v[2],
+                 M[6] * v[0] + M[7] * v[1] + M[8] * v[2]};
+  r[0] = t[0]; r[1] = t[1]; r[2] = t[2];
+}
+static void mulmtv3(double* r, const double* M, const double* v) {
+  double t[3] = {M[0] * v[0] + M[3] * v[1] + M[6] * v[2], M[1] * v[0] + M[4] * v[1] + M[7] * v[2],
+                 M[2] * v[0] + M[5] * v[1] + M[8] * v[2]};
+  r[0] = t[0]; r[1] = t[1]; r[2] = t[2];
+}
+static void mulmm3(double* r, const double* A, const double* B) {
+  double t[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) t[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+  memcpy(r, t, sizeof(t));
+}
+static void quat_mul(double* r, const double* a, const double* b) {
+  double t[4] = {a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+                 a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+                 a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+                 a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0]};
+  memcpy(r, t, sizeof(t));
+}
+static void quat_normalize(double* q) {
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  for (int i = 0; i < 4; i++) q[i] /= n;
+}
+static void quat2mat(double* R, const double* q) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+static void axis_angle_quat(double* q, const double* axis, double angle) {
+  double s = sin(0.5 * angle);
+  q[0] = cos(0.5 * angle); q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
+}
+
+/* spatial algebra in MuJoCo's com-based convention: motion/force = [angular; linear] */
+static void mul_inert_vec(double* r, const double* I, const double* v) {
+  r[0] = I[0] * v[0] + I[3] * v[1] + I[4] * v[2] - I[8] * v[4] + I[7] * v[5];
+  r[1] = I[3] * v[0] + I[1] * v[1] + I[5] * v[2] + I[8] * v[3] - I[6] * v[5];
+  r[2] = I[4] * v[0] + I[5] * v[1] + I[2] * v[2] - I[7] * v[3] + I[6] * v[4];
+  r[3] = I[8] * v[1] - I[7] * v[2] + I[9] * v[3];
+  r[4] = I[6] * v[2] - I[8] * v[0] + I[9] * v[4];
+  r[5] = I[7] * v[0] - I[6] * v[1] + I[9] * v[5];
+}
+static void cross_motion(double* r, const double* v, const double* u) {
+  r[0] = -v[2] * u[1] + v[1] * u[2];
+  r[1] = v[2] * u[0] - v[0] * u[2];
+  r[2] = -v[1] * u[0] + v[0] * u[1];
+  r[3] = -v[2] * u[4] + v[1] * u[5] - v[5] * u[1] + v[4] * u[2];
+  r[4] = v[2] * u[3] - v[0] * u[5] + v[5] * u[0] - v[3] * u[2];
+  r[5] = -v[1] * u[3] + v[0] * u[4] - v[4] * u[0] + v[3] * u[1];
+}
+static void cross_force(double* r, const double* v, const double* f) {
+  r[0] = -v[2] * f[1] + v[1] * f[2] - v[5] * f[4] + v[4] * f[5];
+  r[1] = v[2] * f[0] - v[0] * f[2] + v[5] * f[3] - v[3] * f[5];
+  r[2] = -v[1] * f[0] + v[0] * f[1] - v[4] * f[3] + v[3] * f[4];
+  r[3] = -v[2] * f[4] + v[1] * f[5];
+  r[4] = v[2] * f[3] - v[0] * f[5];
+  r[5] = -v[1] * f[3] + v[0] * f[4];
+}
+static double dot6(const double* a, const double* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+/* dense Cholesky (lower), in place; returns 0 on failure */
+static int cholesky(double* A, int n) {
+  for (int j = 0; j < n; j++) {
+    double s = A[j * NV + j];
+    for (int k = 0; k < j; k++) s -= A[j * NV + k] * A[j * NV + k];
+    if (s <= MINVAL) return 0;
+    double d = sqrt(s);
+    A[j * NV + j] = d;
+    for (int i = j + 1; i < n; i++) {
+      double t = A[i * NV + j];
+      for (int k = 0; k < j; k++) t -= A[i * NV + k] * A[j * NV + k];
+      A[i * NV + j] = t / d;
+    }
+  }
+  return 1;
+}
+static void chol_solve(const double* L, int n, double* x) {
+  for (int i = 0; i < n; i++) {
+    double s = x[i];
+    for (int k = 0; k < i; k++) s -= L[i * NV + k] * x[k];
+    x[i] = s / L[i * NV + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double s = x[i];
+    for (int k = i + 1; k < n; k++) s -= L[k * NV + i] * x[k];
+    x[i] = s / L[i * NV + i];
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* forward-pass scratch                                                                 */
+/* ------------------------------------------------------------------------------------ */
+
+typedef struct fwd_ws {
+  double xanchor[DUCK_MAXJNT][3], xaxis[DUCK_MAXJNT][3];
+  double subtree_com[DUCK_MAXBODY][3];
+  double cinert[DUCK_MAXBODY][10], crb[DUCK_MAXBODY][10];
+  double cdof[NV][6], cdof_dot[NV][6], cvel[DUCK_MAXBODY][6];
+  double site_xquat[DUCK_MAXSITE][4];
+  /* constraint rows */
+  int nefc;
+  double J[MAXEFC][NV], D[MAXEFC], R[MAXEFC], aref[MAXEFC], frictionloss[MAXEFC];
+  int ineq[MAXEFC]; /* 1: inequality (limit/contact), 0: friction */
+} fwd_ws;
+
+/* mj_kinematics (smooth.kinematics): body/site/geom frames from qpos.
+ * Hinge rotation angle is qpos - qpos0 (MuJoCo semantics; DR jitters qpos0, randomize.py:78-86). */
+static void kinematics(const oracle_model* m, oracle_data* d, fwd_ws* w) {
+  d->xpos[0][0] = d->xpos[0][1] = d->xpos[0][2] = 0;
+  d->xquat[0][0] = 1; d->xquat[0][1] = d->xquat[0][2] = d->xquat[0][3] = 0;
+  quat2mat(d->xmat[0], d->xquat[0]);
+  memcpy(d->xipos[0], d->xpos[0], sizeof(d->xpos[0]));
+  memcpy(d->ximat[0], d->xmat[0], sizeof(d->xmat[0]));
+  for (int i = 1; i < m->nbody; i++) {
+    int p = m->body_parentid[i], ja = m->body_jntadr[i], jn = m->body_jntnum[i];
+    if (jn > 0 && m->jnt_type[ja] == DUCK_JNT_FREE) {
+      int a = m->jnt_qposadr[ja];
+      memcpy(d->xpos[i], d->qpos + a, 3 * sizeof(double));
+      memcpy(d->xquat[i], d->qpos + a + 3, 4 * sizeof(double));
+      quat_normalize(d->xquat[i]);
+      memcpy(w->xanchor[ja], d->xpos[i], 3 * sizeof(double));
+      w->xaxis[ja][0] = 0; w->xaxis[ja][1] = 0; w->xaxis[ja][2] = 1;
+    } else {
+      double t[3], q[4], R[9];
+      mulmv3(t, d->xmat[p], m->body_pos[i]);
+      for (int k = 0; k < 3; k++) d->xpos[i][k] = d->xpos[p][k] + t[k];
+      quat_mul(q, d->xquat[p], m->body_quat[i]);
+      for (int j = ja; j < ja + jn; j++) {
+        quat2mat(R, q);
+        mulmv3(t, R, m->jnt_pos[j]);
+        for (int k = 0; k < 3; k++) w->xanchor[j][k] = t[k] + d->xpos[i][k];
+        mulmv3(w->xaxis[j], R, m->jnt_axis[j]);
+        int a = m->jnt_qposadr[j];
+        if (m->jnt_type[j] == DUCK_JNT_HINGE) {
+          double ql[4];
+          axis_angle_quat(ql, m->jnt_axis[j], d->qpos[a] - m->qpos0[a]);
+          quat_mul(q, q, ql);
+          quat2mat(R, q);
+          mulmv3(t, R, m->jnt_pos[j]);
+          for (int k = 0; k < 3; k++) d->xpos[i][k] = w->xanchor[j][k] - t[k];
+        } else if (m->jnt_type[j] == DUCK_JNT_SLIDE) {
+          for (int k = 0; k < 3; k++) d->xpos[i][k] += w->xaxis[j][k] * (d->qpos[a] - m->qpos0[a]);
+        }
+      }
+      memcpy(d->xquat[i], q, sizeof(q));
+      quat_normalize(d->xquat[i]);
+    }
+    quat2mat(d->xmat[i], d->xquat[i]);
+    double t[3], Ri[9];
+    mulmv3(t, d->xmat[i], m->body_ipos[i]);
+    for (int k = 0; k < 3; k++) d->xipos[i][k] = d->xpos[i][k] + t[k];
+    quat2mat(Ri, m->body_iquat[i]);
+    mulmm3(d->ximat[i], d->xmat[i], Ri);
+  }
+  for (int s = 0; s < m->nsite; s++) {
+    int b = m->site_bodyid[s];
+    double t[3], Rs[9];
+    mulmv3(t, d->xmat[b], m->site_pos[s]);
+    for (int k = 0; k < 3; k++) d->site_xpos[s][k] = d->xpos[b][k] + t[k];
+    quat_mul(w->site_xquat[s], d->xquat[b], m->site_quat[s]);
+    quat_normalize(w->site_xquat[s]);
+    quat2mat(Rs, m->site_quat[s]);
+    mulmm3(d->site_xmat[s], d->xmat[b], Rs);
+  }
+  for (int g = 0; g < m->ngeom; g++) {
+    int b = m->geom_bodyid[g];
+    double t[3], Rg[9];
+    mulmv3(t, d->xmat[b], m->geom_pos[g]);
+    for (int k = 0; k < 3; k++) d->geom_xpos[g][k] = d->xpos[b][k] + t[k];
+    quat2mat(Rg, m->geom_quat[g]);
+    mulmm3(d->geom_xmat[g], d->xmat[b], Rg);
+  }
+}
+
+/* mj_comPos (smooth.com_pos): subtree coms, com-based inertias, motion dofs */
+static void com_pos(const oracle_model* m, oracle_data* d, fwd_ws* w) {
+  double msum[DUCK_MAXBODY], acc[DUCK_MAXBODY][3];
+  for (int i = 0; i < m->nbody; i++) {
+    msum[i] = m->body_mass[i];
+    for (int k = 0; k < 3; k++) acc[i][k] = m->body_mass[i] * d->xipos[i][k];
+  }
+  for (int i = m->nbody - 1; i > 0; i--) {
+    int p = m->body_parentid[i];
+    msum[p] += msum[i];
+    for (int k = 0; k < 3; k++) acc[p][k] += acc[i][k];
+  }
+  for (int i = 0; i < m->nbody; i++)
+    for (int k = 0; k < 3; k++) w->subtree_com[i][k] = fabs(msum[i]) > MINVAL ? acc[i][k] / msum[i] : d->xipos[i][k];
+  for (int i = 1; i < m->nbody; i++) {
+    const double* c = w->subtree_com[m->body_rootid[i]];
+    double dif[3] = {d->xipos[i][0] - c[0], d->xipos[i][1] - c[1], d->xipos[i][2] - c[2]};
+    const double* R = d->ximat[i];
+    const double* I = m->body_inertia[i];
+    double mass = m->body_mass[i];
+    double rot[9];
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++)
+        rot[3 * a + b] = R[3 * a] * I[0] * R[3 * b] + R[3 * a + 1] * I[1] * R[3 * b + 1] + R[3 * a + 2] * I[2] * R[3 * b + 2];
+    double dd = dot3(dif, dif);
+    double* ci = w->cinert[i];
+    ci[0] = rot[0] + mass * (dd - dif[0] * dif[0]);
+    ci[1] = rot[4] + mass * (dd - dif[1] * dif[1]);
+    ci[2] = rot[8] + mass * (dd - dif[2] * dif[2]);
+    ci[3] = rot[1] - mass * dif[0] * dif[1];
+    ci[4] = rot[2] - mass * dif[0] * dif[2];
+    ci[5] = rot[5] - mass * dif[1] * dif[2];
+    ci[6] = mass * dif[0]; ci[7] = mass * dif[1]; ci[8] = mass * dif[2];
+    ci[9] = mass;
+  }
+  for (int j = 0; j < m->njnt; j++) {
+    int b = m->jnt_bodyid[j], da = m->jnt_dofadr[j];
+    const double* c = w->subtree_com[m->body_rootid[b]];
+    double off[3] = {c[0] - w->xanchor[j][0], c[1] - w->xanchor[j][1], c[2] - w->xanchor[j][2]};
+    if (m->jnt_type[j] == DUCK_JNT_FREE) {
+      for (int k = 0; k < 3; k++) {
+        memset(w->cdof[da + k], 0, 6 * sizeof(double));
+        w->cdof[da + k][3 + k] = 1;
+      }
+      for (int k = 0; k < 3; k++) {
+        double ax[3] = {d->xmat[b][k], d->xmat[b][3 + k], d->xmat[b][6 + k]};
+        memcpy(w->cdof[da + 3 + k], ax, sizeof(ax));
+        cross3(w->cdof[da + 3 + k] + 3, ax, off);
+      }
+    } else if (m->jnt_type[j] == DUCK_JNT_HINGE) {
+      memcpy(w->cdof[da], w->xaxis[j], 3 * sizeof(double));
+      cross3(w->cdof[da] + 3, w->xaxis[j], off);
+    } else { /* slide */
+      memset(w->cdof[da], 0, 3 * sizeof(double));
+      memcpy(w->cdof[da] + 3, w->xaxis[j], 3 * sizeof(double));
+    }
+  }
+}
+
+/* mj_crb (smooth.crb): composite inertias and joint-space mass matrix */
+static void crb(const oracle_model* m, oracle_data* d, fwd_ws* w) {
+  memcpy(w->crb, w->cinert, sizeof(w->crb));
+  for (int i = m->nbody - 1; i > 0; i--) {
+    int p = m->body_parentid[i];
+    if (p > 0)
+      for (int k = 0; k < 10; k++) w->crb[p][k] += w->crb[i][k];
+  }
+  memset(d->qM, 0, sizeof(d->qM));
+  for (int i = 0; i < m->nv; i++) {
+    double buf[6];
+    mul_inert_vec(buf, w->crb[m->dof_bodyid[i]], w->cdof[i]);
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+      double v = dot6(w->cdof[j], buf);
+      d->qM[i][j] = v;
+      d->qM[j][i] = v;
+    }
+    d->qM[i][i] += m->dof_armature[i];
+  }
+}
+
+/* mj_comVel (smooth.com_vel) */
+static void com_vel(const oracle_model* m, const oracle_data* d, fwd_ws* w) {
+  memset(w->cvel[0], 0, 6 * sizeof(double));
+  for (int i = 1; i < m->nbody; i++) {
+    double cv[6];
+    memcpy(cv, w->cvel[m->body_parentid[i]], sizeof(cv));
+    int da = m->body_dofadr[i], dn = m->body_dofnum[i];
+    int j = 0;
+    while (j < dn) {
+      int dof = da + j;
+      int jt = m->jnt_type[m->dof_jntid[dof]];
+      if (jt == DUCK_JNT_FREE) {
+        for (int k = 0; k < 3; k++) memset(w->cdof_dot[dof + k], 0, 6 * sizeof(double));
+        for (int k = 0; k < 3; k++)
+          for (int c = 0; c < 6; c++) cv[c] += w->cdof[dof + k][c] * d->qvel[dof + k];
+        for (int k = 3; k < 6; k++) cross_motion(w->cdof_dot[dof + k], cv, w->cdof[dof + k]);
+        for (int k = 3; k < 6; k++)
+          for (int c = 0; c < 6; c++) cv[c] += w->cdof[dof + k][c] * d->qvel[dof + k];
+        j += 6;
+      } else {
+        cross_motion(w->cdof_dot[dof], cv, w->cdof[dof]);
+        for (int c = 0; c < 6; c++) cv[c] += w->cdof[dof][c] * d->qvel[dof];
+        j += 1;
+      }
+    }
+    memcpy(w->cvel[i], cv, sizeof(cv));
+  }
+}
+
+/* mj_rne with flg_acc = 0 (smooth.rne): Coriolis/centrifugal + gravity bias forces */
+static void rne_bias(const oracle_model* m, oracle_data* d, const fwd_ws* w) {
+  double cacc[DUCK_MAXBODY][6], cfrc[DUCK_MAXBODY][6];
+  memset(cacc[0], 0, 6 * sizeof(double));
+  for (int k = 0; k < 3; k++) cacc[0][3 + k] = -m->gravity[k];
+  for (int i = 1; i < m->nbody; i++) {
+    int p = m->body_parentid[i];
+    memcpy(cacc[i], cacc[p], 6 * sizeof(double));
+    for (int j = 0; j < m->body_dofnum[i]; j++) {
+      int dof = m->body_dofadr[i] + j;
+      for (int c = 0; c < 6; c++) cacc[i][c] += w->cdof_dot[dof][c] * d->qvel[dof];
+    }
+    double t1[6], t2[6];
+    mul_inert_vec(cfrc[i], w->cinert[i], cacc[i]);
+    mul_inert_vec(t1, w->cinert[i], w->cvel[i]);
+    cross_force(t2, w->cvel[i], t1);
+    for (int c = 0; c < 6; c++) cfrc[i][c] += t2[c];
+  }
+  for (int i = m->nbody - 1; i > 0; i--) {
+    int p = m->body_parentid[i];
+    if (p > 0)
+      for (int c = 0; c < 6; c++) cfrc[p][c] += cfrc[i][c];
+  }
+  for (int i = 0; i < m->nv; i++) d->qfrc_bias[i] = dot6(w->cdof[i], cfrc[m->dof_bodyid[i]]);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* collision (MJX collision_driver semantics, fixed 4 slots per pair)                   */
+/* ------------------------------------------------------------------------------------ */
+
+/* argmax with a tie band: first index whose value is within tol of the maximum */
+static int argmax_tol(const double* v, int n, double tol) {
+  double mx = v[0];
+  for (int i = 1; i < n; i++)
+    if (v[i] > mx) mx = v[i];
+  for (int i = 0; i < n; i++)
+    if (v[i] >= mx - tol) return i;
+  return 0;
+}
+#define MANIFOLD_TOL 2e-8
+
+/* mjx collision_convex._manifold_points: 4 points of approximately maximal area */
+static void manifold_points(const double (*poly)[3], const int* mask, int n, const double* nrm, int idx[4]) {
+  double dm[DUCK_MAXHULLV], s[2 * DUCK_MAXHULLV];
+  for (int k = 0; k < n; k++) dm[k] = mask[k] ? 0.0 : -1e6;
+  int a = argmax_tol(dm, n, 0.0);
+  for (int k = 0; k < n; k++) {
+    double dx = poly[a][0] - poly[k][0], dy = poly[a][1] - poly[k][1], dz = poly[a][2] - poly[k][2];
+    s[k] = dx * dx + dy * dy + dz * dz + dm[k];
+  }
+  int b = argmax_tol(s, n, MANIFOLD_TOL);
+  double ab[3], amb[3] = {poly[a][0] - poly[b][0], poly[a][1] - poly[b][1], poly[a][2] - poly[b][2]};
+  cross3(ab, nrm, amb);
+  for (int k = 0; k < n; k++) {
+    double ap[3] = {poly[a][0] - poly[k][0], poly[a][1] - poly[k][1], poly[a][2] - poly[k][2]};
+    s[k] = fabs(dot3(ap, ab)) + dm[k];
+  }
+  int c = argmax_tol(s, n, MANIFOLD_TOL);
+  double ac[3], bc[3];
+  double amc[3] = {poly[a][0] - poly[c][0], poly[a][1] - poly[c][1], poly[a][2] - poly[c][2]};
+  double bmc[3] = {poly[b][0] - poly[c][0], poly[b][1] - poly[c][1], poly[b][2] - poly[c][2]};
+  cross3(ac, nrm, amc);
+  cross3(bc, nrm, bmc);
+  for (int k = 0; k < n; k++) {
+    double bp[3] = {poly[b][0] - poly[k][0], poly[b][1] - poly[k][1], poly[b][2] - poly[k][2]};
+    double ap[3] = {poly[a][0] - poly[k][0], poly[a][1] - poly[k][1], poly[a][2] - poly[k][2]};
+    s[k] = fabs(dot3(bp, bc)) + dm[k];
+    s[n + k] = fabs(dot3(ap, ac)) + dm[k];
+  }
+  int dd = argmax_tol(s, 2 * n, MANIFOLD_TOL) % n;
+  idx[0] = a; idx[1] = b; idx[2] = c; idx[3] = dd;
+}
+
+/* mjx math.make_frame: rows (normal, t1, t2) */
+static void make_frame(double* fr, const double* nin) {
+  double n[3] = {nin[0], nin[1], nin[2]};
+  double nn = norm3(n);
+  if (nn > MINVAL) { n[0] /= nn; n[1] /= nn; n[2] /= nn; }
+  double b[3];
+  if (-0.5 < n[1] && n[1] < 0.5) { b[0] = 0; b[1] = 1; b[2] = 0; } else { b[0] = 0; b[1] = 0; b[2] = 1; }
+  double nb = dot3(n, b);
+  for (int k = 0; k < 3; k++) b[k] -= n[k] * nb;
+  double bn = norm3(b);
+  if (bn > MINVAL) { b[0] /= bn; b[1] /= bn; b[2] /= bn; }
+  double c[3];
+  cross3(c, n, b);
+  memcpy(fr, n, 3 * sizeof(double)); memcpy(fr + 3, b, 3 * sizeof(double)); memcpy(fr + 6, c, 3 * sizeof(double));
+}
+
+static void set_inactive(oracle_data* d, int slot, int g1, int g2) {
+  d->con_dist[slot] = 1.0;
+  d->con_geom1[slot] = g1; d->con_geom2[slot] = g2;
+  memset(d->con_pos[slot], 0, 3 * sizeof(double));
+  double n[3] = {0, 0, 1};
+  make_frame(d->con_frame[slot], n);
+}
+
+/* plane (geom g1) vs convex hull (geom g2): mjx collision_convex plane_convex */
+static void collide_plane_convex(const oracle_model* m, oracle_data* d, int g1, int g2, int slot0) {
+  const double* pp = d->geom_xpos[g1];
+  const double* PR = d->geom_xmat[g1];
+  const double* cp = d->geom_xpos[g2];
+  const double* CR = d->geom_xmat[g2];
+  double n[3] = {PR[2], PR[5], PR[8]};
+  double dif[3] = {pp[0] - cp[0], pp[1] - cp[1], pp[2] - cp[2]};
+  double plane_local[3], n_local[3];
+  mulmtv3(plane_local, CR, dif);
+  mulmtv3(n_local, CR, n);
+  int nv = m->hull_nvert;
+  double support[DUCK_MAXHULLV];
+  double smax = -1e30;
+  for (int k = 0; k < nv; k++) {
+    double t[3] = {plane_local[0] - m->hull_vert[k][0], plane_local[1] - m->hull_vert[k][1],
+                   plane_local[2] - m->hull_vert[k][2]};
+    support[k] = dot3(t, n_local);
+    if (support[k] > smax) smax = support[k];
+  }
+  double thr = smax - 1e-3 > 0 ? smax - 1e-3 : 0;
+  int mask[DUCK_MAXHULLV];
+  for (int k = 0; k < nv; k++) mask[k] = support[k] > thr;
+  int idx[4];
+  manifold_points((const double(*)[3])m->hull_vert, mask, nv, n_local, idx);
+  double fr[9];
+  make_frame(fr, n);
+  for (int c = 0; c < 4; c++) {
+    int k = idx[c], unique = 1;
+    for (int e = 0; e < c; e++)
+      if (idx[e] == k) unique = 0;
+    double dist = unique ? -support[k] : 1.0;
+    double vw[3];
+    mulmv3(vw, CR, m->hull_vert[k]);
+    int s = slot0 + c;
+    for (int a = 0; a < 3; a++) d->con_pos[s][a] = cp[a] + vw[a] - 0.5 * dist * n[a];
+    d->con_dist[s] = dist;
+    memcpy(d->con_frame[s], fr, sizeof(fr));
+    d->con_geom1[s] = g1; d->con_geom2[s] = g2;
+  }
+}
+
+/* convex hull (g1) vs convex hull (g2): separating-axis test over face normals and edge
+ * pairs; on overlap, a 4-point manifold against the reference face (or one edge-edge
+ * point). Declared simplification of mjx's convex-convex clipping. */
+static void collide_convex_convex(const oracle_model* m, oracle_data* d, int g1, int g2, int slot0) {
+  for (int c = 0; c < 4; c++) set_inactive(d, slot0 + c, g1, g2);
+  const double *p1 = d->geom_xpos[g1], *R1 = d->geom_xmat[g1], *p2 = d->geom_xpos[g2], *R2 = d->geom_xmat[g2];
+  double c1[3], c2[3], t[3];
+  mulmv3(t, R1, m->hull_center);
+  for (int a = 0; a < 3; a++) c1[a] = p1[a] + t[a];
+  mulmv3(t, R2, m->hull_center);
+  for (int a = 0; a < 3; a++) c2[a] = p2[a] + t[a];
+  double cc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+  if (norm3(cc) > 2 * m->hull_radius) return;
+  int nv = m->hull_nvert;
+  double V1[DUCK_MAXHULLV][3], V2[DUCK_MAXHULLV][3];
+  for (int k = 0; k < nv; k++) {
+    mulmv3(t, R1, m->hull_vert[k]);
+    for (int a = 0; a < 3; a++) V1[k][a] = p1[a] + t[a];
+    mulmv3(t, R2, m->hull_vert[k]);
+    for (int a = 0; a < 3; a++) V2[k][a] = p2[a] + t[a];
+  }
+  /* best axis: max separation; type 0 = face of 1, 1 = face of 2, 2 = edge pair */
+  double best = -1e30, bu[3] = {0, 0, 1};
+  int btype = -1, bi = -1, bj = -1;
+  for (int side = 0; side < 2; side++) {
+    const double* R = side == 0 ? R1 : R2;
+    for (int f = 0; f < m->hull_nface; f++) {
+      double u[3];
+      mulmv3(u, R, m->hull_face_normal[f]);
+      if (side == 1) { u[0] = -u[0]; u[1] = -u[1]; u[2] = -u[2]; }
+      double mx1 = -1e30, mn2 = 1e30;
+      for (int k = 0; k < nv; k++) {
+        double a1 = dot3(u, V1[k]), a2 = dot3(u, V2[k]);
+        if (a1 > mx1) mx1 = a1;
+        if (a2 < mn2) mn2 = a2;
+      }
+      double sep = mn2 - mx1;
+      if (sep > 0) return;
+      if (sep > best) { best = sep; memcpy(bu, u, sizeof(u)); btype = side; bi = f; }
+    }
+  }
+  for (int e1 = 0; e1 < m->hull_nedge; e1++) {
+    double ea[3], eb[3], tmp[3];
+    for (int a = 0; a < 3; a++) tmp[a] = m->hull_vert[m->hull_edge[e1][1]][a] - m->hull_vert[m->hull_edge[e1][0]][a];
+    mulmv3(ea, R1, tmp);
+    for (int e2 = 0; e2 < m->hull_nedge; e2++) {
+      for (int a = 0; a < 3; a++) tmp[a] = m->hull_vert[m->hull_edge[e2][1]][a] - m->hull_vert[m->hull_edge[e2][0]][a];
+      mulmv3(eb, R2, tmp);
+      double u[3];
+      cross3(u, ea, eb);
+      double un = norm3(u);
+      if (un < 1e-6 * norm3(ea) * norm3(eb)) continue;
+      for (int a = 0; a < 3; a++) u[a] /= un;
+      if (dot3(u, cc) < 0) { u[0] = -u[0]; u[1] = -u[1]; u[2] = -u[2]; }
+      double mx1 = -1e30, mn2 = 1e30;
+      for (int k = 0; k < nv; k++) {
+        double a1 = dot3(u, V1[k]), a2 = dot3(u, V2[k]);
+        if (a1 > mx1) mx1 = a1;
+        if (a2 < mn2) mn2 = a2;
+      }
+      double sep = mn2 - mx1;
+      if (sep > 0) return;
+      if (sep > best + 1e-9) { best = sep; memcpy(bu, u, sizeof(u)); btype = 2; bi = e1; bj = e2; }
+    }
+  }
+  double fr[9];
+  make_frame(fr, bu);
+  if (btype == 2) {
+    /* closest points of the two edge segments */
+    const double *a0 = V1[m->hull_edge[bi][0]], *a1 = V1[m->hull_edge[bi][1]];
+    const double *b0 = V2[m->hull_edge[bj][0]], *b1 = V2[m->hull_edge[bj][1]];
+    double d1[3], d2[3], r[3];
+    for (int a = 0; a < 3; a++) { d1[a] = a1[a] - a0[a]; d2[a] = b1[a] - b0[a]; r[a] = a0[a] - b0[a]; }
+    double A = dot3(d1, d1), E = dot3(d2, d2), F = dot3(d2, r), C = dot3(d1, r), B = dot3(d1, d2);
+    double den = A * E - B * B, s = 0, tt = 0;
+    if (den > MINVAL) s = (B * F - C * E) / den;
+    s = s < 0 ? 0 : (s > 1 ? 1 : s);
+    tt = E > MINVAL ? (B * s + F) / E : 0;
+    if (tt < 0) { tt = 0; s = A > MINVAL ? -C / A : 0; } else if (tt > 1) { tt = 1; s = A > MINVAL ? (B - C) / A : 0; }
+    s = s < 0 ? 0 : (s > 1 ? 1 : s);
+    for (int a = 0; a < 3; a++) d->con_pos[slot0][a] = 0.5 * (a0[a] + s * d1[a] + b0[a] + tt * d2[a]);
+    d->con_dist[slot0] = best;
+    memcpy(d->con_frame[slot0], fr, sizeof(fr));
+    return;
+  }
+  /* face contact: vertices of the incident hull past the reference face plane */
+  double (*Vi)[3] = btype == 0 ? V2 : V1;
+  const double* Rr = btype == 0 ? R1 : R2;
+  const double* pr = btype == 0 ? p1 : p2;
+  double fn[3], off;
+  mulmv3(fn, Rr, m->hull_face_normal[bi]);
+  off = m->hull_face_offset[bi] + dot3(fn, pr);  /* world plane: fn . x = off (fn outward of ref hull) */
+  double support[DUCK_MAXHULLV], smax = -1e30;
+  for (int k = 0; k < nv; k++) {
+    support[k] = off - dot3(fn, Vi[k]);  /* depth of incident vertex inside the reference face */
+    if (support[k] > smax) smax = support[k];
+  }
+  double thr = smax - 1e-3 > 0 ? smax - 1e-3 : 0;
+  int mask[DUCK_MAXHULLV], idx[4];
+  for (int k = 0; k < nv; k++) mask[k] = support[k] > thr;
+  manifold_points((const double(*)[3])Vi, mask, nv, fn, idx);
+  for (int c = 0; c < 4; c++) {
+    int k = idx[c], unique = 1;
+    for (int e = 0; e < c; e++)
+      if (idx[e] == k) unique = 0;
+    double dist = unique ? -support[k] : 1.0;
+    int s = slot0 + c;
+    for (int a = 0; a < 3; a++) d->con_pos[s][a] = Vi[k][a] - 0.5 * dist * fn[a];
+    d->con_dist[s] = dist;
+    memcpy(d->con_frame[s], fr, sizeof(fr));
+  }
+}
+
+static void collision(const oracle_model* m, oracle_data* d) {
+  d->ncon = m->npair * DUCK_CON_PER_PAIR;
+  for (int p = 0; p < m->npair; p++) {
+    int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p], t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+    int s0 = p * DUCK_CON_PER_PAIR;
+    if (t1 == DUCK_GEOM_PLANE && t2 == DUCK_GEOM_MESH) collide_plane_convex(m, d, g1, g2, s0);
+    else if (t1 == DUCK_GEOM_MESH && t2 == DUCK_GEOM_MESH) collide_convex_convex(m, d, g1, g2, s0);
+    else
+      for (int c = 0; c < 4; c++) set_inactive(d, s0 + c, g1, g2); /* hfield: not yet supported */
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* constraints (mjx constraint.make_constraint semantics)                               */
+/* ------------------------------------------------------------------------------------ */
+
+static void kbi(const oracle_model* m, const double* solref, const double* solimp, double pos, double* k,
+                double* b, double* imp) {
+  double timeconst = solref[0], dampratio = solref[1];
+  if (timeconst < 2 * m->timestep) timeconst = 2 * m->timestep; /* refsafe */
+  double dmin = fmin(fmax(solimp[0], MINIMP), MAXIMP), dmax = fmin(fmax(solimp[1], MINIMP), MAXIMP);
+  double width = fmax(MINVAL, solimp[2]), mid = fmin(fmax(solimp[3], MINIMP), MAXIMP), power = fmax(1.0, solimp[4]);
+  *k = 1.0 / (dmax * dmax * timeconst * timeconst * dampratio * dampratio);
+  *b = 2.0 / (dmax * timeconst);
+  if (solref[0] <= 0) *k = -solref[0] / (dmax * dmax);
+  if (solref[1] <= 0) *b = -solref[1] / dmax;
+  double x = fabs(pos) / width;
+  double ya = (1.0 / pow(mid, power - 1)) * pow(x, power);
+  double yb = 1 - (1.0 / pow(1 - mid, power - 1)) * pow(1 - x, power);
+  double y = x < mid ? ya : yb;
+  double im = dmin + y * (dmax - dmin);
+  im = fmin(fmax(im, dmin), dmax);
+  if (x > 1.0) im = dmax;
+  *imp = im;
+}
+
+static void add_row(const oracle_model* m, oracle_data* d, fwd_ws* w, const double* J, double pos,
+                    double invweight, const double* solref, const double* solimp, double frictionloss, int ineq) {
+  int r = w->nefc++;
+  memcpy(w->J[r], J, sizeof(double) * NV);
+  double k, b, imp;
+  kbi(m, solref, solimp, pos, &k, &b, &imp);
+  double R = fmax(invweight * (1 - imp) / imp, MINVAL);
+  double vel = 0;
+  for (int i = 0; i < m->nv; i++) vel += J[i] * d->qvel[i];
+  w->R[r] = R;
+  w->D[r] = 1.0 / R;
+  w->aref[r] = -b * vel - k * imp * pos;
+  w->frictionloss[r] = frictionloss;
+  w->ineq[r] = ineq;
+}
+
+/* translational jacobian of a world point attached to body b (mj_jac, via cdof) */
+static void jac_point(const oracle_model* m, const fwd_ws* w, int b, const double* p, double (*Jp)[NV]) {
+  for (int a = 0; a < 3; a++) memset(Jp[a], 0, sizeof(double) * NV);
+  if (m->body_weldid[b] == 0) return;
+  int wb = m->body_weldid[b];
+  const double* c = w->subtree_com[m->body_rootid[b]];
+  double off[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]};
+  for (int dof = m->body_dofadr[wb] + m->body_dofnum[wb] - 1; dof >= 0; dof = m->dof_parentid[dof]) {
+    double t[3];
+    cross3(t, w->cdof[dof], off);
+    for (int a = 0; a < 3; a++) Jp[a][dof] = w->cdof[dof][3 + a] + t[a];
+  }
+}
+
+static void make_constraint(const oracle_model* m, oracle_data* d, fwd_ws* w) {
+  w->nefc = 0;
+  double J[NV];
+  /* dof friction loss rows (mjx _instantiate_friction) */
+  for (int i = 0; i < m->nv; i++) {
+    if (!m->dof_has_friction[i]) continue;
+    memset(J, 0, sizeof(J));
+    J[i] = 1;
+    add_row(m, d, w, J, 0.0, m->dof_invweight0[i], m->dof_solref[i], m->dof_solimp[i], m->dof_frictionloss[i], 0);
+  }
+  /* joint limits (mjx _instantiate_limit_slide_hinge): one row per joint, closer side */
+  for (int j = 0; j < m->njnt; j++) {
+    if (!m->jnt_limited[j] || (m->jnt_type[j] != DUCK_JNT_HINGE && m->jnt_type[j] != DUCK_JNT_SLIDE)) continue;
+    double q = d->qpos[m->jnt_qposadr[j]];
+    double dlo = q - m->jnt_range[j][0], dhi = m->jnt_range[j][1] - q;
+    double pos = (dlo < dhi ? dlo : dhi) - m->jnt_margin[j];
+    if (!(pos < 0)) continue;
+    int dof = m->jnt_dofadr[j];
+    memset(J, 0, sizeof(J));
+    J[dof] = dlo < dhi ? 1.0 : -1.0;
+    add_row(m, d, w, J, pos, m->dof_invweight0[dof], m->jnt_solref[j], m->jnt_solimp[j], 0.0, 1);
+  }
+  /* contacts, pyramidal cone (mjx _instantiate_contact) */
+  for (int p = 0; p < m->npair; p++) {
+    int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
+    int b1 = m->geom_bodyid[g1], b2 = m->geom_bodyid[g2];
+    double tran = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+    const double* fri = m->pair_friction[p];
+    int dim = m->pair_condim[p];
+    for (int c = 0; c < DUCK_CON_PER_PAIR; c++) {
+      int s = p * DUCK_CON_PER_PAIR + c;
+      double pos = d->con_dist[s] - m->pair_margin[p];
+      if (!(pos < 0)) continue;
+      double J1[3][NV], J2[3][NV], Jd[3][NV];
+      jac_point(m, w, b1, d->con_pos[s], J1);
+      jac_point(m, w, b2, d->con_pos[s], J2);
+      for (int a = 0; a < 3; a++)
+        for (int i = 0; i < NV; i++) Jd[a][i] = J2[a][i] - J1[a][i];
+      const double* fr = d->con_frame[s];
+      double Jf[3][NV];
+      for (int r = 0; r < 3; r++)
+        for (int i = 0; i < NV; i++) Jf[r][i] = fr[3 * r] * Jd[0][i] + fr[3 * r + 1] * Jd[1][i] + fr[3 * r + 2] * Jd[2][i];
+      for (int t = 0; t < dim - 1; t++) {
+        double mu = fri[t];
+        double iw = (tran + mu * mu * tran) * 2 * fri[0] * fri[0] / m->impratio;
+        for (int sgn = 0; sgn < 2; sgn++) {
+          for (int i = 0; i < NV; i++) J[i] = Jf[0][i] + (sgn == 0 ? mu : -mu) * Jf[1 + t][i];
+          add_row(m, d, w, J, pos, iw, m->pair_solref[p], m->pair_solimp[p], 0.0, 1);
+        }
+      }
+    }
+  }
+  d->nefc = w->nefc;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Newton solver (mjx solver.solve, iterations = opt.iterations, zoom line search)      */
+/* ------------------------------------------------------------------------------------ */
+
+typedef struct sctx {
+  double qacc[NV], Ma[NV], Jaref[MAXEFC], efc_force[MAXEFC], qfrc_constraint[NV];
+  double grad[NV], Mgrad[NV], search[NV];
+  double cost, gauss, prev_cost;
+} sctx;
+
+static void mulM(const oracle_model* m, const oracle_data* d, const double* x, double* y) {
+  for (int i = 0; i < m->nv; i++) {
+    double s = 0;
+    for (int j = 0; j < m->nv; j++) s += d->qM[i][j] * x[j];
+    y[i] = s;
+  }
+}
+
+/* _update_constraint: forces and cost at ctx.qacc */
+static void update_constraint(const oracle_model* m, const oracle_data* d, const fwd_ws* w, sctx* c) {
+  double cost = 0;
+  for (int r = 0; r < w->nefc; r++) {
+    double x = c->Jaref[r], D = w->D[r];
+    if (w->ineq[r]) {
+      if (x < 0) { c->efc_force[r] = -D * x; cost += 0.5 * D * x * x; } else c->efc_force[r] = 0;
+    } else {
+      double f = w->frictionloss[r], rf = w->R[r] * f;
+      if (x <= -rf) { c->efc_force[r] = f; cost += -f * x - 0.5 * rf * f; }
+      else if (x >= rf) { c->efc_force[r] = -f; cost += f * x - 0.5 * rf * f; }
+      else { c->efc_force[r] = -D * x; cost += 0.5 * D * x * x; }
+    }
+  }
+  double gauss = 0;
+  for (int i = 0; i < m->nv; i++) gauss += 0.5 * (c->Ma[i] - d->qfrc_smooth[i]) * (c->qacc[i] - d->qacc_smooth[i]);
+  for (int i = 0; i < m->nv; i++) {
+    double s = 0;
+    for (int r = 0; r < w->nefc; r++) s += w->J[r][i] * c->efc_force[r];
+    c->qfrc_constraint[i] = s;
+  }
+  c->prev_cost = c->cost;
+  c->gauss = gauss;
+  c->cost = gauss + cost;
+}
+
+/* _update_gradient (Newton): grad and H^-1 grad with H = M + J' diag(D*active) J */
+static void update_gradient(const oracle_model* m, const oracle_data* d, const fwd_ws* w, sctx* c) {
+  int nv = m->nv;
+  for (int i = 0; i < nv; i++) c->grad[i] = c->Ma[i] - d->qfrc_smooth[i] - c->qfrc_constraint[i];
+  double H[NV * NV];
+  for (int i = 0; i < nv; i++)
+    for (int j = 0; j < nv; j++) H[i * NV + j] = d->qM[i][j];
+  for (int r = 0; r < w->nefc; r++) {
+    double x = c->Jaref[r];
+    int active;
+    if (w->ineq[r]) active = x < 0;
+    else { double rf = w->R[r] * w->frictionloss[r]; active = (x > -rf) && (x < rf); }
+    if (!active) continue;
+    for (int i = 0; i < nv; i++) {
+      if (w->J[r][i] == 0) continue;
+      double a = w->D[r] * w->J[r][i];
+      for (int j = 0; j < nv; j++) H[i * NV + j] += a * w->J[r][j];
+    }
+  }
+  cholesky(H, nv);
+  memcpy(c->Mgrad, c->grad, sizeof(double) * nv);
+  chol_solve(H, nv, c->Mgrad);
+}
+
+typedef struct lspt { double alpha, cost, d0, d1; } lspt;
+
+static lspt ls_eval(const oracle_model* m, const fwd_ws* w, const sctx* c, const double* jv, const double qg[3],
+                    double alpha) {
+  double q0 = qg[0], q1 = qg[1], q2 = qg[2];
+  for (int r = 0; r < w->nefc; r++) {
+    double x = c->Jaref[r] + alpha * jv[r], D = w->D[r], ja = c->Jaref[r], v = jv[r];
+    if (w->ineq[r]) {
+      if (x < 0) { q0 += 0.5 * D * ja * ja; q1 += D * v * ja; q2 += 0.5 * D * v * v; }
+    } else {
+      double f = w->frictionloss[r], rf = w->R[r] * f;
+      if (x <= -rf) { q0 += -0.5 * rf * f - f * ja; q1 += -f * v; }
+      else if (x >= rf) { q0 += -0.5 * rf * f + f * ja; q1 += f * v; }
+      else { q0 += 0.5 * D * ja * ja; q1 += D * v * ja; q2 += 0.5 * D * v * v; }
+    }
+  }
+  lspt p;
+  p.alpha = alpha;
+  p.cost = alpha * alpha * q2 + alpha * q1 + q0;
+  p.d0 = 2 * alpha * q2 + q1;
+  p.d1 = 2 * q2;
+  return p;
+}
+
+static void linesearch(const oracle_model* m, const oracle_data* d, const fwd_ws* w, sctx* c) {
+  int nv = m->nv;
+  double snorm = 0;
+  for (int i = 0; i < nv; i++) snorm += c->search[i] * c->search[i];
+  snorm = sqrt(snorm);
+  double smag = snorm * m->meaninertia * (nv > 1 ? nv : 1);
+  double gtol = m->tolerance * m->ls_tolerance * smag;
+  double mv[NV], jv[MAXEFC];
+  mulM(m, d, c->search, mv);
+  for (int r = 0; r < w->nefc; r++) {
+    double s = 0;
+    for (int i = 0; i < nv; i++) s += w->J[r][i] * c->search[i];
+    jv[r] = s;
+  }
+  double qg[3];
+  double sMa = 0, sf = 0, sMv = 0;
+  for (int i = 0; i < nv; i++) { sMa += c->search[i] * c->Ma[i]; sf += c->search[i] * d->qfrc_smooth[i]; sMv += c->search[i] * mv[i]; }
+  qg[0] = c->gauss; qg[1] = sMa - sf; qg[2] = 0.5 * sMv;
+
+  lspt p0 = ls_eval(m, w, c, jv, qg, 0.0);
+  lspt lo = ls_eval(m, w, c, jv, qg, p0.alpha - p0.d0 / p0.d1);
+  lspt hi;
+  if (lo.d0 < p0.d0) { hi = p0; } else { hi = lo; lo = p0; }
+  int swap = 1, iter = 0;
+  for (;;) {
+    int done = iter >= m->ls_iterations;
+    done |= !swap;
+    done |= (lo.d0 < 0) && (lo.d0 > -gtol);
+    done |= (hi.d0 > 0) && (hi.d0 < gtol);
+    if (done) break;
+    lspt lo_next = ls_eval(m, w, c, jv, qg, lo.alpha - lo.d0 / lo.d1);
+    lspt hi_next = ls_eval(m, w, c, jv, qg, hi.alpha - hi.d0 / hi.d1);
+    lspt mid = ls_eval(m, w, c, jv, qg, 0.5 * (lo.alpha + hi.alpha));
+    int s1 = (lo.d0 > 0) || (lo.d0 < lo_next.d0);
+    if (s1) lo = lo_next;
+    int s2 = (mid.d0 < 0) && (lo.d0 < mid.d0);
+    if (s2) lo = mid;
+    int s3 = (hi.d0 < 0) || (hi.d0 > hi_next.d0);
+    if (s3) hi = hi_next;
+    int s4 = (mid.d0 > 0) && (hi.d0 > mid.d0);
+    if (s4) hi = mid;
+    swap = s1 || s2 || s3 || s4;
+    iter++;
+  }
+  int improved = (lo.cost < p0.cost) || (hi.cost < p0.cost);
+  double alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+  if (improved) {
+    for (int i = 0; i < nv; i++) { c->qacc[i] += c->search[i] * alpha; c->Ma[i] += mv[i] * alpha; }
+    for (int r = 0; r < w->nefc; r++) c->Jaref[r] += jv[r] * alpha;
+  }
+}
+
+static void ctx_init(const oracle_model* m, const oracle_data* d, const fwd_ws* w, sctx* c, const double* qacc) {
+  memcpy(c->qacc, qacc, sizeof(double) * m->nv);
+  mulM(m, d, c->qacc, c->Ma);
+  for (int r = 0; r < w->nefc; r++) {
+    double s = 0;
+    for (int i = 0; i < m->nv; i++) s += w->J[r][i] * c->qacc[i];
+    c->Jaref[r] = s - w->aref[r];
+  }
+  c->cost = 0;
+  update_constraint(m, d, w, c);
+}
+
+static void solve(const oracle_model* m, oracle_data* d, const fwd_ws* w) {
+  int nv = m->nv;
+  if (w->nefc == 0) {
+    memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv);
+    memset(d->qfrc_constraint, 0, sizeof(double) * nv);
+    memcpy(d->qacc_warmstart, d->qacc, sizeof(double) * nv);
+    return;
+  }
+  sctx warm, smth, *c;
+  ctx_init(m, d, w, &warm, d->qacc_warmstart);
+  ctx_init(m, d, w, &smth, d->qacc_smooth);
+  c = warm.cost < smth.cost ? &warm : &smth;
+  update_gradient(m, d, w, c);
+  for (int i = 0; i < nv; i++) c->search[i] = -c->Mgrad[i];
+  int it = 0;
+  for (;;) {
+    linesearch(m, d, w, c);
+    update_constraint(m, d, w, c);
+    it++;
+    if (it >= m->iterations) break;
+    update_gradient(m, d, w, c);
+    double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+    double improvement = scale * (c->prev_cost - c->cost);
+    double gn = 0;
+    for (int i = 0; i < nv; i++) gn += c->grad[i] * c->grad[i];
+    double gradient = scale * sqrt(gn);
+    if (improvement < m->tolerance || gradient < m->tolerance) break;
+    for (int i = 0; i < nv; i++) c->search[i] = -c->Mgrad[i];
+  }
+  d->solver_niter = it;
+  memcpy(d->qacc, c->qacc, sizeof(double) * nv);
+  memcpy(d->qfrc_constraint, c->qfrc_constraint, sizeof(double) * nv);
+  memcpy(d->efc_force, c->efc_force, sizeof(double) * w->nefc);
+  memcpy(d->qacc_warmstart, d->qacc, sizeof(double) * nv);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* sensors                                                                              */
+/* ------------------------------------------------------------------------------------ */
+
+static void site_vel(const oracle_model* m, const oracle_data* d, const fwd_ws* w, int s, double* ang, double* lin) {
+  int b = m->site_bodyid[s];
+  const double* cv = w->cvel[b];
+  const double* c = w->subtree_com[m->body_rootid[b]];
+  double off[3] = {d->site_xpos[s][0] - c[0], d->site_xpos[s][1] - c[1], d->site_xpos[s][2] - c[2]};
+  double t[3];
+  cross3(t, cv, off);
+  for (int a = 0; a < 3; a++) { ang[a] = cv[a]; lin[a] = cv[3 + a] + t[a]; }
+}
+
+static void sensors(const oracle_model* m, oracle_data* d, const fwd_ws* w, int stage_acc) {
+  double cacc[DUCK_MAXBODY][6];
+  if (stage_acc) { /* mj_rnePostConstraint: com-based accelerations incl. -gravity */
+    memset(cacc[0], 0, 6 * sizeof(double));
+    for (int k = 0; k < 3; k++) cacc[0][3 + k] = -m->gravity[k];
+    for (int i = 1; i < m->nbody; i++) {
+      memcpy(cacc[i], cacc[m->body_parentid[i]], 6 * sizeof(double));
+      for (int j = 0; j < m->body_dofnum[i]; j++) {
+        int dof = m->body_dofadr[i] + j;
+        for (int c = 0; c < 6; c++) cacc[i][c] += w->cdof_dot[dof][c] * d->qvel[dof] + w->cdof[dof][c] * d->qacc[dof];
+      }
+    }
+  }
+  for (int i = 0; i < m->nsensor; i++) {
+    int s = m->sensor_objid[i], adr = m->sensor_adr[i], typ = m->sensor_type[i];
+    double* out = d->sensordata + adr;
+    const double* R = d->site_xmat[s];
+    double ang[3], lin[3];
+    if (typ == DUCK_SENS_ACCELEROMETER) {
+      if (!stage_acc) continue;
+      int b = m->site_bodyid[s];
+      const double* c = w->subtree_com[m->body_rootid[b]];
+      double off[3] = {d->site_xpos[s][0] - c[0], d->site_xpos[s][1] - c[1], d->site_xpos[s][2] - c[2]};
+      double t[3], acc[3];
+      cross3(t, cacc[b], off);
+      for (int a = 0; a < 3; a++) acc[a] = cacc[b][3 + a] + t[a];
+      site_vel(m, d, w, s, ang, lin);
+      cross3(t, ang, lin);
+      for (int a = 0; a < 3; a++) acc[a] += t[a];
+      mulmtv3(out, R, acc);
+      continue;
+    }
+    if (stage_acc) continue;
+    switch (typ) {
+      case DUCK_SENS_GYRO: site_vel(m, d, w, s, ang, lin); mulmtv3(out, R, ang); break;
+      case DUCK_SENS_VELOCIMETER: site_vel(m, d, w, s, ang, lin); mulmtv3(out, R, lin); break;
+      case DUCK_SENS_FRAMEZAXIS: out[0] = R[2]; out[1] = R[5]; out[2] = R[8]; break;
+      case DUCK_SENS_FRAMEXAXIS: out[0] = R[0]; out[1] = R[3]; out[2] = R[6]; break;
+      case DUCK_SENS_FRAMELINVEL: site_vel(m, d, w, s, ang, lin); memcpy(out, lin, sizeof(lin)); break;
+      case DUCK_SENS_FRAMEANGVEL: site_vel(m, d, w, s, ang, lin); memcpy(out, ang, sizeof(ang)); break;
+      case DUCK_SENS_FRAMEPOS: memcpy(out, d->site_xpos[s], 3 * sizeof(double)); break;
+      case DUCK_SENS_FRAMEQUAT: memcpy(out, w->site_xquat[s], 4 * sizeof(double)); break;
+      default: break;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* forward / step                                                                       */
+/* ------------------------------------------------------------------------------------ */
+
+static void forward_ws(const oracle_model* m, oracle_data* d, fwd_ws* w) {
+  int nv = m->nv;
+  kinematics(m, d, w);
+  com_pos(m, d, w);
+  crb(m, d, w);
+  collision(m, d);
+  make_constraint(m, d, w);
+  com_vel(m, d, w);
+  sensors(m, d, w, 0);
+  /* passive: explicit joint damping (springs are zero in these models) */
+  for (int i = 0; i < nv; i++) d->qfrc_passive[i] = -m->dof_damping[i] * d->qvel[i];
+  rne_bias(m, d, w);
+  /* actuation: <position> servos (mjx forward.fwd_actuation) */
+  memset(d->qfrc_actuator, 0, sizeof(double) * nv);
+  for (int a = 0; a < m->nu; a++) {
+    int j = m->actuator_trnid[a];
+    double ctrl = d->ctrl[a];
+    if (m->actuator_ctrllimited[a]) ctrl = fmin(fmax(ctrl, m->actuator_ctrlrange[a][0]), m->actuator_ctrlrange[a][1]);
+    double gear = m->actuator_gear[a];
+    double len = gear * d->qpos[m->jnt_qposadr[j]], vel = gear * d->qvel[m->jnt_dofadr[j]];
+    double f = m->actuator_kp[a] * ctrl - m->actuator_kp[a] * len - m->actuator_kv[a] * vel;
+    if (m->actuator_forcelimited[a]) f = fmin(fmax(f, m->actuator_forcerange[a][0]), m->actuator_forcerange[a][1]);
+    d->actuator_force[a] = f;
+    d->qfrc_actuator[m->jnt_dofadr[j]] += gear * f;
+  }
+  /* smooth acceleration */
+  for (int i = 0; i < nv; i++) d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i];
+  double L[NV * NV];
+  for (int i = 0; i < nv; i++)
+    for (int j = 0; j < nv; j++) L[i * NV + j] = d->qM[i][j];
+  cholesky(L, nv);
+  memcpy(d->qacc_smooth, d->qfrc_smooth, sizeof(double) * nv);
+  chol_solve(L, nv, d->qacc_smooth);
+  solve(m, d, w);
+  sensors(m, d, w, 1);
+}
+
+void oracle_forward(const oracle_model* m, oracle_data* d) {
+  fwd_ws w;
+  forward_ws(m, d, &w);
+}
+
+/* mj_Euler with eulerdamp disabled (integrator.euler -> _advance), semi-implicit */
+static void euler(const oracle_model* m, oracle_data* d) {
+  double dt = m->timestep;
+  for (int i = 0; i < m->nv; i++) d->qvel[i] += dt * d->qacc[i];
+  for (int j = 0; j < m->njnt; j++) {
+    int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+    if (m->jnt_type[j] == DUCK_JNT_FREE) {
+      for (int k = 0; k < 3; k++) d->qpos[qa + k] += dt * d->qvel[da + k];
+      double* q = d->qpos + qa + 3;
+      double v[3] = {d->qvel[da + 3], d->qvel[da + 4], d->qvel[da + 5]};
+      double nv = norm3(v), axis[3] = {1, 0, 0};
+      if (nv > MINVAL) { axis[0] = v[0] / nv; axis[1] = v[1] / nv; axis[2] = v[2] / nv; }
+      double qr[4];
+      axis_angle_quat(qr, axis, dt * nv);
+      quat_mul(q, q, qr);
+      quat_normalize(q);
+    } else {
+      d->qpos[qa] += dt * d->qvel[da];
+    }
+  }
+}
+
+void oracle_step(const oracle_model* m, oracle_data* d, int nsubstep) {
+  for (int s = 0; s < nsubstep; s++) {
+    oracle_forward(m, d);
+    euler(m, d);
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* RNG: threefry2x32 with 20 rounds                                                     */
+/* ------------------------------------------------------------------------------------ */
+
+static uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+void oracle_threefry2x32(const uint32_t key[2], const uint32_t ctr[2], uint32_t out[2]) {
+  static const int R[8] = {13, 15, 26, 6, 17, 29, 16, 24};
+  uint32_t ks[3] = {key[0], key[1], 0x1BD11BDAu ^ key[0] ^ key[1]};
+  uint32_t x0 = ctr[0] + ks[0], x1 = ctr[1] + ks[1];
+  for (int r = 0; r < 20; r++) {
+    x0 += x1;
+    x1 = rotl32(x1, R[r % 8]);
+    x1 ^= x0;
+    if (r % 4 == 3) {
+      uint32_t s = (uint32_t)(r / 4 + 1);
+      x0 += ks[s % 3];
+      x1 += ks[(s + 1) % 3] + s;
+    }
+  }
+  out[0] = x0; out[1] = x1;
+}
+
+typedef struct rng_t { uint32_t key[2]; uint32_t ctr; } rng_t;
+
+/* slot k of counter ctr -> uniform in [0,1) with 23 random bits (exact in fp32) */
+static double rng_u(const rng_t* r, int slot) {
+  uint32_t c[2] = {r->ctr, (uint32_t)(slot >> 1)}, o[2];
+  oracle_threefry2x32(r->key, c, o);
+  return (double)(o[slot & 1] >> 9) * (1.0 / 8388608.0);
+}
+static double rng_uniform(const rng_t* r, int slot, double lo, double hi) {
+  return (double)(float)(lo + (hi - lo) * rng_u(r, slot));
+}
+static int rng_randint(const rng_t* r, int slot, int lo, int hi) {
+  int k = (int)floor(rng_u(r, slot) * (hi - lo));
+  if (k > hi - lo - 1) k = hi - lo - 1;
+  return lo + k;
+}
+static void derive_key(uint64_t seed, int64_t env_id, uint32_t tag, uint32_t out[2]) {
+  uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t c[2] = {(uint32_t)env_id, tag ^ (uint32_t)((uint64_t)env_id >> 32)};
+  oracle_threefry2x32(k, c, out);
+}
+
+/* per-step slot map (documented in DESIGN.md) */
+enum {
+  SLOT_ACTION_DELAY = 0, SLOT_PUSH_THETA = 1, SLOT_PUSH_MAG = 2, SLOT_GYRO = 3, SLOT_ACCEL = 6,
+  SLOT_GRAVITY = 9, SLOT_IMU_IDX = 12, SLOT_QPOS = 13, SLOT_QVEL = 29, SLOT_CMD = 45
+};
+/* reset slot map */
+enum { RSLOT_DXY = 0, RSLOT_YAW = 2, RSLOT_QSCALE = 3, RSLOT_QVEL = 19, RSLOT_CMD = 25, RSLOT_PUSH = 33, RSLOT_OBS = 64 };
+#define KEY_TAG_ENV 0x5EEDu
+#define KEY_TAG_DR 0xD0D0u
+
+/* ------------------------------------------------------------------------------------ */
+/* domain randomisation (randomize.py:26-146)                                            */
+/* ------------------------------------------------------------------------------------ */
+
+void oracle_dr_sample(const oracle_model* m, uint64_t seed, int64_t env_id, double* dr) {
+  duck_dr_layout L = duck_dr_layout_make(m->nbody, m->nu);
+  rng_t r;
+  derive_key(seed, env_id, KEY_TAG_DR, r.key);
+  r.ctr = 0;
+  int slot = 0;
+  dr[L.floor_friction] = rng_uniform(&r, slot++, 0.5, 1.0);
+  for (int a = 0; a < m->nu; a++) dr[L.frictionloss + a] = rng_uniform(&r, slot++, 0.9, 1.1);
+  for (int a = 0; a < m->nu; a++) dr[L.armature + a] = rng_uniform(&r, slot++, 1.0, 1.05);
+  for (int k = 0; k < 3; k++) dr[L.base_ipos + k] = rng_uniform(&r, slot++, -0.05, 0.05);
+  for (int b = 0; b < m->nbody; b++) dr[L.body_mass + b] = rng_uniform(&r, slot++, 0.9, 1.1);
+  double dmass = rng_uniform(&r, slot++, -0.1, 0.1);
+  for (int a = 0; a < m->nu; a++) dr[L.qpos0 + a] = rng_uniform(&r, slot++, -0.03, 0.03);
+  for (int a = 0; a < m->nu; a++) dr[L.kp + a] = rng_uniform(&r, slot++, 0.9, 1.1);
+  /* convert factors to absolute values of the randomised model */
+  for (int a = 0; a < m->nu; a++) {
+    int dof = m->jnt_dofadr[m->actuator_trnid[a]];
+    int qa = m->jnt_qposadr[m->actuator_trnid[a]];
+    dr[L.frictionloss + a] *= m->dof_frictionloss[dof];
+    dr[L.armature + a] *= m->dof_armature[dof];
+    dr[L.qpos0 + a] += m->qpos0[qa];
+    dr[L.kp + a] *= m->actuator_kp[a];
+  }
+  for (int k = 0; k < 3; k++) dr[L.base_ipos + k] += m->body_ipos[1][k];
+  for (int b = 0; b < m->nbody; b++) dr[L.body_mass + b] *= m->body_mass[b];
+  dr[L.body_mass + 1] += dmass;
+}
+
+oracle_model* oracle_model_randomized(const oracle_model* m, const double* dr) {
+  duck_dr_layout L = duck_dr_layout_make(m->nbody, m->nu);
+  oracle_model* r = (oracle_model*)malloc(sizeof(oracle_model));
+  memcpy(r, m, sizeof(oracle_model));
+  if (m->hfield_data) {
+    r->hfield_data = (double*)malloc(sizeof(double) * (size_t)m->hfield_nrow * m->hfield_ncol);
+    memcpy(r->hfield_data, m->hfield_data, sizeof(double) * (size_t)m->hfield_nrow * m->hfield_ncol);
+  }
+  for (int k = 0; k < 3; k++) r->body_ipos[1][k] = dr[L.base_ipos + k];
+  for (int b = 0; b < m->nbody; b++) r->body_mass[b] = dr[L.body_mass + b];
+  for (int a = 0; a < m->nu; a++) {
+    int j = m->actuator_trnid[a];
+    r->dof_frictionloss[m->jnt_dofadr[j]] = dr[L.frictionloss + a];
+    r->dof_armature[m->jnt_dofadr[j]] = dr[L.armature + a];
+    r->qpos0[m->jnt_qposadr[j]] = dr[L.qpos0 + a];
+    r->actuator_kp[a] = dr[L.kp + a];
+  }
+  return r;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* env: reference motion, rewards, obs, reset, step                                     */
+/* ------------------------------------------------------------------------------------ */
+
+static int nearest(const float* grid, int n, double v) {
+  int best = 0;
+  double bd = fabs((double)grid[0] - v);
+  for (int i = 1; i < n; i++) {
+    double dd = fabs((double)grid[i] - v);
+    if (dd < bd) { bd = dd; best = i; }
+  }
+  return best;
+}
+
+/* PolyReferenceMotion.get_reference_motion (poly_reference_motion.py:148-168) */
+void oracle_reference_motion(const duck_refmotion* ref, double dx, double dy, double dth, int i, double out[40]) {
+  dx = fmin(fmax(dx, ref->dx_range[0]), ref->dx_range[1]);
+  dy = fmin(fmax(dy, ref->dy_range[0]), ref->dy_range[1]);
+  dth = fmin(fmax(dth, ref->dtheta_range[0]), ref->dtheta_range[1]);
+  int ix = nearest(ref->dxs, ref->n_dx, dx), iy = nearest(ref->dys, ref->n_dy, dy),
+      it = nearest(ref->dthetas, ref->n_dtheta, dth);
+  int nb = ref->nb_steps_in_period;
+  double t = (double)(((i % nb) + nb) % nb) / nb;
+  t = fmin(fmax(t, 0.0), 1.0);
+  const double* c = ref->coeffs + ((size_t)((ix * ref->n_dy + iy) * ref->n_dtheta + it)) * ref->n_dim * ref->n_coef;
+  for (int d = 0; d < ref->n_dim && d < 40; d++) {
+    /* np.polyval on the flipped (descending) coefficients = Horner from the top power */
+    double acc = 0;
+    for (int k = ref->n_coef - 1; k >= 0; k--) acc = acc * t + c[d * ref->n_coef + k];
+    out[d] = acc;
+  }
+}
+
+static double nan_to_num(double x) {
+  if (isnan(x)) return 0.0;
+  if (isinf(x)) return x > 0 ? 3.4028234663852886e38 : -3.4028234663852886e38;
+  return x;
+}
+
+/* custom_rewards.reward_imitation (custom_rewards.py:4-148), use_imitation_reward = True */
+double oracle_reward_imitation(const double base_qpos[7], const double base_qvel[6], const double* jq,
+                               const double* jqd, const double contacts[2], const double* ref,
+                               const double cmd[7], int nu) {
+  (void)base_qpos;
+  double cmd_norm = sqrt(cmd[0] * cmd[0] + cmd[1] * cmd[1] + cmd[2] * cmd[2]);
+  double lxy = 0, ax = 0;
+  for (int k = 0; k < 2; k++) lxy += (base_qvel[k] - ref[34 + k]) * (base_qvel[k] - ref[34 + k]);
+  double lin_xy = exp(-8.0 * lxy);
+  double lin_z = exp(-8.0 * (base_qvel[2] - ref[36]) * (base_qvel[2] - ref[36]));
+  for (int k = 0; k < 2; k++) ax += (base_qvel[3 + k] - ref[37 + k]) * (base_qvel[3 + k] - ref[37 + k]);
+  double ang_xy = exp(-2.0 * ax) * 0.5;
+  double ang_z = exp(-2.0 * (base_qvel[5] - ref[39]) * (base_qvel[5] - ref[39])) * 0.5;
+  /* legs only: ref dims [0:5] + [11:16] vs joints [0:5] + [9:14] */
+  double jp = 0, jv = 0;
+  for (int k = 0; k < 5; k++) {
+    jp += (jq[k] - ref[k]) * (jq[k] - ref[k]);
+    jp += (jq[nu - 5 + k] - ref[11 + k]) * (jq[nu - 5 + k] - ref[11 + k]);
+    jv += (jqd[k] - ref[16 + k]) * (jqd[k] - ref[16 + k]);
+    jv += (jqd[nu - 5 + k] - ref[27 + k]) * (jqd[nu - 5 + k] - ref[27 + k]);
+  }
+  double joint_pos = -jp * 15.0, joint_vel = -jv * 1e-3;
+  double contact = 0;
+  for (int k = 0; k < 2; k++) contact += (contacts[k] == (ref[32 + k] > 0.5 ? 1.0 : 0.0)) ? 1.0 : 0.0;
+  double r = lin_xy + lin_z + ang_xy + ang_z + joint_pos + joint_vel + contact;
+  r *= cmd_norm > 0.01 ? 1.0 : 0.0;
+  return nan_to_num(r);
+}
+
+/* common/rewards.py terms used by joystick.py:634-667 (unscaled):
+ * out = {tracking_lin_vel, tracking_ang_vel, torques, action_rate, stand_still} */
+void oracle_rewards(const double cmd[7], const double lv[3], const double gyro[3], const double* af,
+                    const double* action, const double* last_act, const double* jq, const double* jqd,
+                    const double* q0, int nu, double sigma, double out[5]) {
+  double ex = (cmd[0] - lv[0]) * (cmd[0] - lv[0]);
+  double ey = fmax(fabs(lv[1] - cmd[1]) - 0.1, 0.0);
+  out[0] = nan_to_num(exp(-(ex + ey * ey) / sigma));
+  out[1] = nan_to_num(exp(-((cmd[2] - gyro[2]) * (cmd[2] - gyro[2])) / sigma));
+  double t = 0, a = 0, pc = 0, vc = 0;
+  for (int k = 0; k < nu; k++) {
+    t += af[k] * af[k];
+    a += (action[k] - last_act[k]) * (action[k] - last_act[k]);
+    pc += fabs(jq[k] - q0[k]);
+    vc += fabs(jqd[k]);
+  }
+  out[2] = nan_to_num(t);
+  out[3] = nan_to_num(a);
+  double cn = sqrt(cmd[0] * cmd[0] + cmd[1] * cmd[1] + cmd[2] * cmd[2]);
+  out[4] = nan_to_num(pc + vc) * (cn < 0.01 ? 1.0 : 0.0);
+}
+
+/* Joystick.sample_command (joystick.py:671-725) */
+static void sample_command(const duck_env_config* cfg, const rng_t* r, int slot, double cmd[7]) {
+  double f = cfg->head_range_factor;
+  cmd[0] = rng_uniform(r, slot + 0, cfg->lin_vel_x[0], cfg->lin_vel_x[1]);
+  cmd[1] = rng_uniform(r, slot + 1, cfg->lin_vel_y[0], cfg->lin_vel_y[1]);
+  cmd[2] = rng_uniform(r, slot + 2, cfg->ang_vel_yaw[0], cfg->ang_vel_yaw[1]);
+  cmd[3] = rng_uniform(r, slot + 3, cfg->neck_pitch_range[0] * f, cfg->neck_pitch_range[1] * f);
+  cmd[4] = rng_uniform(r, slot + 4, cfg->head_pitch_range[0] * f, cfg->head_pitch_range[1] * f);
+  cmd[5] = rng_uniform(r, slot + 5, cfg->head_yaw_range[0] * f, cfg->head_yaw_range[1] * f);
+  cmd[6] = rng_uniform(r, slot + 6, cfg->head_roll_range[0] * f, cfg->head_roll_range[1] * f);
+  if (rng_u(r, slot + 7) < 0.1)
+    for (int k = 0; k < 7; k++) cmd[k] = 0;
+}
+
+/* mujoco_playground collision.geoms_colliding on the fixed contact slots */
+static double geoms_colliding(const oracle_data* d, int g1, int g2) {
+  double best = 1e4;
+  int found = 0;
+  for (int s = 0; s < d->ncon; s++) {
+    int a = d->con_geom1[s], b = d->con_geom2[s];
+    if ((a == g1 && b == g2) || (a == g2 && b == g1)) {
+      found = 1;
+      if (d->con_dist[s] < best) best = d->con_dist[s];
+    }
+  }
+  return (found && best < 0) ? 1.0 : 0.0;
+}
+
+/* Joystick._get_obs (joystick.py:487-620). fstate/istate = this env, stride 1. */
+static void get_obs(const oracle_model* m, const duck_env_config* cfg, const duck_layout* L, const oracle_data* d,
+                    double* fs, const rng_t* r, int slot_base, const double contact[2], double* obs, double* priv) {
+  int nu = m->nu;
+  const double* sd = d->sensordata;
+  double gyro[3], acc[3], grav[3], jangle[DUCK_MAXU], jvel[DUCK_MAXU];
+  const double* R = d->site_xmat[cfg->imu_site];
+  for (int k = 0; k < 3; k++) {
+    gyro[k] = sd[cfg->sens_gyro + k];
+    acc[k] = sd[cfg->sens_accelerometer + k];
+    grav[k] = -R[6 + k]; /* site_xmat.T @ [0,0,-1] */
+  }
+  double ngyro[3], nacc[3], ngrav[3];
+  for (int k = 0; k < 3; k++) {
+    ngyro[k] = gyro[k] + (2 * rng_u(r, slot_base + SLOT_GYRO + k) - 1) * cfg->noise_level * cfg->noise_gyro;
+    nacc[k] = acc[k] + (2 * rng_u(r, slot_base + SLOT_ACCEL + k) - 1) * cfg->noise_level * cfg->noise_accelerometer;
+    ngrav[k] = grav[k] + (2 * rng_u(r, slot_base + SLOT_GRAVITY + k) - 1) * cfg->noise_level * cfg->noise_gravity;
+  }
+  /* IMU delay history (joystick.py:521-530); the delayed sample is never emitted */
+  double* ih = fs + L->imu_history;
+  for (int k = 8; k >= 3; k--) ih[k] = ih[k - 3];
+  for (int k = 0; k < 3; k++) ih[k] = ngrav[k];
+  for (int a = 0; a < nu; a++) {
+    jangle[a] = d->qpos[cfg->actuator_qposadr[a]];
+    if (cfg->backlash_qposadr[a] >= 0) jangle[a] += d->qpos[cfg->backlash_qposadr[a]];
+    jvel[a] = d->qvel[cfg->actuator_qveladr[a]];
+  }
+  int o = 0;
+  for (int k = 0; k < 3; k++) obs[o++] = ngyro[k];
+  for (int k = 0; k < 3; k++) obs[o++] = nacc[k];
+  for (int k = 0; k < 7; k++) obs[o++] = fs[L->command + k];
+  for (int a = 0; a < nu; a++)
+    obs[o++] = jangle[a] + (2 * rng_u(r, slot_base + SLOT_QPOS + a) - 1) * cfg->noise_level * cfg->qpos_noise_scale[a] -
+               cfg->default_actuator[a];
+  for (int a = 0; a < nu; a++)
+    obs[o++] = (jvel[a] + (2 * rng_u(r, slot_base + SLOT_QVEL + a) - 1) * cfg->noise_level * cfg->noise_joint_vel) *
+               cfg->dof_vel_scale;
+  for (int a = 0; a < nu; a++) obs[o++] = fs[L->last_act + a];
+  for (int a = 0; a < nu; a++) obs[o++] = fs[L->last_last_act + a];
+  for (int a = 0; a < nu; a++) obs[o++] = fs[L->last_last_last_act + a];
+  for (int a = 0; a < nu; a++) obs[o++] = fs[L->motor_targets + a];
+  obs[o++] = contact[0];
+  obs[o++] = contact[1];
+  obs[o++] = fs[L->imitation_phase];
+  obs[o++] = fs[L->imitation_phase + 1];
+  /* privileged */
+  int p = 0;
+  for (int k = 0; k < o; k++) priv[p++] = obs[k];
+  for (int k = 0; k < 3; k++) priv[p++] = gyro[k];
+  for (int k = 0; k < 3; k++) priv[p++] = acc[k];
+  for (int k = 0; k < 3; k++) priv[p++] = grav[k];
+  for (int k = 0; k < 3; k++) priv[p++] = sd[cfg->sens_local_linvel + k];
+  for (int k = 0; k < 3; k++) priv[p++] = sd[cfg->sens_global_angvel + k];
+  for (int a = 0; a < nu; a++) priv[p++] = jangle[a] - cfg->default_actuator[a];
+  for (int a = 0; a < nu; a++) priv[p++] = jvel[a];
+  priv[p++] = d->qpos[2];
+  for (int a = 0; a < nu; a++) priv[p++] = d->actuator_force[a];
+  priv[p++] = contact[0];
+  priv[p++] = contact[1];
+  for (int k = 0; k < 3; k++) priv[p++] = sd[cfg->sens_left_foot_linvel + k];
+  for (int k = 0; k < 3; k++) priv[p++] = sd[cfg->sens_right_foot_linvel + k];
+  priv[p++] = fs[L->feet_air_time];
+  priv[p++] = fs[L->feet_air_time + 1];
+  if (L->imitation)
+    for (int k = 0; k < 40; k++) priv[p++] = fs[L->ref_motion + k];
+  priv[p++] = 0; /* imitation_i, filled by caller */
+  priv[p++] = fs[L->imitation_phase];
+  priv[p++] = fs[L->imitation_phase + 1];
+}
+
+static void load_data(const duck_layout* L, const double* fs, oracle_data* d) {
+  memset(d, 0, sizeof(*d));
+  memcpy(d->qpos, fs + L->qpos, sizeof(double) * L->nq);
+  memcpy(d->qvel, fs + L->qvel, sizeof(double) * L->nv);
+  memcpy(d->qacc_warmstart, fs + L->qacc_warmstart, sizeof(double) * L->nv);
+  memcpy(d->ctrl, fs + L->ctrl, sizeof(double) * L->nu);
+}
+static void store_data(const duck_layout* L, const oracle_data* d, double* fs) {
+  memcpy(fs + L->qpos, d->qpos, sizeof(double) * L->nq);
+  memcpy(fs + L->qvel, d->qvel, sizeof(double) * L->nv);
+  memcpy(fs + L->qacc_warmstart, d->qacc_warmstart, sizeof(double) * L->nv);
+  memcpy(fs + L->ctrl, d->ctrl, sizeof(double) * L->nu);
+}
+
+/* Joystick.reset (joystick.py:206-321) */
+int oracle_env_reset(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref, uint64_t seed,
+                     int64_t env_id, double* fs, int32_t* is, double* obs, double* priv) {
+  duck_layout L = duck_layout_make(m->nq, m->nv, m->nu, cfg->use_imitation);
+  int nu = m->nu;
+  memset(fs, 0, sizeof(double) * L.nfloat);
+  memset(is, 0, sizeof(int32_t) * L.nint);
+  rng_t r;
+  derive_key(seed, env_id, KEY_TAG_ENV, r.key);
+  r.ctr = 0;
+  oracle_data d;
+  memset(&d, 0, sizeof(d));
+  for (int i = 0; i < m->nq; i++) d.qpos[i] = cfg->init_qpos[i];
+  d.qpos[0] += rng_uniform(&r, RSLOT_DXY + 0, -0.05, 0.05);
+  d.qpos[1] += rng_uniform(&r, RSLOT_DXY + 1, -0.05, 0.05);
+  double yaw = rng_uniform(&r, RSLOT_YAW, -3.14, 3.14);
+  double zax[3] = {0, 0, 1}, qy[4];
+  axis_angle_quat(qy, zax, yaw);
+  quat_mul(d.qpos + 3, d.qpos + 3, qy);
+  for (int a = 0; a < nu; a++) d.qpos[cfg->actuator_qposadr[a]] *= rng_uniform(&r, RSLOT_QSCALE + a, 0.5, 1.5);
+  for (int k = 0; k < 6; k++) d.qvel[k] = rng_uniform(&r, RSLOT_QVEL + k, -0.05, 0.05);
+  for (int a = 0; a < nu; a++) d.ctrl[a] = d.qpos[cfg->actuator_qposadr[a]];
+  oracle_forward(m, &d); /* mjx_env.init -> mjx.forward */
+  double cmd[7];
+  sample_command(cfg, &r, RSLOT_CMD, cmd);
+  double push_interval = rng_uniform(&r, RSLOT_PUSH, cfg->push_interval_range[0], cfg->push_interval_range[1]);
+  is[L.push_interval] = (int32_t)nearbyint((double)(float)(push_interval / cfg->ctrl_dt));
+  is[L.rng_key] = (int32_t)r.key[0];
+  is[L.rng_key + 1] = (int32_t)r.key[1];
+  is[L.rng_ctr] = 1;
+  for (int k = 0; k < 7; k++) fs[L.command + k] = cmd[k];
+  for (int a = 0; a < nu; a++) fs[L.motor_targets + a] = cfg->default_actuator[a];
+  if (L.imitation) oracle_reference_motion(ref, cmd[0], cmd[1], cmd[2], 0, fs + L.ref_motion);
+  store_data(&L, &d, fs);
+  double contact[2] = {geoms_colliding(&d, cfg->left_foot_geom, cfg->floor_geom),
+                       geoms_colliding(&d, cfg->right_foot_geom, cfg->floor_geom)};
+  get_obs(m, cfg, &L, &d, fs, &r, RSLOT_OBS, contact, obs, priv);
+  priv[L.priv_size - 3] = is[L.imitation_i];
+  /* AutoReset first-state snapshot */
+  memcpy(fs + L.first_qpos, fs + L.qpos, sizeof(double) * m->nq);
+  memcpy(fs + L.first_qvel, fs + L.qvel, sizeof(double) * m->nv);
+  memcpy(fs + L.first_qacc_warmstart, fs + L.qacc_warmstart, sizeof(double) * m->nv);
+  memcpy(fs + L.first_ctrl, fs + L.ctrl, sizeof(double) * nu);
+  memcpy(fs + L.first_obs, obs, sizeof(double) * L.obs_size);
+  memcpy(fs + L.first_priv, priv, sizeof(double) * L.priv_size);
+  return 0;
+}
+
+/* Joystick.step (joystick.py:323-481) + EpisodeWrapper + BraxAutoResetWrapper when cfg->auto_reset */
+int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref, double* fs,
+                    int32_t* is, const double* action, double* obs, double* priv, double* reward_out,
+                    double* done_out, oracle_data* d_out) {
+  duck_layout L = duck_layout_make(m->nq, m->nv, m->nu, cfg->use_imitation);
+  int nu = m->nu;
+  double dt = cfg->ctrl_dt;
+  if (cfg->auto_reset) {
+    if (fs[L.done] != 0) is[L.ep_steps] = 0;
+  }
+  rng_t r;
+  r.key[0] = (uint32_t)is[L.rng_key];
+  r.key[1] = (uint32_t)is[L.rng_key + 1];
+  r.ctr = (uint32_t)is[L.rng_ctr];
+  /* imitation phase (:325-355) */
+  if (L.imitation) {
+    int nb = ref->nb_steps_in_period;
+    is[L.imitation_i] = (is[L.imitation_i] + 1) % nb;
+    double ph = (double)(float)((double)is[L.imitation_i] / nb) * 2 * PI;
+    fs[L.imitation_phase] = cos(ph);
+    fs[L.imitation_phase + 1] = sin(ph);
+    oracle_reference_motion(ref, fs[L.command], fs[L.command + 1], fs[L.command + 2], is[L.imitation_i],
+                            fs + L.ref_motion);
+  } else {
+    is[L.imitation_i] = 0;
+  }
+  /* action delay (:362-376) */
+  double* ah = fs + L.action_history;
+  for (int k = 3 * nu - 1; k >= nu; k--) ah[k] = ah[k - nu];
+  for (int a = 0; a < nu; a++) ah[a] = action[a];
+  int didx = rng_randint(&r, SLOT_ACTION_DELAY, cfg->action_min_delay, cfg->action_max_delay);
+  const double* adel = ah + didx * nu;
+  /* push (:381-400) */
+  double theta = rng_uniform(&r, SLOT_PUSH_THETA, 0.0, 2 * PI);
+  double mag = rng_uniform(&r, SLOT_PUSH_MAG, cfg->push_magnitude_range[0], cfg->push_magnitude_range[1]);
+  double gate = ((is[L.push_step] + 1) % is[L.push_interval] == 0) ? 1.0 : 0.0;
+  double push[2] = {cos(theta) * gate * cfg->push_enable, sin(theta) * gate * cfg->push_enable};
+  oracle_data dd, *d = d_out ? d_out : &dd;
+  load_data(&L, fs, d);
+  d->qvel[0] += push[0] * mag;
+  d->qvel[1] += push[1] * mag;
+  /* motor targets (:404-417) */
+  double mt[DUCK_MAXU];
+  for (int a = 0; a < nu; a++) {
+    mt[a] = cfg->default_actuator[a] + adel[a] * cfg->action_scale;
+    if (cfg->use_motor_speed_limits) {
+      double prev = fs[L.motor_targets + a], lim = cfg->max_motor_velocity * dt;
+      mt[a] = fmin(fmax(mt[a], prev - lim), prev + lim);
+    }
+    d->ctrl[a] = mt[a];
+  }
+  /* physics (:420) */
+  for (int s = 0; s < cfg->n_substeps; s++) {
+    oracle_forward(m, d);
+    euler(m, d);
+  }
+  for (int a = 0; a < nu; a++) fs[L.motor_targets + a] = mt[a];
+  /* contacts and feet bookkeeping (:424-435) */
+  double contact[2] = {geoms_colliding(d, cfg->left_foot_geom, cfg->floor_geom),
+                       geoms_colliding(d, cfg->right_foot_geom, cfg->floor_geom)};
+  for (int k = 0; k < 2; k++) {
+    fs[L.feet_air_time + k] += dt;
+    int site = k == 0 ? cfg->left_foot_site : cfg->right_foot_site;
+    fs[L.swing_peak + k] = fmax(fs[L.swing_peak + k], d->site_xpos[site][2]);
+  }
+  store_data(&L, d, fs);
+  get_obs(m, cfg, &L, d, fs, &r, 0, contact, obs, priv);
+  priv[L.priv_size - 3] = is[L.imitation_i];
+  /* termination (:483-485) */
+  int nan = 0;
+  for (int i = 0; i < m->nq; i++) nan |= isnan(d->qpos[i]);
+  for (int i = 0; i < m->nv; i++) nan |= isnan(d->qvel[i]);
+  double done = (d->sensordata[cfg->sens_upvector + 2] < 0.0 || nan) ? 1.0 : 0.0;
+  /* rewards (:440-447, :622-669) */
+  double jq[DUCK_MAXU], jqd[DUCK_MAXU], la[DUCK_MAXU], act[DUCK_MAXU];
+  for (int a = 0; a < nu; a++) {
+    jq[a] = d->qpos[cfg->actuator_qposadr[a]];
+    jqd[a] = d->qvel[cfg->actuator_qveladr[a]];
+    la[a] = fs[L.last_act + a];
+    act[a] = action[a];
+  }
+  double rr[5], cmd[7], q0[DUCK_MAXU];
+  for (int k = 0; k < 7; k++) cmd[k] = fs[L.command + k];
+  for (int a = 0; a < nu; a++) q0[a] = cfg->default_actuator[a];
+  oracle_rewards(cmd, d->sensordata + cfg->sens_local_linvel, d->sensordata + cfg->sens_gyro, d->actuator_force, act,
+                 la, jq, jqd, q0, nu, cfg->tracking_sigma, rr);
+  double imit = 0;
+  if (L.imitation) {
+    double c2[2] = {contact[0], contact[1]};
+    imit = oracle_reward_imitation(d->qpos, d->qvel, jq, jqd, c2, fs + L.ref_motion, cmd, nu);
+  }
+  double terms[7] = {rr[0] * cfg->scale_tracking_lin_vel, rr[1] * cfg->scale_tracking_ang_vel,
+                     rr[2] * cfg->scale_torques, rr[3] * cfg->scale_action_rate, 1.0 * cfg->scale_alive,
+                     imit * cfg->scale_imitation, rr[4] * cfg->scale_stand_still};
+  double sum = 0;
+  for (int k = 0; k < 7; k++) sum += terms[k];
+  double reward = fmin(fmax(sum * dt, 0.0), 10000.0);
+  /* info bookkeeping (:449-477) */
+  fs[L.push] = push[0];
+  fs[L.push + 1] = push[1];
+  is[L.step] += 1;
+  is[L.push_step] += 1;
+  for (int a = 0; a < nu; a++) {
+    fs[L.last_last_last_act + a] = fs[L.last_last_act + a];
+    fs[L.last_last_act + a] = fs[L.last_act + a];
+    fs[L.last_act + a] = action[a];
+  }
+  if (is[L.step] > 500) {
+    sample_command(cfg, &r, SLOT_CMD, cmd);
+    for (int k = 0; k < 7; k++) fs[L.command + k] = cmd[k];
+  }
+  if (done != 0 || is[L.step] > 500) is[L.step] = 0;
+  for (int k = 0; k < 2; k++) {
+    fs[L.feet_air_time + k] *= contact[k] ? 0.0 : 1.0;
+    fs[L.last_contact + k] = contact[k];
+    fs[L.swing_peak + k] *= contact[k] ? 0.0 : 1.0;
+  }
+  double scales[7] = {cfg->scale_tracking_lin_vel, cfg->scale_tracking_ang_vel, cfg->scale_torques,
+                      cfg->scale_action_rate, cfg->scale_alive, cfg->scale_imitation, cfg->scale_stand_still};
+  for (int k = 0; k < 7; k++) fs[L.metrics + k] = scales[k] > 0 ? terms[k] : -terms[k];
+  fs[L.metrics + DUCK_M_SWING_PEAK] = 0.5 * (fs[L.swing_peak] + fs[L.swing_peak + 1]);
+  is[L.rng_ctr] = (int32_t)(r.ctr + 1);
+  /* training wrappers */
+  double trunc = 0;
+  if (cfg->auto_reset) {
+    is[L.ep_steps] += 1;
+    if (is[L.ep_steps] >= cfg->episode_length) { trunc = 1.0 - done; done = 1.0; }
+    if (done != 0) {
+      memcpy(fs + L.qpos, fs + L.first_qpos, sizeof(double) * m->nq);
+      memcpy(fs + L.qvel, fs + L.first_qvel, sizeof(double) * m->nv);
+      memcpy(fs + L.qacc_warmstart, fs + L.first_qacc_warmstart, sizeof(double) * m->nv);
+      memcpy(fs + L.ctrl, fs + L.first_ctrl, sizeof(double) * nu);
+      memcpy(obs, fs + L.first_obs, sizeof(double) * L.obs_size);
+      memcpy(priv, fs + L.first_priv, sizeof(double) * L.priv_size);
+    }
+  }
+  fs[L.reward] = reward;
+  fs[L.done] = done;
+  fs[L.truncation] = trunc;
+  if (reward_out) *reward_out = reward;
+  if (done_out) *done_out = done;
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* batched entry points (CPU baseline)                                                  */
+/* ------------------------------------------------------------------------------------ */
+
+int oracle_batch_reset(const oracle_model* const* models, int n_models, const duck_env_config* cfg,
+                       const duck_refmotion* ref, int n, uint64_t seed, int64_t env_offset, double* fstate,
+                       int32_t* istate, double* obs, double* priv, int n_threads) {
+  const oracle_model* m0 = models[0];
+  duck_layout L = duck_layout_make(m0->nq, m0->nv, m0->nu, cfg->use_imitation);
+#ifdef _OPENMP
+  if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(static)
+#endif
+  for (int e = 0; e < n; e++) {
+    const oracle_model* m = models[n_models == 1 ? 0 : e];
+    double fs[1024];
+    int32_t is[16];
+    oracle_env_reset(m, cfg, ref, seed, env_offset + e, fs, is, obs + (size_t)e * L.obs_size,
+                     priv + (size_t)e * L.priv_size);
+    for (int k = 0; k < L.nfloat; k++) fstate[(size_t)k * n + e] = fs[k];
+    for (int k = 0; k < L.nint; k++) istate[(size_t)k * n + e] = is[k];
+  }
+  return 0;
+}
+
+int oracle_batch_step(const oracle_model* const* models, int n_models, const duck_env_config* cfg,
+                      const duck_refmotion* ref, int n, double* fstate, int32_t* istate, const double* actions,
+                      double* obs, double* priv, double* reward, double* done, int n_threads) {
+  const oracle_model* m0 = models[0];
+  duck_layout L = duck_layout_make(m0->nq, m0->nv, m0->nu, cfg->use_imitation);
+#ifdef _OPENMP
+  if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(static)
+#endif
+  for (int e = 0; e < n; e++) {
+    const oracle_model* m = models[n_models == 1 ? 0 : e];
+    double fs[1024];
+    int32_t is[16];
+    for (int k = 0; k < L.nfloat; k++) fs[k] = fstate[(size_t)k * n + e];
+    for (int k = 0; k < L.nint; k++) is[k] = istate[(size_t)k * n + e];
+    oracle_env_step(m, cfg, ref, fs, is, actions + (size_t)e * m->nu, obs + (size_t)e * L.obs_size,
+                    priv + (size_t)e * L.priv_size, reward + e, done + e, NULL);
+    for (int k = 0; k < L.nfloat; k++) fstate[(size_t)k * n + e] = fs[k];
+    for (int k = 0; k < L.nint; k++) istate[(size_t)k * n + e] = is[k];
+  }
+  return 0;
+}

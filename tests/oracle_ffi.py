@@ -1,0 +1,207 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) — test infrastructure only.
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker;
+the product path never imports this module.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Optional
+
+import numpy as np
+
+from open_duck_playground_amd.cabi import (DuckEnvConfig, DuckRefMotion, ModelDescHolder, dr_layout, layout,
+                                           refmotion_struct)
+from open_duck_playground_amd.mjcf import Model
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+
+MAXQ, MAXV, MAXU, MAXSD, MAXBODY, MAXSITE, MAXGEOM, MAXCON = 40, 32, 16, 64, 20, 8, 64, 16
+
+
+class OracleData(C.Structure):
+    _fields_ = [
+        ("qpos", C.c_double * MAXQ), ("qvel", C.c_double * MAXV), ("qacc_warmstart", C.c_double * MAXV),
+        ("ctrl", C.c_double * MAXU),
+        ("qacc", C.c_double * MAXV), ("qacc_smooth", C.c_double * MAXV), ("qfrc_smooth", C.c_double * MAXV),
+        ("qfrc_bias", C.c_double * MAXV), ("qfrc_passive", C.c_double * MAXV), ("qfrc_actuator", C.c_double * MAXV),
+        ("qfrc_constraint", C.c_double * MAXV),
+        ("actuator_force", C.c_double * MAXU),
+        ("sensordata", C.c_double * MAXSD),
+        ("xpos", C.c_double * 3 * MAXBODY), ("xquat", C.c_double * 4 * MAXBODY), ("xmat", C.c_double * 9 * MAXBODY),
+        ("xipos", C.c_double * 3 * MAXBODY), ("ximat", C.c_double * 9 * MAXBODY),
+        ("site_xpos", C.c_double * 3 * MAXSITE), ("site_xmat", C.c_double * 9 * MAXSITE),
+        ("geom_xpos", C.c_double * 3 * MAXGEOM), ("geom_xmat", C.c_double * 9 * MAXGEOM),
+        ("qM", C.c_double * MAXV * MAXV),
+        ("ncon", C.c_int),
+        ("con_dist", C.c_double * MAXCON), ("con_pos", C.c_double * 3 * MAXCON), ("con_frame", C.c_double * 9 * MAXCON),
+        ("con_geom1", C.c_int * MAXCON), ("con_geom2", C.c_int * MAXCON),
+        ("nefc", C.c_int), ("efc_force", C.c_double * 128), ("solver_niter", C.c_int),
+    ]
+
+    def arr(self, name, n=None):
+        a = np.ctypeslib.as_array(getattr(self, name))
+        return a if n is None else a[:n]
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
+            os.path.getmtime(os.path.join(ROOT, "oracle", f)) for f in ("duck_oracle.c", "duck_oracle.h")):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB)
+        vp = C.c_void_p
+        L.oracle_model_create.restype = vp
+        L.oracle_model_create.argtypes = [C.c_void_p]
+        L.oracle_model_destroy.argtypes = [vp]
+        L.oracle_model_randomized.restype = vp
+        L.oracle_model_randomized.argtypes = [vp, C.POINTER(C.c_double)]
+        L.oracle_dr_sample.argtypes = [vp, C.c_uint64, C.c_int64, C.POINTER(C.c_double)]
+        L.oracle_forward.argtypes = [vp, C.POINTER(OracleData)]
+        L.oracle_step.argtypes = [vp, C.POINTER(OracleData), C.c_int]
+        L.oracle_threefry2x32.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        L.oracle_env_reset.argtypes = [vp, C.POINTER(DuckEnvConfig), C.POINTER(DuckRefMotion), C.c_uint64, C.c_int64,
+                                       dp, ip, dp, dp]
+        L.oracle_env_step.argtypes = [vp, C.POINTER(DuckEnvConfig), C.POINTER(DuckRefMotion), dp, ip, dp, dp, dp, dp,
+                                      dp, C.POINTER(OracleData)]
+        L.oracle_reference_motion.argtypes = [C.POINTER(DuckRefMotion), C.c_double, C.c_double, C.c_double, C.c_int, dp]
+        L.oracle_reward_imitation.restype = C.c_double
+        L.oracle_reward_imitation.argtypes = [dp, dp, dp, dp, dp, dp, dp, C.c_int]
+        L.oracle_rewards.argtypes = [dp, dp, dp, dp, dp, dp, dp, dp, dp, C.c_int, C.c_double, dp]
+        L.oracle_batch_step.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(DuckEnvConfig), C.POINTER(DuckRefMotion),
+                                        C.c_int, dp, ip, dp, dp, dp, dp, dp, C.c_int]
+        L.oracle_batch_reset.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(DuckEnvConfig), C.POINTER(DuckRefMotion),
+                                         C.c_int, C.c_uint64, C.c_int64, dp, ip, dp, dp, C.c_int]
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+class OracleModel:
+    def __init__(self, m: Model, dr: Optional[np.ndarray] = None):
+        self.m = m
+        self._holder = ModelDescHolder(m)
+        L = lib()
+        self.ptr = L.oracle_model_create(C.byref(self._holder.desc))
+        if not self.ptr:
+            raise RuntimeError("oracle_model_create failed")
+        self.base_ptr = None
+        if dr is not None:
+            self.base_ptr = self.ptr
+            self.ptr = L.oracle_model_randomized(self.base_ptr, _dp(np.ascontiguousarray(dr, dtype=np.float64)))
+
+    def dr_sample(self, seed: int, env_id: int) -> np.ndarray:
+        out = np.zeros(dr_layout(self.m.nbody, self.m.nu)["nfloat"])
+        lib().oracle_dr_sample(self.ptr, seed, env_id, _dp(out))
+        return out
+
+    def __del__(self):
+        try:
+            lib().oracle_model_destroy(self.ptr)
+            if self.base_ptr:
+                lib().oracle_model_destroy(self.base_ptr)
+        except Exception:
+            pass
+
+    def new_data(self, qpos=None, qvel=None, ctrl=None, warm=None) -> OracleData:
+        d = OracleData()
+        m = self.m
+        q = qpos if qpos is not None else m.key_qpos[0]
+        d.arr("qpos")[:m.nq] = q
+        if qvel is not None:
+            d.arr("qvel")[:m.nv] = qvel
+        if ctrl is not None:
+            d.arr("ctrl")[:m.nu] = ctrl
+        if warm is not None:
+            d.arr("qacc_warmstart")[:m.nv] = warm
+        return d
+
+    def forward(self, d: OracleData):
+        lib().oracle_forward(self.ptr, C.byref(d))
+
+    def step(self, d: OracleData, n: int = 1):
+        lib().oracle_step(self.ptr, C.byref(d), n)
+
+
+class OracleEnv:
+    """Single-env Joystick on the oracle (fstate/istate in duck_env.h layout, stride 1)."""
+
+    def __init__(self, model: OracleModel, cfg: DuckEnvConfig, table=None):
+        self.model = model
+        self.cfg = cfg
+        self.L = layout(model.m.nq, model.m.nv, model.m.nu, bool(cfg.use_imitation))
+        if table is None:
+            from open_duck_playground_amd import constants
+            table = dict(np.load(constants.POLY_COEFFICIENTS, allow_pickle=False))
+        self.ref, self._coeffs = refmotion_struct(table)
+        self.fs = np.zeros(self.L.nfloat)
+        self.is_ = np.zeros(self.L.nint, dtype=np.int32)
+        self.obs = np.zeros(self.L.obs_size)
+        self.priv = np.zeros(self.L.priv_size)
+
+    def reset(self, seed: int, env_id: int = 0):
+        lib().oracle_env_reset(self.model.ptr, C.byref(self.cfg), C.byref(self.ref), seed, env_id, _dp(self.fs),
+                               _ip(self.is_), _dp(self.obs), _dp(self.priv))
+        return self.obs.copy(), self.priv.copy()
+
+    def step(self, action, data: Optional[OracleData] = None):
+        a = np.ascontiguousarray(action, dtype=np.float64)
+        rew = np.zeros(1)
+        done = np.zeros(1)
+        lib().oracle_env_step(self.model.ptr, C.byref(self.cfg), C.byref(self.ref), _dp(self.fs), _ip(self.is_),
+                              _dp(a), _dp(self.obs), _dp(self.priv), _dp(rew), _dp(done),
+                              C.byref(data) if data is not None else None)
+        return self.obs.copy(), self.priv.copy(), float(rew[0]), float(done[0])
+
+
+class OracleBatch:
+    """SoA batch of envs on the oracle with OpenMP (CPU baseline)."""
+
+    def __init__(self, models, cfg: DuckEnvConfig, n_envs: int, table=None):
+        self.models = models if isinstance(models, list) else [models]
+        self.cfg = cfg
+        self.n = n_envs
+        m = self.models[0].m
+        self.L = layout(m.nq, m.nv, m.nu, bool(cfg.use_imitation))
+        if table is None:
+            from open_duck_playground_amd import constants
+            table = dict(np.load(constants.POLY_COEFFICIENTS, allow_pickle=False))
+        self.ref, self._coeffs = refmotion_struct(table)
+        self.fs = np.zeros(self.L.nfloat * n_envs)
+        self.is_ = np.zeros(self.L.nint * n_envs, dtype=np.int32)
+        self.obs = np.zeros((n_envs, self.L.obs_size))
+        self.priv = np.zeros((n_envs, self.L.priv_size))
+        self.rew = np.zeros(n_envs)
+        self.done = np.zeros(n_envs)
+        self._ptrs = (C.c_void_p * len(self.models))(*[mm.ptr for mm in self.models])
+
+    def reset(self, seed: int, env_offset: int = 0, threads: int = 0):
+        lib().oracle_batch_reset(self._ptrs, len(self.models), C.byref(self.cfg), C.byref(self.ref), self.n, seed,
+                                 env_offset, _dp(self.fs), _ip(self.is_), _dp(self.obs), _dp(self.priv), threads)
+
+    def step(self, actions, threads: int = 0):
+        a = np.ascontiguousarray(actions, dtype=np.float64)
+        lib().oracle_batch_step(self._ptrs, len(self.models), C.byref(self.cfg), C.byref(self.ref), self.n,
+                                _dp(self.fs), _ip(self.is_), _dp(a), _dp(self.obs), _dp(self.priv), _dp(self.rew),
+                                _dp(self.done), threads)

@@ -1,0 +1,111 @@
+"""GPU env parity: Joystick.reset/step in libduck.so vs the oracle's restatement.
+
+Same seeds -> same threefry streams, so obs noise, action delays, pushes and commands
+match draw for draw. Obs/priv/reward are compared within fp32 tolerances; done flags and
+integer bookkeeping exactly (for envs whose physics stayed within tolerance).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from open_duck_playground_amd.config import default_config, env_config_struct
+from open_duck_playground_amd.joystick import Joystick, domain_randomize, wrap_for_brax_training
+from tests.oracle_ffi import OracleBatch, OracleModel
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(env, st, ob, L, tol_obs=2e-3, frac=0.95):
+    obs = st.obs["state"].cpu().numpy().astype(np.float64)
+    priv = st.obs["privileged_state"].cpu().numpy().astype(np.float64)
+    err = np.abs(obs - ob.obs).max(axis=1) / (1 + np.abs(ob.obs).max(axis=1))
+    errp = np.abs(priv - ob.priv).max(axis=1) / (1 + np.abs(ob.priv).max(axis=1))
+    good = (err < tol_obs) & (errp < tol_obs * 10)
+    assert good.mean() >= frac, (good.mean(), np.sort(err)[-5:], np.sort(errp)[-5:])
+    rew = st.reward.cpu().numpy()
+    assert np.allclose(rew[good], ob.rew[good], rtol=1e-3, atol=1e-3)
+    assert np.array_equal(st.done.cpu().numpy()[good], ob.done[good])
+    ist = st.istate.view(L.nint, -1).cpu().numpy()
+    oist = ob.is_.reshape(L.nint, -1)
+    for name in ("rng_key", "rng_ctr", "push_step", "push_interval"):
+        k = L.ioff[name]
+        assert np.array_equal(ist[k][good], oist[k][good]), name
+    return good
+
+
+@pytest.mark.parametrize("task,imit", [("flat_terrain", False), ("flat_terrain", True), ("flat_terrain_backlash", True)])
+def test_reset_step_parity(task, imit, gpu):
+    n = 100  # not a multiple of the 16-lane workgroup
+    env = Joystick(task, num_envs=n, device=gpu, use_imitation=imit)
+    st = env.reset(rng=7)
+    om = OracleModel(env.mj_model)
+    cfg = env_config_struct(env.mj_model, default_config(), imit)
+    ob = OracleBatch(om, cfg, n)
+    ob.reset(seed=7)
+    L = env._layout
+    good = _compare(env, st, ob, L)
+    rng = np.random.default_rng(0)
+    for t in range(5):
+        a = rng.uniform(-1, 1, (n, env.action_size)).astype(np.float32)
+        env.step(st, torch.tensor(a, device=gpu))
+        ob.step(a.astype(np.float64))
+        good &= _compare(env, st, ob, L)
+    assert good.mean() > 0.9
+
+
+def test_autoreset_and_episode(gpu):
+    n = 64
+    env = wrap_for_brax_training(Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False),
+                                 episode_length=5)
+    st = env.reset(rng=3)
+    first_obs = st.obs["state"].clone()
+    for t in range(5):
+        env.step(st, torch.zeros(n, env.action_size, device=gpu))
+    torch.cuda.synchronize()
+    # episode_length reached: every env is done and restored to its first state
+    assert torch.all(st.done == 1)
+    assert torch.allclose(st.obs["state"], first_obs)
+    assert torch.all(st.info["steps"] == 5)
+    env.step(st, torch.zeros(n, env.action_size, device=gpu))
+    assert torch.all(st.info["steps"] == 1)
+
+
+def test_domain_randomization_parity(gpu):
+    n = 48
+    env = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
+    dr = domain_randomize(env, rng=11)
+    st = env.reset(rng=5)
+    base = OracleModel(env.mj_model)
+    models = [OracleModel(env.mj_model, dr=base.dr_sample(11, e)) for e in range(n)]
+    # the GPU DR record must match the oracle's sampling of the same streams
+    D = dr.view(-1, n).cpu().numpy().T
+    ref = np.array([base.dr_sample(11, e) for e in range(n)])
+    np.testing.assert_allclose(D, ref, rtol=1e-5, atol=1e-6)
+    cfg = env_config_struct(env.mj_model, default_config(), False, domain_randomize=True)
+    ob = OracleBatch(models, cfg, n)
+    ob.reset(seed=5)
+    L = env._layout
+    good = _compare(env, st, ob, L)
+    rng = np.random.default_rng(1)
+    for t in range(3):
+        a = rng.uniform(-1, 1, (n, env.action_size)).astype(np.float32)
+        env.step(st, torch.tensor(a, device=gpu))
+        ob.step(a.astype(np.float64))
+        good &= _compare(env, st, ob, L)
+
+
+def test_edge_sizes(gpu):
+    for n in (1, 17):
+        env = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
+        st = env.reset(rng=1)
+        env.step(st, torch.zeros(n, env.action_size, device=gpu))
+        torch.cuda.synchronize()
+        assert torch.isfinite(st.obs["state"]).all()
+
+
+def test_host_action_is_moved(gpu):
+    env = Joystick("flat_terrain", num_envs=4, device=gpu, use_imitation=False)
+    st = env.reset(rng=1)
+    out = env.step(st, torch.zeros(4, env.action_size))  # host tensor is moved to the device
+    assert out is st
