@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Env-step throughput of the batched Open Duck Mini v2 Joystick env on MI355X.
+
+Metric (BASELINE.json): env steps/sec (all envs), open_duck_mini_v2 flat, 4096 envs per GPU.
+One env-step = one ``Joystick.step`` (joystick.py:323-481): 10 physics substeps + obs +
+termination + reward, under the training wrappers (episode_length 1000, auto-reset), i.e.
+what brax PPO drives through ``wrap_for_brax_training`` (common/runner.py:117).
+
+Workload C2 (BASELINE.json configs[1]): flat terrain, no imitation reward, 4096 envs per
+GPU, inputs (state, actions) resident in HBM. Actions are i.i.d. U(-1,1)^14 (seed 1234).
+Multi-GPU: one process per GPU, envs sharded by global env id (env_offset = rank * envs),
+no collective in the step -> weak scaling; the timed region is bracketed by barrier +
+synchronize and the max over ranks is reported.
+
+Extra JSON objects:
+  roofline      the step kernel against HBM: algorithmic bytes per env-step
+                x envs per launch / average launch time from HIP events on the launch stream.
+  cpu_baseline  the fp64 C oracle (oracle/, a restatement of the same step) over OpenMP host
+                threads on a bounded sample (rank 0, N=1 only).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from open_duck_playground_amd.joystick import Joystick, wrap_for_brax_training  # noqa: E402
+from open_duck_playground_amd.sharding import shard_from_env  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(env: Joystick) -> int:
+    """Compulsory HBM bytes of one env-step of one env.
+
+    read + write of the persistent per-env state the step carries (qpos .. imitation_phase,
+    int counters and RNG words), read of the action, write of obs, privileged obs, reward,
+    done, truncation and the 8 metrics. The auto-reset snapshot (first_*) is read only by
+    envs that terminate and is not counted; the reference-motion row is counted only with
+    imitation (it is untouched otherwise).
+    """
+    L = env._layout
+    o = L.off
+    state_f = o["metrics"] - o["qpos"]
+    if not env.use_imitation:
+        state_f -= 40
+    state_i = L.nint
+    rd = 4 * (state_f + state_i + L.nu)
+    wr = 4 * (state_f + state_i + L.obs_size + L.priv_size + 1 + 1 + 1 + 8)
+    if env.dr is not None:
+        rd += 4 * env.dr.numel() // env.num_envs
+    return rd + wr
+
+
+def cpu_baseline(task: str, use_imitation: bool, budget_s: float, threads: int):
+    """Time the fp64 C oracle (same step semantics) on host cores: OpenMP, one env per thread-iteration."""
+    from open_duck_playground_amd.config import default_config, env_config_struct
+    from open_duck_playground_amd.joystick import OpenDuckMiniV2Env
+    from open_duck_playground_amd import constants
+    from tests.oracle_ffi import OracleBatch, OracleModel
+
+    base = OpenDuckMiniV2Env(xml_path=constants.task_to_xml(task), config=default_config())
+    m = base.mj_model
+    cfg = env_config_struct(m, base._config, use_imitation, True, False)
+    n = 32 * threads
+    batch = OracleBatch(OracleModel(m), cfg, n)
+    batch.reset(seed=0, threads=threads)
+    rng = np.random.default_rng(1234)
+    acts = rng.uniform(-1, 1, (4, n, m.nu))
+    batch.step(acts[0], threads=threads)  # warm-up
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        batch.step(acts[steps % 4], threads=threads)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": n * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{task}, {n} envs x {steps} env-steps ({el:.1f} s), fp64 oracle, OpenMP {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--task", default="flat_terrain")
+    ap.add_argument("--imitation", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline sampling (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    n = args.envs
+    shard = shard_from_env(n)
+    env = Joystick(args.task, num_envs=n, device=dev, use_imitation=args.imitation, env_offset=shard.env_offset)
+    env = wrap_for_brax_training(env, episode_length=1000)
+    state = env.reset(rng=0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    pool = [torch.rand(n, env.action_size, device=dev, generator=g) * 2 - 1 for _ in range(8)]
+
+    for i in range(args.warmup):
+        env.step(state, pool[i % len(pool)])
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        s, e = ev[i]
+        s.record()
+        env.step(state, pool[i % len(pool)])
+        e.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    ok = bool(torch.isfinite(state.obs["state"]).all().item())
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        thr = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        cpu = cpu_baseline(args.task, args.imitation, args.cpu_budget, thr)
+
+    if rank == 0:
+        B = algorithmic_bytes(env)
+        achieved = B * n / (kern_ms * 1e-3) / 1e9
+        total = world * n * K
+        line = {
+            "metric": "env steps/sec (all envs) open_duck_mini_v2 flat, 4096 envs, 1/2/4/8 GPUs",
+            "value": total / el, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
+            "ms_per_step": el / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic (keyframe home + reset randomisation, actions U(-1,1)^14)",
+            "config": {"workload": f"C2: {args.task}, {'imitation' if args.imitation else 'no imitation'}, "
+                                   f"{n} envs per GPU, episode_length 1000 + auto-reset",
+                       "envs_per_gpu": n, "total_envs": world * n, "substeps": env.n_substeps,
+                       "parallelism": f"env-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "step_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": B},
+            "cpu_baseline": cpu,
+            "finite": ok,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

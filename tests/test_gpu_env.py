@@ -109,3 +109,22 @@ def test_host_action_is_moved(gpu):
     st = env.reset(rng=1)
     out = env.step(st, torch.zeros(4, env.action_size))  # host tensor is moved to the device
     assert out is st
+
+
+def test_env_offset_shards_are_bit_identical(gpu):
+    """Two shards (env_offset 0 and 24) reproduce one 48-env batch exactly (global env ids)."""
+    n, h = 48, 24
+    rng = np.random.default_rng(3)
+    acts = [torch.tensor(rng.uniform(-1, 1, (n, 14)).astype(np.float32), device=gpu) for _ in range(3)]
+    full = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=True)
+    sf = full.reset(rng=9)
+    parts = [Joystick("flat_terrain", num_envs=h, device=gpu, use_imitation=True, env_offset=k * h) for k in range(2)]
+    sp = [p.reset(rng=9) for p in parts]
+    for a in acts:
+        full.step(sf, a)
+        for k in range(2):
+            parts[k].step(sp[k], a[k * h:(k + 1) * h])
+    for key in ("state", "privileged_state"):
+        got = torch.cat([s.obs[key] for s in sp])
+        assert torch.equal(got, sf.obs[key]), key
+    assert torch.equal(torch.cat([s.reward for s in sp]), sf.reward)

@@ -1,0 +1,121 @@
+"""Known-answer and property tests of the CPU oracle (physics is not pinned by any
+reference test: mujoco/mjx are absent, see DESIGN.md "Parity"). These are build-authored
+analytic checks: threefry KATs, exact semi-implicit-Euler free fall, standing at rest,
+reset determinism, and the auto-reset wrapper semantics (BraxAutoResetWrapper)."""
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from open_duck_playground_amd import constants
+from open_duck_playground_amd.config import default_config, env_config_struct
+from open_duck_playground_amd.mjcf import Model
+from tests.oracle_ffi import OracleBatch, OracleEnv, OracleModel, lib
+
+
+@pytest.fixture(scope="module")
+def m():
+    return Model.load(constants.task_to_xml("flat_terrain"))
+
+
+@pytest.fixture(scope="module")
+def om(m):
+    return OracleModel(m)
+
+
+@pytest.mark.parametrize("ctr,key,out", [
+    ((0, 0), (0, 0), (0x6B200159, 0x99BA4EFE)),
+    ((0xFFFFFFFF, 0xFFFFFFFF), (0xFFFFFFFF, 0xFFFFFFFF), (0x1CB996FC, 0xBB002BE7)),
+    ((0x243F6A88, 0x85A308D3), (0x13198A2E, 0x03707344), (0xC4923A9C, 0x483DF7A0)),
+])
+def test_threefry_kat(ctr, key, out):
+    """Random123 kat_vectors, threefry2x32 with 20 rounds."""
+    k = (C.c_uint32 * 2)(*key)
+    c = (C.c_uint32 * 2)(*ctr)
+    o = (C.c_uint32 * 2)()
+    lib().oracle_threefry2x32(k, c, o)
+    assert (o[0], o[1]) == out
+
+
+def _home(m):
+    key = m.names["key"].index("home")
+    return m.key_qpos[key].copy(), m.key_ctrl[key].copy()
+
+
+def test_free_fall_is_exact_euler(m, om):
+    q, _ = _home(m)
+    q[2] = 5.0  # far above the floor: no contacts
+    ctrl = q[7:7 + m.nu].copy()  # position servo at its target: zero actuator force
+    d = om.new_data(qpos=q, qvel=np.zeros(m.nv), ctrl=ctrl)
+    om.forward(d)
+    qacc = d.arr("qacc", m.nv)
+    g = -m.opt_gravity[2]
+    np.testing.assert_allclose(qacc[2], -g, atol=1e-9)
+    np.testing.assert_allclose(np.delete(qacc, 2), 0, atol=1e-9)
+    n, dt = 25, m.opt_timestep
+    om.step(d, n)
+    qpos, qvel = d.arr("qpos", m.nq), d.arr("qvel", m.nv)
+    np.testing.assert_allclose(qvel[2], -g * dt * n, rtol=1e-12)
+    np.testing.assert_allclose(qpos[2], 5.0 - g * dt * dt * n * (n + 1) / 2, rtol=1e-12)
+    np.testing.assert_allclose(qpos[7:], q[7:], atol=1e-12)
+
+
+def test_standing_at_rest(m, om):
+    q, ctrl = _home(m)
+    d = om.new_data(qpos=q, qvel=np.zeros(m.nv), ctrl=ctrl)
+    om.step(d, 500)  # 1 s
+    qpos, qvel = d.arr("qpos", m.nq), d.arr("qvel", m.nv)
+    assert 0.10 < qpos[2] < 0.20
+    w, x, y, z = qpos[3:7]
+    up_z = 1 - 2 * (x * x + y * y)
+    assert up_z > 0.95
+    assert np.abs(qvel).max() < 0.2
+    assert np.isfinite(qpos).all()
+    assert (d.arr("con_dist", 12) < 0.005).sum() >= 4  # both feet carry contacts
+
+
+def _env(m, om, imit=False, auto_reset=False, episode_length=1000):
+    cfgd = default_config()
+    cfgd.episode_length = episode_length
+    return OracleEnv(om, env_config_struct(m, cfgd, imit, auto_reset))
+
+
+def test_reset_is_deterministic_per_env_id(m, om):
+    e = _env(m, om)
+    o1, p1 = e.reset(seed=3, env_id=5)
+    o2, p2 = e.reset(seed=3, env_id=5)
+    o3, _ = e.reset(seed=3, env_id=6)
+    np.testing.assert_array_equal(o1, o2)
+    np.testing.assert_array_equal(p1, p2)
+    assert not np.array_equal(o1[6:13], o3[6:13])  # commands differ across envs
+
+
+def test_autoreset_restores_first_state(m, om):
+    e = _env(m, om, auto_reset=True, episode_length=5)
+    o0, p0 = e.reset(seed=1)
+    for t in range(5):
+        o, p, r, done = e.step(np.zeros(m.nu))
+    assert done == 1.0
+    np.testing.assert_array_equal(o, o0)
+    o, p, r, done = e.step(np.zeros(m.nu))
+    assert done == 0.0
+
+
+def test_batch_equals_single_env(m, om):
+    """The OpenMP batch (SoA, stride n) gives the single-env results column by column."""
+    n = 6
+    cfg = env_config_struct(m, default_config(), False)
+    b = OracleBatch(om, cfg, n)
+    b.reset(seed=2, threads=2)
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(-1, 1, (3, n, m.nu))
+    for a in acts:
+        b.step(a, threads=2)
+    for env_id in (0, 4):
+        e = OracleEnv(om, cfg)
+        e.reset(seed=2, env_id=env_id)
+        for a in acts:
+            o, p, r, done = e.step(a[env_id])
+        np.testing.assert_array_equal(b.obs[env_id], o)
+        np.testing.assert_array_equal(b.rew[env_id], r)
