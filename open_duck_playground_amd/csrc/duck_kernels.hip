@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(WG) reset_kernel(KArgs A) {
   if (e >= A.n) return;
   if (A.mask && !A.mask[e]) return;
   extern __shared__ float lds[];
-  Slice<WG> L{lds + threadIdx.x};
+  Slice<WG> L{(lds_float*)(lds + threadIdx.x)};
   const duck_env_config& c = A.cfg;
   const duck_layout& Lo = A.lay;
   constexpr int NQ = Md::NQ, NV = Md::NV, NU = Md::NU;
@@ -300,7 +300,7 @@ __global__ void __launch_bounds__(WG) step_kernel(KArgs A) {
   const int e = blockIdx.x * WG + threadIdx.x;
   if (e >= A.n) return;
   extern __shared__ float lds[];
-  Slice<WG> L{lds + threadIdx.x};
+  Slice<WG> L{(lds_float*)(lds + threadIdx.x)};
   const duck_env_config& c = A.cfg;
   const duck_layout& Lo = A.lay;
   constexpr int NQ = Md::NQ, NV = Md::NV, NU = Md::NU;
@@ -488,7 +488,7 @@ __global__ void __launch_bounds__(WG) physics_kernel(KArgs A, float* qpos_g, flo
   const int n = A.n;
   if (e >= n) return;
   extern __shared__ float lds[];
-  Slice<WG> L{lds + threadIdx.x};
+  Slice<WG> L{(lds_float*)(lds + threadIdx.x)};
   for (int i = 0; i < Md::NQ; i++) L[Ly::QPOS + i] = qpos_g[(size_t)i * n + e];
   for (int i = 0; i < Md::NV; i++) { L[Ly::QVEL + i] = qvel_g[(size_t)i * n + e]; L[Ly::WARM + i] = warm_g[(size_t)i * n + e]; }
   for (int a = 0; a < Md::NU; a++) L[Ly::CTRL + a] = ctrl_g[(size_t)a * n + e];
@@ -537,7 +537,10 @@ __global__ void randomize_kernel(int n, float* dr, duck_dr_layout D, uint64_t se
 // host side
 // --------------------------------------------------------------------------------------
 enum Variant { V_FLAT = 0, V_BACKLASH = 1 };
-constexpr int WG = 16;  // one 16-lane wave per workgroup: 4096 envs fill all 256 CUs
+#ifndef DUCK_WG
+#define DUCK_WG 16
+#endif
+constexpr int WG = DUCK_WG;  // lanes (= envs) per workgroup: 16 -> 4096 envs fill all 256 CUs
 
 struct duck_sim {
   int device;

@@ -22,11 +22,19 @@
 #include "duck_math.h"
 
 #define DNI __device__ __noinline__
+// compiler-only barrier: stops the scheduler from hoisting a whole unrolled loop's LDS
+// loads into registers at once (which spills); costs no instruction
+#define SCHED_FENCE() asm volatile("" ::: "memory")
+
+// LDS-qualified pointer: keeps every slice access a ds_read/ds_write (a generic float*
+// passed into a non-inlined stage would compile to flat_load/flat_store through the
+// vector-memory pipe)
+typedef __attribute__((address_space(3))) float lds_float;
 
 template <int WG>
 struct Slice {
-  float* p;
-  DK float& operator[](int k) const { return p[k * WG]; }
+  lds_float* p;
+  DK lds_float& operator[](int k) const { return p[k * WG]; }
 };
 
 // Per-lane LDS layout (floats)
@@ -266,6 +274,7 @@ struct Phys {
 #pragma unroll
     for (int b = 1; b < NB; b++) {
       if (Md::body_weldid[b] == 0) continue;
+      SCHED_FENCE();
       float R[9], t[3], ip[3];
 #pragma unroll
       for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
@@ -283,6 +292,7 @@ struct Phys {
 #pragma unroll
     for (int b = 1; b < NB; b++) {
       if (Md::body_weldid[b] == 0) continue;
+      SCHED_FENCE();
       float R[9], t[3], ip[3], Ri[9];
 #pragma unroll
       for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
@@ -312,6 +322,7 @@ struct Phys {
     }
 #pragma unroll
     for (int j = 0; j < Md::NJ; j++) {
+      SCHED_FENCE();
       const int b = Md::jnt_bodyid[j], da = Md::jnt_dofadr[j];
       const float off[3] = {com[0] - L[Ly::XPOS + 3 * b], com[1] - L[Ly::XPOS + 3 * b + 1], com[2] - L[Ly::XPOS + 3 * b + 2]};
       if (Md::jnt_type[j] == 0) {
@@ -344,6 +355,7 @@ struct Phys {
 #pragma unroll
     for (int b = 1; b < NB; b++) {
       if (Md::body_weldid[b] == 0) continue;
+      SCHED_FENCE();
       const int pa = Md::body_parentid[b];
       float cv[6], ca[6];
 #pragma unroll
@@ -409,6 +421,7 @@ struct Phys {
     }
 #pragma unroll
     for (int i = 0; i < NV; i++) {
+      SCHED_FENCE();
       const int b = Md::dof_bodyid[i];
       float s = 0.0f;
 #pragma unroll
@@ -428,6 +441,7 @@ struct Phys {
     }
 #pragma unroll
     for (int i = 0; i < NV; i++) {
+      SCHED_FENCE();
       float cd[6], buf[6], I[10];
 #pragma unroll
       for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
@@ -437,6 +451,7 @@ struct Phys {
 #pragma unroll
       for (int j = 0; j <= i; j++) {
         if (Md::M_adr[i][j] >= 0) {
+          SCHED_FENCE();
           float s = 0.0f;
 #pragma unroll
           for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * j + k] * buf[k];
@@ -1134,6 +1149,7 @@ struct Phys {
     }
 #pragma unroll
     for (int s = 0; s < Md::NSENSOR; s++) {
+      SCHED_FENCE();
       const int typ = Md::sensor_type[s], site = Md::sensor_objid[s], adr = Md::sensor_adr[s];
       const int b = Md::site_bodyid[site];
       float R[9], sp[3], sR[9], t[3];

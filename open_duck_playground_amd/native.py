@@ -13,7 +13,7 @@ import subprocess
 from .cabi import DuckEnvConfig, DuckModelDesc, DuckRefMotion
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libduck.so")
+LIB_PATH = os.environ.get("DUCK_LIB") or os.path.join(HERE, "libduck.so")
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 
