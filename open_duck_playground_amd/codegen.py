@@ -116,6 +116,64 @@ def sparse_code(m: Model, adr) -> str:
     return "".join(o)
 
 
+def team_tables(m: Model, rows, adr, pre: str, floor: int):
+    """Index tables for the team (16 lanes per env) kernel: lanes pick their work items
+    (bodies of a tree level, mass-matrix entries, LDL updates) from these."""
+    nb, nv = m.nbody, m.nv
+    depth = np.zeros(nb, dtype=int)
+    for b in range(1, nb):
+        depth[b] = depth[m.body_parentid[b]] + 1
+    nlev = int(depth.max())
+    levels = [[b for b in range(1, nb) if depth[b] == lv + 1] for lv in range(nlev)]
+    levw = max(len(lv) for lv in levels)
+    assert levw <= 16
+    lev = np.full((nlev, levw), -1)
+    for i, lv in enumerate(levels):
+        lev[i, :len(lv)] = lv
+    children = [[c for c in range(1, nb) if m.body_parentid[c] == b] for b in range(nb)]
+    maxch = max(1, max(len(c) for c in children))
+    child = np.full((nb, maxch), -1)
+    for b, c in enumerate(children):
+        child[b, :len(c)] = c
+    full = np.full((nv, nv), -1)
+    mi, mj = np.zeros(int(adr.max()) + 1, dtype=int), np.zeros(int(adr.max()) + 1, dtype=int)
+    for i in range(nv):
+        for j in rows[i]:
+            full[i, j] = full[j, i] = adr[i, j]
+            mi[adr[i, j]], mj[adr[i, j]] = i, j
+    ldl, ldl_off = [], [0]
+    anc_dof, anc_adr, anc_off = [], [], [0]
+    for k in range(nv):
+        for i in _ancestors(m, k, False):
+            for j in _ancestors(m, i, True):
+                ldl.append((adr[i, j], adr[k, i], adr[k, j]))
+            anc_dof.append(i)
+            anc_adr.append(adr[k, i])
+        ldl_off.append(len(ldl))
+        anc_off.append(len(anc_dof))
+    pplane = [p for p in range(m.npair) if m.pair_geom1[p] == floor]
+    pfoot = [p for p in range(m.npair) if m.pair_geom1[p] != floor]
+    assert len(pplane) == 2 and len(pfoot) <= 1
+    T = lambda name, a, t: f"__device__ const {t} {pre}_{name}{''.join(f'[{d}]' for d in np.shape(a))} = " + \
+        _arr("x", np.asarray(a), t).split("= ", 1)[1]
+    tabs = {"lev": (lev, "int"), "child": (child, "int"), "madr": (full, "int"), "mi": (mi, "int"), "mj": (mj, "int"),
+            "ldl": (np.array(ldl).reshape(-1, 3), "int"), "ldl_off": (ldl_off, "int"), "anc_dof": (anc_dof, "int"),
+            "anc_adr": (anc_adr, "int"), "anc_off": (anc_off, "int")}
+    dev = [T(k, a, t) for k, (a, t) in tabs.items()]
+    acc = [f"  static constexpr int T_NLEV = {nlev}, T_LEVW = {levw}, T_MAXCH = {maxch};\n",
+           f"  static constexpr int T_MAXLDL = {max(ldl_off[k + 1] - ldl_off[k] for k in range(nv))}, "
+           f"T_MAXANC = {max(anc_off[k + 1] - anc_off[k] for k in range(nv))};\n",
+           f"  static constexpr int PLANE_PAIR[2] = {{{pplane[0]}, {pplane[1]}}};\n",
+           f"  static constexpr int FOOT_PAIR = {pfoot[0] if pfoot else -1};\n"]
+    for k, (a, t) in tabs.items():
+        shp = np.shape(a)
+        if len(shp) == 1:
+            acc.append(f"  static __device__ __forceinline__ const {t}* t_{k}() {{ return {pre}_{k}; }}\n")
+        else:
+            acc.append(f"  static __device__ __forceinline__ const {t} (*t_{k}())[{shp[1]}] {{ return {pre}_{k}; }}\n")
+    return dev, acc
+
+
 def model_header(m: Model, variant: str) -> str:
     nb, nv, nq, nu, nj = m.nbody, m.nv, m.nq, m.nu, m.njnt
     rows, adr, nm = sparse_pattern(m)
@@ -236,8 +294,10 @@ def model_header(m: Model, variant: str) -> str:
     out.append(_arr("fric_dof", fric, "int"))
     out.append(_arr("lim_jnt", lim, "int"))
     out.append(sparse_code(m, adr))
+    tdev, tacc = team_tables(m, rows, adr, pre, floor)
+    out.extend(tacc)
     out.append("};\n")
-    return "".join(out)
+    return "".join(out[:2] + tdev + out[2:])
 
 
 def main():

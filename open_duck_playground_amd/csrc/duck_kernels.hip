@@ -15,6 +15,7 @@
 
 #include "../../include/duck.h"
 #include "duck_physics.h"
+#include "duck_team.h"
 #include "generated/duck_model_backlash.h"
 #include "generated/duck_model_flat.h"
 
@@ -66,6 +67,63 @@ struct KArgs {
   duck_layout lay;
   duck_dr_layout drl;
 };
+
+// Launch geometry. Team mode (default): 16 lanes per env, 16 envs (4 waves) per workgroup,
+// so 4096 envs are exactly one workgroup per CU. Single-lane mode (-DDUCK_TEAM=0): one env
+// per lane, WG envs per workgroup, EPW envs per wave.
+#ifndef DUCK_TEAM
+#define DUCK_TEAM 1
+#endif
+#if DUCK_TEAM
+constexpr int WG = 16;
+constexpr int EPW = 4;
+constexpr int TPB = WG * TEAM;
+constexpr int SW = 1;  // slice stride (contiguous per-env slices)
+#else
+#ifndef DUCK_WG
+#define DUCK_WG 16
+#endif
+#ifndef DUCK_EPW
+#define DUCK_EPW DUCK_WG
+#endif
+constexpr int WG = DUCK_WG;
+constexpr int EPW = DUCK_EPW;
+static_assert(WG % EPW == 0 && EPW <= 64, "EPW must divide WG");
+constexpr int TPB = EPW >= WG ? WG : (WG / EPW) * 64;  // threads per block
+constexpr int SW = WG;  // slice stride (interleaved per-lane slices)
+#endif
+
+// this lane's env within the workgroup (-1: idle lane) and its rank in the env's team
+DK int local_env(int& lane) {
+#if DUCK_TEAM
+  lane = threadIdx.x % TEAM;
+  return threadIdx.x / TEAM;
+#else
+  lane = 0;
+  if (EPW >= WG) return threadIdx.x;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  return l < EPW ? w * EPW + l : -1;
+#endif
+}
+
+template <class Md>
+DK Slice<SW> env_slice(float* lds, int t) {
+#if DUCK_TEAM
+  return Slice<SW>{(lds_float*)(lds + t * TLay<Md>::STRIDE)};
+#else
+  return Slice<SW>{(lds_float*)(lds + t)};
+#endif
+}
+
+template <class Md>
+DK void phys_step(Slice<SW> L, int lane, bool integrate, bool want_out, float* aux, int aux_stride, float* scratch,
+                  int sstride) {
+#if DUCK_TEAM
+  TPhys<Md>::step(L.p, lane, integrate, want_out, aux, aux_stride, scratch, sstride);
+#else
+  Phys<Md, WG>::step(L, integrate, want_out, aux, aux_stride, scratch, sstride);
+#endif
+}
 
 template <int WG>
 struct Col {  // SoA accessor for env e
@@ -233,13 +291,16 @@ DK void write_obs(const KArgs& A, int e, Slice<WG> L, const Rng& r, int slot_bas
 }
 
 template <class Md, int WG>
-__global__ void __launch_bounds__(WG) reset_kernel(KArgs A) {
+__global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
   using Ly = Lay<Md>;
-  const int e = blockIdx.x * WG + threadIdx.x;
+  int lane;
+  const int t = local_env(lane);
+  if (t < 0) return;
+  const int e = blockIdx.x * WG + t;
   if (e >= A.n) return;
   if (A.mask && !A.mask[e]) return;
   extern __shared__ float lds[];
-  Slice<WG> L{(lds_float*)(lds + threadIdx.x)};
+  const Slice<SW> L = env_slice<Md>(lds, t);
   const duck_env_config& c = A.cfg;
   const duck_layout& Lo = A.lay;
   constexpr int NQ = Md::NQ, NV = Md::NV, NU = Md::NU;
@@ -250,7 +311,7 @@ __global__ void __launch_bounds__(WG) reset_kernel(KArgs A) {
   Rng r;
   derive_key(A.seed, A.env_offset + e, KEY_TAG_ENV, r.k0, r.k1);
   r.ctr = 0;
-  load_dyn<Md, WG>(A, e, L);
+  load_dyn<Md, SW>(A, e, L);
   // Joystick.reset (joystick.py:206-258)
   for (int i = 0; i < NQ; i++) L[Ly::QPOS + i] = c.init_qpos[i];
   for (int i = 0; i < NV; i++) { L[Ly::QVEL + i] = 0.0f; L[Ly::WARM + i] = 0.0f; }
@@ -268,7 +329,7 @@ __global__ void __launch_bounds__(WG) reset_kernel(KArgs A) {
   for (int a = 0; a < NU; a++) L[Ly::QPOS + c.actuator_qposadr[a]] *= r.uniform(RSLOT_QSCALE + a, 0.5f, 1.5f);
   for (int k = 0; k < 6; k++) L[Ly::QVEL + k] = r.uniform(RSLOT_QVEL + k, -0.05f, 0.05f);
   for (int a = 0; a < NU; a++) L[Ly::CTRL + a] = L[Ly::QPOS + c.actuator_qposadr[a]];
-  Phys<Md, WG>::step(L, false, true, nullptr, 0, A.scratch ? A.scratch + e : nullptr, A.n);
+  phys_step<Md>(L, lane, false, true, nullptr, 0, A.scratch ? A.scratch + e : nullptr, A.n);
   float cmd[7];
   sample_command(c, r, RSLOT_CMD, cmd);
   const float push_interval = r.uniform(RSLOT_PUSH, c.push_interval_range[0], c.push_interval_range[1]);
@@ -289,18 +350,21 @@ __global__ void __launch_bounds__(WG) reset_kernel(KArgs A) {
     F[Lo.qacc_warmstart + i] = L[Ly::WARM + i]; F[Lo.first_qacc_warmstart + i] = L[Ly::WARM + i];
   }
   for (int a = 0; a < NU; a++) { F[Lo.ctrl + a] = L[Ly::CTRL + a]; F[Lo.first_ctrl + a] = L[Ly::CTRL + a]; }
-  write_obs<Md, WG>(A, e, L, r, RSLOT_OBS, 0);
+  write_obs<Md, SW>(A, e, L, r, RSLOT_OBS, 0);
   for (int k = 0; k < Lo.obs_size; k++) F[Lo.first_obs + k] = A.obs[(size_t)e * Lo.obs_size + k];
   for (int k = 0; k < Lo.priv_size; k++) F[Lo.first_priv + k] = A.priv[(size_t)e * Lo.priv_size + k];
 }
 
 template <class Md, int WG>
-__global__ void __launch_bounds__(WG) step_kernel(KArgs A) {
+__global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   using Ly = Lay<Md>;
-  const int e = blockIdx.x * WG + threadIdx.x;
+  int lane;
+  const int t = local_env(lane);
+  if (t < 0) return;
+  const int e = blockIdx.x * WG + t;
   if (e >= A.n) return;
   extern __shared__ float lds[];
-  Slice<WG> L{(lds_float*)(lds + threadIdx.x)};
+  const Slice<SW> L = env_slice<Md>(lds, t);
   const duck_env_config& c = A.cfg;
   const duck_layout& Lo = A.lay;
   constexpr int NQ = Md::NQ, NV = Md::NV, NU = Md::NU;
@@ -357,10 +421,10 @@ __global__ void __launch_bounds__(WG) step_kernel(KArgs A) {
   for (int i = 0; i < NV; i++) { L[Ly::QVEL + i] = F[Lo.qvel + i]; L[Ly::WARM + i] = F[Lo.qacc_warmstart + i]; }
   L[Ly::QVEL + 0] += push[0] * mag;
   L[Ly::QVEL + 1] += push[1] * mag;
-  load_dyn<Md, WG>(A, e, L);
+  load_dyn<Md, SW>(A, e, L);
   // physics (joystick.py:420)
   float* scr = A.scratch ? A.scratch + e : nullptr;
-  for (int s = 0; s < c.n_substeps; s++) Phys<Md, WG>::step(L, true, s == c.n_substeps - 1, nullptr, 0, scr, n);
+  for (int s = 0; s < c.n_substeps; s++) phys_step<Md>(L, lane, true, s == c.n_substeps - 1, nullptr, 0, scr, n);
   for (int a = 0; a < NU; a++) { F[Lo.motor_targets + a] = L[Ly::CTRL + a]; F[Lo.ctrl + a] = L[Ly::CTRL + a]; }
   const float con[2] = {L[Ly::OCON], L[Ly::OCON + 1]};
   // feet bookkeeping (joystick.py:424-435)
@@ -368,7 +432,7 @@ __global__ void __launch_bounds__(WG) step_kernel(KArgs A) {
     F[Lo.feet_air_time + k] = F[Lo.feet_air_time + k] + dt;
     F[Lo.swing_peak + k] = fmaxf(F[Lo.swing_peak + k], L[Ly::FOOTZ + k]);
   }
-  write_obs<Md, WG>(A, e, L, r, 0, imitation_i);
+  write_obs<Md, SW>(A, e, L, r, 0, imitation_i);
   // termination (joystick.py:483-485)
   bool nan = false;
   for (int i = 0; i < NQ; i++) nan = nan || isnan(L[Ly::QPOS + i]);
@@ -481,24 +545,27 @@ __global__ void __launch_bounds__(WG) step_kernel(KArgs A) {
 }
 
 template <class Md, int WG>
-__global__ void __launch_bounds__(WG) physics_kernel(KArgs A, float* qpos_g, float* qvel_g, float* warm_g,
+__global__ void __launch_bounds__(TPB) physics_kernel(KArgs A, float* qpos_g, float* qvel_g, float* warm_g,
                                                      const float* ctrl_g, int nsub, float* aux) {
   using Ly = Lay<Md>;
-  const int e = blockIdx.x * WG + threadIdx.x;
+  int lane;
+  const int t = local_env(lane);
+  if (t < 0) return;
+  const int e = blockIdx.x * WG + t;
   const int n = A.n;
   if (e >= n) return;
   extern __shared__ float lds[];
-  Slice<WG> L{(lds_float*)(lds + threadIdx.x)};
+  const Slice<SW> L = env_slice<Md>(lds, t);
   for (int i = 0; i < Md::NQ; i++) L[Ly::QPOS + i] = qpos_g[(size_t)i * n + e];
   for (int i = 0; i < Md::NV; i++) { L[Ly::QVEL + i] = qvel_g[(size_t)i * n + e]; L[Ly::WARM + i] = warm_g[(size_t)i * n + e]; }
   for (int a = 0; a < Md::NU; a++) L[Ly::CTRL + a] = ctrl_g[(size_t)a * n + e];
-  load_dyn<Md, WG>(A, e, L);
+  load_dyn<Md, SW>(A, e, L);
   float* ax = aux ? aux + e : nullptr;
   float* scr = A.scratch ? A.scratch + e : nullptr;
   if (nsub == 0) {
-    Phys<Md, WG>::step(L, false, true, ax, n, scr, n);
+    phys_step<Md>(L, lane, false, true, ax, n, scr, n);
   } else {
-    for (int s = 0; s < nsub; s++) Phys<Md, WG>::step(L, true, s == nsub - 1, ax, n, scr, n);
+    for (int s = 0; s < nsub; s++) phys_step<Md>(L, lane, true, s == nsub - 1, ax, n, scr, n);
   }
   for (int i = 0; i < Md::NQ; i++) qpos_g[(size_t)i * n + e] = L[Ly::QPOS + i];
   for (int i = 0; i < Md::NV; i++) { qvel_g[(size_t)i * n + e] = L[Ly::QVEL + i]; warm_g[(size_t)i * n + e] = L[Ly::WARM + i]; }
@@ -537,10 +604,6 @@ __global__ void randomize_kernel(int n, float* dr, duck_dr_layout D, uint64_t se
 // host side
 // --------------------------------------------------------------------------------------
 enum Variant { V_FLAT = 0, V_BACKLASH = 1 };
-#ifndef DUCK_WG
-#define DUCK_WG 16
-#endif
-constexpr int WG = DUCK_WG;  // lanes (= envs) per workgroup: 16 -> 4096 envs fill all 256 CUs
 
 struct duck_sim {
   int device;
@@ -576,7 +639,11 @@ static bool matches(const duck_model_desc* m) {
 
 template <class Md>
 static size_t lds_bytes() {
+#if DUCK_TEAM
+  return (size_t)TLay<Md>::STRIDE * WG * sizeof(float);
+#else
   return (size_t)Lay<Md>::TOTAL * WG * sizeof(float);
+#endif
 }
 
 static KArgs make_args(duck_sim* s, int n) {
@@ -593,7 +660,7 @@ static KArgs make_args(duck_sim* s, int n) {
 
 template <class Md>
 static int launch_reset(duck_sim* s, KArgs& A, hipStream_t st) {
-  const dim3 grid((A.n + WG - 1) / WG), block(WG);
+  const dim3 grid((A.n + WG - 1) / WG), block(TPB);
   hipLaunchKernelGGL((reset_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A);
   HIPCHECK(hipGetLastError());
   return DUCK_OK;
@@ -601,7 +668,7 @@ static int launch_reset(duck_sim* s, KArgs& A, hipStream_t st) {
 
 template <class Md>
 static int launch_step(duck_sim* s, KArgs& A, hipStream_t st) {
-  const dim3 grid((A.n + WG - 1) / WG), block(WG);
+  const dim3 grid((A.n + WG - 1) / WG), block(TPB);
   hipLaunchKernelGGL((step_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A);
   HIPCHECK(hipGetLastError());
   return DUCK_OK;
@@ -610,7 +677,7 @@ static int launch_step(duck_sim* s, KArgs& A, hipStream_t st) {
 template <class Md>
 static int launch_physics(duck_sim* s, int n, float* qpos, float* qvel, float* warm, const float* ctrl, const float* dr,
                           int nsub, float* aux, float* scratch, hipStream_t st) {
-  const dim3 grid((n + WG - 1) / WG), block(WG);
+  const dim3 grid((n + WG - 1) / WG), block(TPB);
   KArgs A = make_args(s, n);
   A.dr = dr;
   A.scratch = scratch;
@@ -753,3 +820,14 @@ int duck_physics_step(duck_sim* s, int n, float* qpos, float* qvel, float* warm,
 }
 
 }  // extern "C"
+
+#ifdef DUCK_STAGE_PROF
+extern "C" int duck_debug_stage_cycles(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), sizeof(unsigned long long) * 16);
+  if (e == hipSuccess && reset) {
+    unsigned long long z[16] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, sizeof(z));
+  }
+  return e == hipSuccess ? 0 : -3;
+}
+#endif

@@ -31,6 +31,27 @@
 // vector-memory pipe)
 typedef __attribute__((address_space(3))) float lds_float;
 
+// optional per-stage cycle counters (build with -DDUCK_STAGE_PROF; read by duck_debug_stage_cycles)
+#ifdef DUCK_STAGE_PROF
+__device__ unsigned long long g_stage_cycles[16];
+#define STAGE_T0() unsigned long long _t0 = wall_clock64(), _c0 = clock64()
+#define STAGE_MARK(k)                                                             \
+  do {                                                                            \
+    asm volatile("s_waitcnt lgkmcnt(0) vmcnt(0)" ::: "memory");                   \
+    const unsigned long long _c1 = clock64();                                     \
+    if (threadIdx.x == 0) atomicAdd(&g_stage_cycles[k], _c1 - _c0);               \
+    _c0 = _c1;                                                                    \
+    (void)_t0;                                                                    \
+  } while (0)
+#else
+#define STAGE_T0() \
+  do {             \
+  } while (0)
+#define STAGE_MARK(k) \
+  do {                \
+  } while (0)
+#endif
+
 template <int WG>
 struct Slice {
   lds_float* p;
@@ -1246,16 +1267,25 @@ struct Phys {
 
   // one substep: forward (+ outputs when want_out) and optional integration
   static DK void step(S L, bool integrate, bool want_out, float* aux, int aux_stride, float* scratch, int sstride) {
+    STAGE_T0();
     kinematics(L);
+    STAGE_MARK(0);
     com_pos(L);
+    STAGE_MARK(1);
     rne(L);
+    STAGE_MARK(2);
     crb(L);
+    STAGE_MARK(3);
     smooth(L);
     factor_H(L);
     solve_H(L, Ly::FSM, Ly::QSM, 1.0f);
+    STAGE_MARK(4);
     collision(L);
+    STAGE_MARK(5);
     make_rows(L);
+    STAGE_MARK(6);
     solve(L, scratch, sstride);
+    STAGE_MARK(7);
     if (want_out) {
       sensors(L);
       if (aux) write_aux(L, aux, aux_stride);
@@ -1263,6 +1293,7 @@ struct Phys {
 #pragma unroll
     for (int i = 0; i < NV; i++) L[Ly::WARM + i] = L[Ly::QACC + i];
     if (integrate) euler(L);
+    STAGE_MARK(8);
   }
 };
 

@@ -1,0 +1,1016 @@
+// duck_team.h — mjx.step with a team of 16 lanes per env (CDNA4, fp32).
+//
+// Same physics, same LDS layout (Lay<Md>) and same arithmetic as duck_physics.h, but each
+// env is worked by 16 consecutive lanes of a wave (4 envs per wave, 4 waves per CU at
+// 16 envs per CU): lanes split every stage's independent items — bodies of one tree level,
+// degrees of freedom, mass-matrix entries, LDL' updates of one pivot, hull vertices,
+// constraint rows — and combine with DPP row reductions. A team never spans waves, so a
+// team barrier is only a compiler ordering point (LDS operations of one wave complete in
+// issue order).
+//
+// The env slice is contiguous (element k of env t at lds[t*STRIDE + k]); STRIDE = 16 mod 32
+// so the two teams of a 32-lane half hit disjoint banks. Rare paths (foot/foot contact)
+// fall back to the single-lane code of duck_physics.h executed identically by all 16 lanes.
+#pragma once
+#include "duck_physics.h"
+
+constexpr int TEAM = 16;
+
+#define TSYNC()                           \
+  do {                                    \
+    asm volatile("" ::: "memory");        \
+    __builtin_amdgcn_wave_barrier();      \
+    asm volatile("" ::: "memory");        \
+  } while (0)
+
+template <int CTRL>
+DK float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+DK int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+// reductions over the 16 lanes of a DPP row (= one team); every lane gets the result
+DK float tsum(float v) {
+  v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dppf<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dppf<0x141>(v);  // row_half_mirror
+  v += dppf<0x140>(v);  // row_mirror
+  return v;
+}
+// reductions over the 8-lane halves of a team
+DK float hmax8(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  return v;
+}
+DK int hmin8i(int v) {
+  v = min(v, dppi<0xB1>(v));
+  v = min(v, dppi<0x4E>(v));
+  v = min(v, dppi<0x141>(v));
+  return v;
+}
+
+template <class Md>
+struct TLay {
+  using Ly = Lay<Md>;
+  static constexpr int KC = Ly::TOTAL;                 // K.cdof per chain dof (6 x MAXCHAIN)
+  static constexpr int TSP = KC + 6 * Md::MAXCHAIN;    // foot spatial motions (12)
+  static constexpr int USED = TSP + 12;
+  static constexpr int STRIDE = ((USED + 15) / 32) * 32 + 16;  // = 16 (mod 32), >= USED
+  static_assert(STRIDE >= USED && STRIDE % 32 == 16, "stride");
+  static constexpr int FTMP = Ly::JA;                  // crb: F_i = I_b cdof_i (dead row storage)
+  static_assert(6 * Md::NV <= 4 * Ly::NROW, "crb scratch must fit in the row storage");
+};
+
+template <class Md>
+struct TPhys {
+  using Ly = Lay<Md>;
+  using TL = TLay<Md>;
+  using P1 = Phys<Md, 1>;
+  using S1 = Slice<1>;
+  typedef lds_float* LP;
+  static constexpr int NV = Md::NV, NB = Md::NB, NQ = Md::NQ, NU = Md::NU, NJ = Md::NJ;
+  static constexpr int NCON = Ly::NCON, NFRIC = Md::NFRIC, NLIM = Md::NLIM, NROW = Ly::NROW;
+  static constexpr int R_LIM = Ly::R_LIM, R_CON = Ly::R_CON;
+  static_assert(NFRIC <= TEAM, "one friction row per lane");
+  static_assert(NCON <= TEAM, "one contact slot per lane");
+  static_assert(NU <= TEAM, "one actuator per lane");
+
+  // ---------------- mj_kinematics: one tree level at a time, a body per lane ----------------
+  static DNI void kinematics(LP L, int lane) {
+    const int(*LEV)[Md::T_LEVW] = Md::t_lev();
+    for (int lv = 0; lv < Md::T_NLEV; lv++) {
+      const int b = lane < Md::T_LEVW ? LEV[lv][lane] : -1;
+      if (b > 0) {
+        float p[3], q[4];
+        const int pa = Md::body_parentid[b];
+        if (b == 1) {
+          p[0] = L[Ly::QPOS + 0]; p[1] = L[Ly::QPOS + 1]; p[2] = L[Ly::QPOS + 2];
+          q[0] = L[Ly::QPOS + 3]; q[1] = L[Ly::QPOS + 4]; q[2] = L[Ly::QPOS + 5]; q[3] = L[Ly::QPOS + 6];
+        } else {
+          const float bq[4] = {Md::body_quat[b][0], Md::body_quat[b][1], Md::body_quat[b][2], Md::body_quat[b][3]};
+          const float bp[3] = {Md::body_pos[b][0], Md::body_pos[b][1], Md::body_pos[b][2]};
+          if (pa == 0) {
+            for (int k = 0; k < 3; k++) p[k] = bp[k];
+            for (int k = 0; k < 4; k++) q[k] = bq[k];
+          } else {
+            float R[9], pq[4], t[3];
+            for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * pa + k];
+            for (int k = 0; k < 4; k++) pq[k] = L[Ly::XQ + 4 * pa + k];
+            mulmv3(t, R, bp);
+            for (int k = 0; k < 3; k++) p[k] = L[Ly::XPOS + 3 * pa + k] + t[k];
+            qmul(q, pq, bq);
+          }
+          const int nj = Md::body_jntnum[b], j0 = Md::body_jntadr[b];
+          for (int jj = 0; jj < nj; jj++) {
+            const int j = j0 + jj, a = Md::jnt_qposadr[j];
+            float s, c;
+            sincosf(0.5f * (L[Ly::QPOS + a] - L[Ly::DQ0 + a]), &s, &c);
+            const float ql[4] = {c, Md::jnt_axis[j][0] * s, Md::jnt_axis[j][1] * s, Md::jnt_axis[j][2] * s};
+            qmul(q, q, ql);
+          }
+        }
+        qnormalize(q);
+        float R[9];
+        q2m(R, q);
+        for (int k = 0; k < 3; k++) L[Ly::XPOS + 3 * b + k] = p[k];
+        for (int k = 0; k < 4; k++) L[Ly::XQ + 4 * b + k] = q[k];
+        for (int k = 0; k < 9; k++) L[Ly::XMAT + 9 * b + k] = R[k];
+      }
+      TSYNC();
+    }
+  }
+
+  // ---------------- mj_comPos: subtree com (team reduction), cinert, cdof ----------------
+  static DNI void com_pos(LP L, int lane) {
+    float ms = 0.0f, cx = 0.0f, cy = 0.0f, cz = 0.0f;
+    for (int b = 1 + lane; b < NB; b += TEAM) {
+      if (Md::body_weldid[b] == 0) continue;
+      float R[9], t[3], ip[3];
+      for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
+      for (int k = 0; k < 3; k++) ip[k] = (b == 1) ? L[Ly::DIPOS + k] : Md::body_ipos[b][k];
+      mulmv3(t, R, ip);
+      const float m = L[Ly::DMASS + b];
+      ms += m;
+      cx += m * (L[Ly::XPOS + 3 * b] + t[0]);
+      cy += m * (L[Ly::XPOS + 3 * b + 1] + t[1]);
+      cz += m * (L[Ly::XPOS + 3 * b + 2] + t[2]);
+    }
+    ms = tsum(ms);
+    const float inv = 1.0f / ms;
+    const float com[3] = {tsum(cx) * inv, tsum(cy) * inv, tsum(cz) * inv};
+    if (lane == 0)
+      for (int k = 0; k < 3; k++) L[Ly::COM + k] = com[k];
+    for (int b = 1 + lane; b < NB; b += TEAM) {
+      if (Md::body_weldid[b] == 0) continue;
+      float R[9], t[3], ip[3], Ri[9], Bi[9];
+      for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
+      for (int k = 0; k < 3; k++) ip[k] = (b == 1) ? L[Ly::DIPOS + k] : Md::body_ipos[b][k];
+      for (int k = 0; k < 9; k++) Bi[k] = Md::body_imat[b][k];
+      mulmv3(t, R, ip);
+      mulmm3(Ri, R, Bi);
+      const float I[3] = {Md::body_inertia[b][0], Md::body_inertia[b][1], Md::body_inertia[b][2]};
+      float rot[9];
+      for (int a = 0; a < 3; a++)
+        for (int c = 0; c < 3; c++)
+          rot[3 * a + c] = Ri[3 * a] * I[0] * Ri[3 * c] + Ri[3 * a + 1] * I[1] * Ri[3 * c + 1] + Ri[3 * a + 2] * I[2] * Ri[3 * c + 2];
+      const float d[3] = {L[Ly::XPOS + 3 * b] + t[0] - com[0], L[Ly::XPOS + 3 * b + 1] + t[1] - com[1],
+                          L[Ly::XPOS + 3 * b + 2] + t[2] - com[2]};
+      const float m = L[Ly::DMASS + b], dd = dot3(d, d);
+      const int o = Ly::CIN + 10 * b;
+      L[o + 0] = rot[0] + m * (dd - d[0] * d[0]);
+      L[o + 1] = rot[4] + m * (dd - d[1] * d[1]);
+      L[o + 2] = rot[8] + m * (dd - d[2] * d[2]);
+      L[o + 3] = rot[1] - m * d[0] * d[1];
+      L[o + 4] = rot[2] - m * d[0] * d[2];
+      L[o + 5] = rot[5] - m * d[1] * d[2];
+      L[o + 6] = m * d[0]; L[o + 7] = m * d[1]; L[o + 8] = m * d[2];
+      L[o + 9] = m;
+    }
+    for (int j = lane; j < NJ; j += TEAM) {
+      const int b = Md::jnt_bodyid[j], da = Md::jnt_dofadr[j];
+      const float off[3] = {com[0] - L[Ly::XPOS + 3 * b], com[1] - L[Ly::XPOS + 3 * b + 1], com[2] - L[Ly::XPOS + 3 * b + 2]};
+      if (Md::jnt_type[j] == 0) {
+        for (int k = 0; k < 3; k++)
+          for (int q = 0; q < 6; q++) L[Ly::CDOF + 6 * (da + k) + q] = (q == 3 + k) ? 1.0f : 0.0f;
+        for (int k = 0; k < 3; k++) {
+          const float ax[3] = {L[Ly::XMAT + 9 * b + k], L[Ly::XMAT + 9 * b + 3 + k], L[Ly::XMAT + 9 * b + 6 + k]};
+          float t[3];
+          cross3(t, ax, off);
+          const int o = Ly::CDOF + 6 * (da + 3 + k);
+          L[o] = ax[0]; L[o + 1] = ax[1]; L[o + 2] = ax[2]; L[o + 3] = t[0]; L[o + 4] = t[1]; L[o + 5] = t[2];
+        }
+      } else {
+        float R[9], ax[3], t[3];
+        const float ja[3] = {Md::jnt_axis[j][0], Md::jnt_axis[j][1], Md::jnt_axis[j][2]};
+        for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
+        mulmv3(ax, R, ja);
+        cross3(t, ax, off);
+        const int o = Ly::CDOF + 6 * da;
+        L[o] = ax[0]; L[o + 1] = ax[1]; L[o + 2] = ax[2]; L[o + 3] = t[0]; L[o + 4] = t[1]; L[o + 5] = t[2];
+      }
+    }
+    TSYNC();
+  }
+
+  // ---------------- mj_comVel + mj_rne (flg_acc = 0) ----------------
+  static DNI void rne(LP L, int lane) {
+    const int(*LEV)[Md::T_LEVW] = Md::t_lev();
+    const int(*CH)[Md::T_MAXCH] = Md::t_child();
+    for (int lv = 0; lv < Md::T_NLEV; lv++) {
+      const int b = lane < Md::T_LEVW ? LEV[lv][lane] : -1;
+      if (b > 0 && Md::body_weldid[b] != 0) {
+        const int pa = Md::body_parentid[b];
+        float cv[6], ca[6];
+        for (int k = 0; k < 6; k++) {
+          cv[k] = (pa == 0) ? 0.0f : L[Ly::CVEL + 6 * pa + k];
+          ca[k] = (pa == 0) ? ((k >= 3) ? -Md::gravity[k - 3] : 0.0f) : L[Ly::CACC + 6 * pa + k];
+        }
+        const int da = Md::body_dofadr[b];
+        if (b == 1) {
+          for (int i = 0; i < 3; i++) {
+            const float v = L[Ly::QVEL + i];
+            for (int k = 0; k < 6; k++) cv[k] += L[Ly::CDOF + 6 * i + k] * v;
+          }
+          float cvt[6];
+          for (int k = 0; k < 6; k++) cvt[k] = cv[k];
+          for (int i = 3; i < 6; i++) {
+            float cd[6], cdd[6];
+            for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
+            cross_motion(cdd, cvt, cd);
+            const float v = L[Ly::QVEL + i];
+            for (int k = 0; k < 6; k++) { L[Ly::CDD1 + 6 * (i - 3) + k] = cdd[k]; ca[k] += cdd[k] * v; cv[k] += cd[k] * v; }
+          }
+        } else {
+          const int nd = Md::body_dofnum[b];
+          for (int jj = 0; jj < nd; jj++) {
+            const int i = da + jj;
+            float cd[6], cdd[6];
+            for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
+            cross_motion(cdd, cv, cd);
+            const float v = L[Ly::QVEL + i];
+            for (int k = 0; k < 6; k++) { ca[k] += cdd[k] * v; cv[k] += cd[k] * v; }
+          }
+        }
+        float I[10], f[6], t1[6], t2[6];
+        for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * b + k];
+        mul_inert_vec(f, I, ca);
+        mul_inert_vec(t1, I, cv);
+        cross_force(t2, cv, t1);
+        for (int k = 0; k < 6; k++) {
+          L[Ly::CFRC + 6 * b + k] = f[k] + t2[k];
+          L[Ly::CVEL + 6 * b + k] = cv[k];
+          L[Ly::CACC + 6 * b + k] = ca[k];
+        }
+      }
+      TSYNC();
+    }
+    // cfrc: children into parents, deepest level first (pull, no write conflicts)
+    for (int lv = Md::T_NLEV - 2; lv >= 0; lv--) {
+      const int b = lane < Md::T_LEVW ? LEV[lv][lane] : -1;
+      if (b > 0 && Md::body_weldid[b] != 0) {
+        for (int c = 0; c < Md::T_MAXCH; c++) {
+          const int ch = CH[b][c];
+          if (ch > 0 && Md::body_weldid[ch] != 0)
+            for (int k = 0; k < 6; k++) L[Ly::CFRC + 6 * b + k] += L[Ly::CFRC + 6 * ch + k];
+        }
+      }
+      TSYNC();
+    }
+    for (int i = lane; i < NV; i += TEAM) {
+      const int b = Md::dof_bodyid[i];
+      float s = 0.0f;
+      for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * i + k] * L[Ly::CFRC + 6 * b + k];
+      L[Ly::FSM + i] = -s;
+    }
+    TSYNC();
+  }
+
+  // ---------------- mj_crb: composite inertias (pull by level) and the sparse M ----------------
+  static DNI void crb(LP L, int lane) {
+    const int(*LEV)[Md::T_LEVW] = Md::t_lev();
+    const int(*CH)[Md::T_MAXCH] = Md::t_child();
+    for (int lv = Md::T_NLEV - 2; lv >= 0; lv--) {
+      const int b = lane < Md::T_LEVW ? LEV[lv][lane] : -1;
+      if (b > 0 && Md::body_weldid[b] != 0) {
+        for (int c = 0; c < Md::T_MAXCH; c++) {
+          const int ch = CH[b][c];
+          if (ch > 0 && Md::body_weldid[ch] != 0)
+            for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * b + k] += L[Ly::CIN + 10 * ch + k];
+        }
+      }
+      TSYNC();
+    }
+    for (int i = lane; i < NV; i += TEAM) {
+      float cd[6], buf[6], I[10];
+      for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
+      for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * Md::dof_bodyid[i] + k];
+      mul_inert_vec(buf, I, cd);
+      for (int k = 0; k < 6; k++) L[TL::FTMP + 6 * i + k] = buf[k];
+    }
+    TSYNC();
+    const int* MI = Md::t_mi();
+    const int* MJ = Md::t_mj();
+    for (int a = lane; a < Md::NM; a += TEAM) {
+      const int i = MI[a], j = MJ[a];
+      float s = 0.0f;
+      for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * j + k] * L[TL::FTMP + 6 * i + k];
+      if (i == j) s += L[Ly::DARM + i];
+      L[Ly::M + a] = s;
+    }
+    TSYNC();
+  }
+
+  // ---------------- actuation + passive; H = M ----------------
+  static DNI void smooth(LP L, int lane) {
+    for (int i = lane; i < NV; i += TEAM) L[Ly::FSM + i] += -Md::dof_damping[i] * L[Ly::QVEL + i];
+    TSYNC();
+    if (lane < NU) {
+      const int a = lane;
+      float c = L[Ly::CTRL + a];
+      if (Md::actuator_ctrllimited[a]) c = fminf(fmaxf(c, Md::actuator_ctrlrange[a][0]), Md::actuator_ctrlrange[a][1]);
+      const float g = Md::actuator_gear[a], kp = L[Ly::DKP + a];
+      const float len = g * L[Ly::QPOS + Md::actuator_qadr[a]], vel = g * L[Ly::QVEL + Md::actuator_dof[a]];
+      float f = kp * c + (-kp * len - Md::actuator_kv[a] * vel);
+      if (Md::actuator_forcelimited[a]) f = fminf(fmaxf(f, Md::actuator_forcerange[a][0]), Md::actuator_forcerange[a][1]);
+      L[Ly::AF + a] = f;
+      L[Ly::FSM + Md::actuator_dof[a]] += g * f;
+    }
+    for (int k = lane; k < Md::NM; k += TEAM) L[Ly::H + k] = L[Ly::M + k];
+    TSYNC();
+  }
+
+  // ---------------- sparse LDL' of H in place (mj_factorM): one pivot per pass ----------------
+  // pass k updates the ancestors' block of pivot k and scales row k+1 (independent data)
+  static DNI void factor_H(LP L, int lane) {
+    const int(*LD)[3] = Md::t_ldl();
+    const int* LO = Md::t_ldl_off();
+    const int* AO = Md::t_anc_off();
+    const int* AA = Md::t_anc_adr();
+    for (int k = NV - 1; k >= -1; k--) {
+      if (k >= 0) {
+        const float inv = 1.0f / L[Ly::H + diag_adr(k)];
+        for (int p = LO[k] + lane; p < LO[k + 1]; p += TEAM) {
+          const int aij = LD[p][0], aki = LD[p][1], akj = LD[p][2];
+          L[Ly::H + aij] -= L[Ly::H + aki] * inv * L[Ly::H + akj];
+        }
+      }
+      const int s = k + 1;  // scale row s (its pass is complete)
+      if (s < NV) {
+        const float dinv = 1.0f / L[Ly::H + diag_adr(s)];
+        for (int p = AO[s] + lane; p < AO[s + 1]; p += TEAM) L[Ly::H + AA[p]] *= dinv;
+      }
+      TSYNC();
+    }
+  }
+
+  static DK int diag_adr(int i) { return Md::t_madr()[i][i]; }
+
+  // DST = sign * H^-1 SRC with H factored in place (mj_solveLD)
+  static DNI void solve_H(LP L, int lane, int SRC, int DST, float sign) {
+    const int* AO = Md::t_anc_off();
+    const int* AD = Md::t_anc_dof();
+    const int* AA = Md::t_anc_adr();
+    for (int i = lane; i < NV; i += TEAM) L[DST + i] = L[SRC + i];
+    TSYNC();
+    for (int k = NV - 1; k >= 0; k--) {
+      const float xk = L[DST + k];
+      for (int p = AO[k] + lane; p < AO[k + 1]; p += TEAM) L[DST + AD[p]] -= L[Ly::H + AA[p]] * xk;
+      TSYNC();
+    }
+    for (int i = lane; i < NV; i += TEAM) L[DST + i] = L[DST + i] / L[Ly::H + diag_adr(i)];
+    TSYNC();
+    for (int k = 0; k < NV; k++) {
+      float s = 0.0f;
+      for (int p = AO[k] + lane; p < AO[k + 1]; p += TEAM) s += L[Ly::H + AA[p]] * L[DST + AD[p]];
+      s = tsum(s);
+      if (lane == 0) L[DST + k] -= s;
+      TSYNC();
+    }
+    if (sign != 1.0f) {
+      for (int i = lane; i < NV; i += TEAM) L[DST + i] *= sign;
+      TSYNC();
+    }
+  }
+
+  // ---------------- collision ----------------
+  // plane vs hull for both feet at once: lanes 0-7 take the first floor pair, 8-15 the second
+  static DNI void collide_planes(LP L, int lane) {
+    constexpr int NH = Md::NHV;
+    const int h = lane >> 3, sub = lane & 7;
+    const int p = Md::PLANE_PAIR[0] * (1 - h) + Md::PLANE_PAIR[1] * h;
+    const int gs = cgeom_slot<Md>(Md::pair_geom2[p]);
+    float pp[3], PR[9], cp[3], CR[9];
+    S1 Ls{L};
+    P1::geom_frame(Ls, 0, pp, PR);
+    P1::geom_frame(Ls, gs, cp, CR);
+    const float n[3] = {PR[2], PR[5], PR[8]};
+    const float dif[3] = {pp[0] - cp[0], pp[1] - cp[1], pp[2] - cp[2]};
+    float pl[3], nl[3];
+    mulmtv3(pl, CR, dif);
+    mulmtv3(nl, CR, n);
+    const float(*HV)[3] = Md::hull_vert_d();
+    // this lane's vertices: k = sub + 8r
+    constexpr int R = (NH + 7) / 8;
+    float sup[R], vx[R], vy[R], vz[R];
+    float smax = -1e30f;
+    for (int r = 0; r < R; r++) {
+      const int k = sub + 8 * r;
+      const bool ok = k < NH;
+      vx[r] = ok ? HV[k][0] : 0.0f; vy[r] = ok ? HV[k][1] : 0.0f; vz[r] = ok ? HV[k][2] : 0.0f;
+      sup[r] = ok ? (pl[0] - vx[r]) * nl[0] + (pl[1] - vy[r]) * nl[1] + (pl[2] - vz[r]) * nl[2] : -1e30f;
+      smax = fmaxf(smax, sup[r]);
+    }
+    smax = hmax8(smax);
+    const float thr = fmaxf(smax - 1e-3f, 0.0f);
+    float dm[R];
+    for (int r = 0; r < R; r++) dm[r] = (sub + 8 * r < NH) ? (sup[r] > thr ? 0.0f : -1e6f) : -1e30f;
+    // manifold_points (mjx collision_convex._manifold_points), argmax = first index within tol
+    auto argmax = [&](const float* v, float tol) -> int {
+      float mx = -1e30f;
+      for (int r = 0; r < R; r++) mx = fmaxf(mx, v[r]);
+      mx = hmax8(mx);
+      int best = 1 << 20;
+      for (int r = 0; r < R; r++) {
+        const int k = sub + 8 * r;
+        if (k < NH && v[r] >= mx - tol) best = min(best, k);
+      }
+      best = hmin8i(best);
+      return best < NH ? best : NH - 1;  // argmax_tol's default (also for NaN data)
+    };
+    auto vert = [&](int k, float* o) { o[0] = HV[k][0]; o[1] = HV[k][1]; o[2] = HV[k][2]; };
+    float s[R];
+    const int a = argmax(dm, 0.0f);
+    float pa[3];
+    vert(a, pa);
+    for (int r = 0; r < R; r++) {
+      const float dx = pa[0] - vx[r], dy = pa[1] - vy[r], dz = pa[2] - vz[r];
+      s[r] = dx * dx + dy * dy + dz * dz + dm[r];
+    }
+    const int b = argmax(s, MANIFOLD_TOL);
+    float pb[3];
+    vert(b, pb);
+    float amb[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]}, ab[3];
+    cross3(ab, nl, amb);
+    for (int r = 0; r < R; r++) {
+      const float ap[3] = {pa[0] - vx[r], pa[1] - vy[r], pa[2] - vz[r]};
+      s[r] = fabsf(dot3(ap, ab)) + dm[r];
+    }
+    const int c = argmax(s, MANIFOLD_TOL);
+    float pc[3];
+    vert(c, pc);
+    float amc[3] = {pa[0] - pc[0], pa[1] - pc[1], pa[2] - pc[2]};
+    float bmc[3] = {pb[0] - pc[0], pb[1] - pc[1], pb[2] - pc[2]};
+    float ac[3], bc[3];
+    cross3(ac, nl, amc);
+    cross3(bc, nl, bmc);
+    // argmax over the 2N array [|bp.bc| + dm ; |ap.ac| + dm]
+    int d;
+    {
+      float s1[R], s2[R];
+      float mx = -1e30f;
+      for (int r = 0; r < R; r++) {
+        const float bp[3] = {pb[0] - vx[r], pb[1] - vy[r], pb[2] - vz[r]};
+        const float ap[3] = {pa[0] - vx[r], pa[1] - vy[r], pa[2] - vz[r]};
+        s1[r] = fabsf(dot3(bp, bc)) + dm[r];
+        s2[r] = fabsf(dot3(ap, ac)) + dm[r];
+        mx = fmaxf(mx, fmaxf(s1[r], s2[r]));
+      }
+      mx = hmax8(mx);
+      int best = 1 << 20;
+      for (int r = 0; r < R; r++) {
+        const int k = sub + 8 * r;
+        if (k < NH && s1[r] >= mx - MANIFOLD_TOL) best = min(best, k);
+        if (k < NH && s2[r] >= mx - MANIFOLD_TOL) best = min(best, NH + k);
+      }
+      d = hmin8i(best);
+      d = d < 2 * NH ? d : 2 * NH - 1;
+      d = d >= NH ? d - NH : d;
+    }
+    float fr[9];
+    make_frame(fr, n);
+    if (sub < 4) {
+      const int idx[4] = {a, b, c, d};
+      const int me = idx[sub];
+      bool unique = true;
+      for (int e = 0; e < 4; e++) unique = unique && !(e < sub && idx[e] == me);
+      float v[3], vw[3], pos[3];
+      vert(me, v);
+      const float sp = (pl[0] - v[0]) * nl[0] + (pl[1] - v[1]) * nl[1] + (pl[2] - v[2]) * nl[2];
+      const float dist = unique ? -sp : 1.0f;
+      mulmv3(vw, CR, v);
+      for (int q = 0; q < 3; q++) pos[q] = cp[q] + vw[q] - 0.5f * dist * n[q];
+      P1::store_contact(Ls, 4 * p + sub, dist, pos, fr);
+    }
+  }
+
+  static DNI void collision(LP L, int lane) {
+    collide_planes(L, lane);
+    if (Md::FOOT_PAIR >= 0) {
+      constexpr int p = Md::FOOT_PAIR;
+      const int s1 = cgeom_slot<Md>(Md::pair_geom1[p]), s2 = cgeom_slot<Md>(Md::pair_geom2[p]);
+      S1 Ls{L};
+      // bounding-sphere reject (the common case) is uniform over the team
+      float p1[3], R1[9], p2[3], R2[9], t[3];
+      P1::geom_frame(Ls, s1, p1, R1);
+      P1::geom_frame(Ls, s2, p2, R2);
+      float c1[3], c2[3];
+      const float hc[3] = {Md::hull_center[0], Md::hull_center[1], Md::hull_center[2]};
+      mulmv3(t, R1, hc);
+      for (int a = 0; a < 3; a++) c1[a] = p1[a] + t[a];
+      mulmv3(t, R2, hc);
+      for (int a = 0; a < 3; a++) c2[a] = p2[a] + t[a];
+      const float cc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+      if (dot3(cc, cc) > 4.0f * Md::hull_radius * Md::hull_radius) {
+        if (lane < 4) {
+          const float nofr[9] = {0, 0, 1, 0, 1, 0, -1, 0, 0};
+          const float zero[3] = {L[Ly::COM], L[Ly::COM + 1], L[Ly::COM + 2]};
+          P1::store_contact(Ls, 4 * p + lane, 1.0f, zero, nofr);
+        }
+      } else {
+        TSYNC();
+        P1::collide_hulls(Ls, s1, s2, 4 * p);  // rare: every lane runs the single-lane path
+      }
+    }
+    TSYNC();
+  }
+
+  // ---------------- constraint rows ----------------
+  static DNI void make_rows(LP L, int lane) {
+    const float dt = Md::timestep;
+    S1 Ls{L};
+    if (lane < NFRIC) {
+      const int r = lane, i = Md::fric_dof[r];
+      float k, b, imp;
+      kbi(Md::dof_solref[i], Md::dof_solimp[i], 0.0f, dt, k, b, imp);
+      const float R = fmaxf(Md::dof_invweight0[i] * (1.0f - imp) / imp, 1e-15f);
+      L[Ly::RD + r] = 1.0f / R;
+      L[Ly::AREF + r] = -b * L[Ly::QVEL + i];
+    }
+    for (int r = lane; r < NLIM; r += TEAM) {
+      const int j = Md::lim_jnt[r], i = Md::jnt_dofadr[j];
+      const float q = L[Ly::QPOS + Md::jnt_qposadr[j]];
+      const float dlo = q - Md::jnt_range[j][0], dhi = Md::jnt_range[j][1] - q;
+      const float pos = fminf(dlo, dhi) - Md::jnt_margin[j];
+      const float sgn = dlo < dhi ? 1.0f : -1.0f;
+      float k, b, imp;
+      kbi(Md::jnt_solref[j], Md::jnt_solimp[j], pos, dt, k, b, imp);
+      const float R = fmaxf(Md::dof_invweight0[i] * (1.0f - imp) / imp, 1e-15f);
+      const bool active = pos < 0.0f;
+      L[Ly::RD + R_LIM + r] = active ? 1.0f / R : 0.0f;
+      L[Ly::AREF + R_LIM + r] = active ? (-b * sgn * L[Ly::QVEL + i] - k * imp * pos) : 0.0f;
+      L[Ly::LSGN + r] = sgn;
+    }
+    if (lane < NCON) {
+      const int slot = lane, p = slot >> 2;
+      float SL[6], SR[6];
+      for (int k = 0; k < 6; k++) { SL[k] = L[Ly::CVEL + 6 * Md::LFOOT_BODY + k]; SR[k] = L[Ly::CVEL + 6 * Md::RFOOT_BODY + k]; }
+      const int s1 = cgeom_slot<Md>(Md::pair_geom1[p]), s2 = cgeom_slot<Md>(Md::pair_geom2[p]);
+      const int b1 = Md::cgeom_body[s1], b2 = Md::cgeom_body[s2];
+      const float tran = Md::body_invweight0[b1][0] + Md::body_invweight0[b2][0];
+      const float mu = Md::pair_friction[p][0];
+      const float iw = (tran + mu * mu * tran) * 2.0f * mu * mu / Md::impratio;
+      const float pos = L[Ly::CDIST + slot] - Md::pair_margin[p];
+      const bool active = pos < 0.0f;
+      float k, b, imp;
+      kbi(Md::pair_solref[p], Md::pair_solimp[p], pos, dt, k, b, imp);
+      const float R = fmaxf(iw * (1.0f - imp) / imp, 1e-15f);
+      float vel[4];
+      contact_jx(L, p, slot, SL, SR, vel);
+      for (int e = 0; e < 4; e++) {
+        const int row = R_CON + 4 * slot + e;
+        L[Ly::RD + row] = active ? 1.0f / R : 0.0f;
+        L[Ly::AREF + row] = active ? (-b * vel[e] - k * imp * pos) : 0.0f;
+      }
+    }
+    TSYNC();
+  }
+
+  // J.x of one contact slot (4 pyramid edges) for body spatial motions SL/SR (runtime pair)
+  static DK void contact_jx(LP L, int p, int slot, const float* SL, const float* SR, float* out4) {
+    const int s1 = cgeom_slot<Md>(Md::pair_geom1[p]), s2 = cgeom_slot<Md>(Md::pair_geom2[p]);
+    const float mu = Md::pair_friction[p][0];
+    const float r[3] = {L[Ly::CR + 3 * slot], L[Ly::CR + 3 * slot + 1], L[Ly::CR + 3 * slot + 2]};
+    float v[3] = {0.0f, 0.0f, 0.0f}, t[3];
+    if (s2 != 0) { P1::contact_vel(s2 == 1 ? SL : SR, r, t); v[0] += t[0]; v[1] += t[1]; v[2] += t[2]; }
+    if (s1 != 0) { P1::contact_vel(s1 == 1 ? SL : SR, r, t); v[0] -= t[0]; v[1] -= t[1]; v[2] -= t[2]; }
+    float jr[3];
+    for (int q = 0; q < 3; q++)
+      jr[q] = L[Ly::CFR + 9 * slot + 3 * q] * v[0] + L[Ly::CFR + 9 * slot + 3 * q + 1] * v[1] +
+              L[Ly::CFR + 9 * slot + 3 * q + 2] * v[2];
+    out4[0] = jr[0] + mu * jr[1];
+    out4[1] = jr[0] - mu * jr[1];
+    out4[2] = jr[0] + mu * jr[2];
+    out4[3] = jr[0] - mu * jr[2];
+  }
+
+  // ---------------- Newton solver pieces ----------------
+  // J.x for all rows -> DST (x at X); sub_aref: DST = J.x - aref
+  static DNI void jmul(LP L, int lane, int X, int DST, bool sub_aref) {
+    // foot spatial motions: lanes 0-5 left, 6-11 right
+    if (lane < 12) {
+      const int b = lane < 6 ? Md::LFOOT_BODY : Md::RFOOT_BODY, k = lane < 6 ? lane : lane - 6;
+      const int(*CHN)[Md::MAXCHAIN] = Md::chain_d();
+      float s = 0.0f;
+      for (int c = 0; c < Md::MAXCHAIN; c++) {
+        const int i = CHN[b][c];
+        if (i >= 0) s += L[Ly::CDOF + 6 * i + k] * L[X + i];
+      }
+      L[TL::TSP + lane] = s;
+    }
+    if (lane < NFRIC) {
+      const int r = lane;
+      L[DST + r] = L[X + Md::fric_dof[r]] - (sub_aref ? L[Ly::AREF + r] : 0.0f);
+    }
+    for (int r = lane; r < NLIM; r += TEAM)
+      L[DST + R_LIM + r] = L[Ly::LSGN + r] * L[X + Md::jnt_dofadr[Md::lim_jnt[r]]] -
+                           (sub_aref ? L[Ly::AREF + R_LIM + r] : 0.0f);
+    TSYNC();
+    if (lane < NCON) {
+      float SL[6], SR[6], v[4];
+      for (int k = 0; k < 6; k++) { SL[k] = L[TL::TSP + k]; SR[k] = L[TL::TSP + 6 + k]; }
+      contact_jx(L, lane >> 2, lane, SL, SR, v);
+      for (int e = 0; e < 4; e++) {
+        const int row = R_CON + 4 * lane + e;
+        L[DST + row] = v[e] - (sub_aref ? L[Ly::AREF + row] : 0.0f);
+      }
+    }
+    TSYNC();
+  }
+
+  // Y = M X (sparse symmetric)
+  static DNI void mul_M(LP L, int lane, int X, int Y) {
+    const int(*MA)[NV] = Md::t_madr();
+    for (int i = lane; i < NV; i += TEAM) {
+      float acc = 0.0f;
+      for (int j = 0; j < NV; j++) {
+        const int a = MA[i][j];
+        if (a >= 0) acc += L[Ly::M + a] * L[X + j];
+      }
+      L[Y + i] = acc;
+    }
+    TSYNC();
+  }
+
+  static DK float gauss(LP L, int lane, int X, int MX) {
+    float g = 0.0f;
+    for (int i = lane; i < NV; i += TEAM) g += 0.5f * (L[MX + i] - L[Ly::FSM + i]) * (L[X + i] - L[Ly::QSM + i]);
+    return tsum(g);
+  }
+
+  // constraint cost of all rows for Jaref at JA
+  static DNI float cost_rows(LP L, int lane) {
+    float cost = 0.0f;
+    if (lane < NFRIC) {
+      const int r = lane;
+      const float D = L[Ly::RD + r], x = L[Ly::JA + r], f = L[Ly::DFRIC + Md::fric_dof[r]];
+      const float rf = f / D;
+      cost += x <= -rf ? (-f * x - 0.5f * rf * f) : (x >= rf ? (f * x - 0.5f * rf * f) : 0.5f * D * x * x);
+    }
+    for (int r = R_LIM + lane; r < NROW; r += TEAM) {
+      const float D = L[Ly::RD + r], x = L[Ly::JA + r];
+      cost += x < 0.0f ? 0.5f * D * x * x : 0.0f;
+    }
+    return tsum(cost);
+  }
+
+  // gradient and H = M + J' D J at JA; SRCH = -H^-1 grad. Returns false when the
+  // foot/foot rows are active (the caller takes the single-lane dense path).
+  static DNI bool newton_direction(LP L, int lane) {
+    for (int i = lane; i < NV; i += TEAM) L[Ly::GRAD + i] = L[Ly::MA + i] - L[Ly::FSM + i];
+    for (int k = lane; k < Md::NM; k += TEAM) L[Ly::H + k] = L[Ly::M + k];
+    TSYNC();
+    if (lane < NFRIC) {
+      const int r = lane, i = Md::fric_dof[r];
+      const float D = L[Ly::RD + r], x = L[Ly::JA + r], f = L[Ly::DFRIC + i], rf = f / D;
+      const float force = x <= -rf ? f : (x >= rf ? -f : -D * x);
+      L[Ly::GRAD + i] -= force;
+      if (x > -rf && x < rf) L[Ly::H + diag_adr(i)] += D;
+    }
+    TSYNC();
+    for (int r = lane; r < NLIM; r += TEAM) {
+      const int i = Md::jnt_dofadr[Md::lim_jnt[r]];
+      const float D = L[Ly::RD + R_LIM + r], x = L[Ly::JA + R_LIM + r];
+      if (x < 0.0f) {
+        L[Ly::GRAD + i] -= L[Ly::LSGN + r] * (-D * x);
+        L[Ly::H + diag_adr(i)] += D;
+      }
+    }
+    TSYNC();
+    // contact rows: lane = slot-in-pair * 4 + edge; pair p rows R_CON + 16p + lane
+    bool ff = false;
+    if (Md::FOOT_PAIR >= 0) {
+      const int row = R_CON + 16 * Md::FOOT_PAIR + lane;
+      const float act = (L[Ly::JA + row] < 0.0f && L[Ly::RD + row] != 0.0f) ? 1.0f : 0.0f;
+      ff = tsum(act) > 0.0f;
+    }
+    if (ff) return false;
+    for (int side = 0; side < 2; side++) {
+      const int p = Md::PLANE_PAIR[side];
+      const int foot = cgeom_slot<Md>(Md::pair_geom2[p]);  // 1 left, 2 right
+      const int b = foot == 1 ? Md::LFOOT_BODY : Md::RFOOT_BODY;
+      const float mu = Md::pair_friction[p][0];
+      const int slot = 4 * p + (lane >> 2), e = lane & 3, row = R_CON + 4 * slot + e;
+      const float D = L[Ly::RD + row], x = L[Ly::JA + row];
+      const float w = (x < 0.0f && D != 0.0f) ? D : 0.0f;
+      const float force = -w * x;
+      const int t = 1 + (e >> 1);
+      const float sg = (e & 1) ? -mu : mu;
+      float u[3], r[3], a[6];
+      for (int q = 0; q < 3; q++) {
+        u[q] = L[Ly::CFR + 9 * slot + q] + sg * L[Ly::CFR + 9 * slot + 3 * t + q];
+        r[q] = L[Ly::CR + 3 * slot + q];
+      }
+      cross3(a, r, u);
+      a[3] = u[0]; a[4] = u[1]; a[5] = u[2];
+      float K[21], F[6];
+      {
+        int o = 0;
+        for (int q = 0; q < 6; q++)
+          for (int kk = q; kk < 6; kk++) { K[o] = tsum(w * a[q] * a[kk]); o++; }
+        for (int q = 0; q < 6; q++) F[q] = tsum(force * a[q]);
+      }
+      // K.cdof_j and the gradient for the chain dofs (lane = chain position)
+      const int(*CHN)[Md::MAXCHAIN] = Md::chain_d();
+      const int jl = lane < Md::MAXCHAIN ? CHN[b][lane] : -1;
+      if (jl >= 0) {
+        float cdj[6];
+        for (int k = 0; k < 6; k++) cdj[k] = L[Ly::CDOF + 6 * jl + k];
+        float g = 0.0f;
+        for (int q = 0; q < 6; q++) {
+          float s = 0.0f;
+          for (int k = 0; k < 6; k++) s += K[kidx(q, k)] * cdj[k];
+          L[TL::KC + 6 * lane + q] = s;
+          g += cdj[q] * F[q];
+        }
+        L[Ly::GRAD + jl] -= g;
+      }
+      TSYNC();
+      // H[i][j] += cdof_i . (K cdof_j) for chain pairs; lane = row position ci
+      if (jl >= 0) {
+        float cdi[6];
+        for (int k = 0; k < 6; k++) cdi[k] = L[Ly::CDOF + 6 * jl + k];
+        for (int cj = 0; cj <= lane; cj++) {
+          const int j = CHN[b][cj];
+          float s = 0.0f;
+          for (int k = 0; k < 6; k++) s += cdi[k] * L[TL::KC + 6 * cj + k];
+          L[Ly::H + Md::t_madr()[jl][j]] += s;
+        }
+      }
+      TSYNC();
+    }
+    return true;
+  }
+
+  static DK constexpr int kidx(int q, int k) {
+    // packed upper-triangular index of (min(q,k), max(q,k)) in a 6x6 symmetric block
+    return q <= k ? (q * 6 - (q * (q - 1)) / 2 + (k - q)) : (k * 6 - (k * (k - 1)) / 2 + (q - k));
+  }
+
+  struct Pt { float alpha, cost, d0, d1; };
+
+  // line-search rows held in registers: one friction row and up to RQ one-sided rows per lane
+  static constexpr int RQ = (NROW - R_LIM + TEAM - 1) / TEAM;
+  struct Rows {
+    float fD, fja, fv, ff;
+    float D[RQ], ja[RQ], v[RQ];
+  };
+
+  static DK void load_rows(LP L, int lane, Rows& R) {
+    const bool fr = lane < NFRIC;
+    R.fD = fr ? L[Ly::RD + lane] : 0.0f;
+    R.fja = fr ? L[Ly::JA + lane] : 0.0f;
+    R.fv = fr ? L[Ly::JV + lane] : 0.0f;
+    R.ff = fr ? L[Ly::DFRIC + Md::fric_dof[lane]] : 0.0f;
+    for (int m = 0; m < RQ; m++) {
+      const int r = R_LIM + lane + TEAM * m;
+      const bool ok = r < NROW;
+      R.D[m] = ok ? L[Ly::RD + r] : 0.0f;
+      R.ja[m] = ok ? L[Ly::JA + r] : 0.0f;
+      R.v[m] = ok ? L[Ly::JV + r] : 0.0f;
+    }
+  }
+
+  // partial quadratic coefficients of this lane's rows at alpha
+  static DK void row_quad(const Rows& R, int lane, float alpha, float& q0, float& q1, float& q2) {
+    if (lane < NFRIC) {
+      const float D = R.fD, ja = R.fja, v = R.fv, f = R.ff;
+      const float rf = f / D, x = ja + alpha * v;
+      if (x <= -rf) { q0 += -0.5f * rf * f - f * ja; q1 += -f * v; }
+      else if (x >= rf) { q0 += -0.5f * rf * f + f * ja; q1 += f * v; }
+      else { q0 += 0.5f * D * ja * ja; q1 += D * v * ja; q2 += 0.5f * D * v * v; }
+    }
+    for (int m = 0; m < RQ; m++) {
+      const float D = R.D[m], ja = R.ja[m], v = R.v[m];
+      const float x = ja + alpha * v;
+      if (x < 0.0f) { q0 += 0.5f * D * ja * ja; q1 += D * v * ja; q2 += 0.5f * D * v * v; }
+    }
+  }
+
+  static DK Pt eval1(const Rows& R, int lane, float g0, float g1, float g2, float alpha) {
+    float q0 = 0.0f, q1 = 0.0f, q2 = 0.0f;
+    row_quad(R, lane, alpha, q0, q1, q2);
+    q0 = tsum(q0) + g0; q1 = tsum(q1) + g1; q2 = tsum(q2) + g2;
+    Pt p;
+    p.alpha = alpha;
+    p.cost = alpha * alpha * q2 + alpha * q1 + q0;
+    p.d0 = 2.0f * alpha * q2 + q1;
+    p.d1 = 2.0f * q2;
+    return p;
+  }
+
+  // mjx solver.solve, iterations = 1
+  static DNI void solve(LP L, int lane, float* scratch, int stride) {
+    mul_M(L, lane, Ly::WARM, Ly::MA);
+    const float gw = gauss(L, lane, Ly::WARM, Ly::MA);
+    jmul(L, lane, Ly::WARM, Ly::JA, true);
+    const float cw = gw + cost_rows(L, lane);
+    jmul(L, lane, Ly::QSM, Ly::JA, true);
+    const float cs = cost_rows(L, lane);
+    if (cw < cs) {
+      for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] = L[Ly::WARM + i];
+      TSYNC();
+      jmul(L, lane, Ly::QACC, Ly::JA, true);
+    } else {
+      for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] = L[Ly::QSM + i];
+      TSYNC();
+      mul_M(L, lane, Ly::QACC, Ly::MA);
+    }
+    const float g0 = gauss(L, lane, Ly::QACC, Ly::MA);
+    const bool sparse_ok = newton_direction(L, lane);
+    if (sparse_ok) {
+      factor_H(L, lane);
+      solve_H(L, lane, Ly::GRAD, Ly::SRCH, -1.0f);
+    } else {
+      TSYNC();
+      S1 Ls{L};
+      P1::newton_direction(Ls);  // all lanes, identical values
+      P1::dense_direction(Ls, scratch, stride);
+      TSYNC();
+    }
+    jmul(L, lane, Ly::SRCH, Ly::JV, false);
+    mul_M(L, lane, Ly::SRCH, Ly::GRAD);
+    float sn = 0.0f, sMa = 0.0f, sf = 0.0f, sMv = 0.0f;
+    for (int i = lane; i < NV; i += TEAM) {
+      const float s = L[Ly::SRCH + i];
+      sn += s * s;
+      sMa += s * L[Ly::MA + i];
+      sf += s * L[Ly::FSM + i];
+      sMv += s * L[Ly::GRAD + i];
+    }
+    sn = tsum(sn); sMa = tsum(sMa); sf = tsum(sf); sMv = tsum(sMv);
+    const float gtol = Md::tolerance * Md::ls_tolerance * sqrtf(sn) * Md::meaninertia * (float)(NV > 1 ? NV : 1);
+    const float G0 = g0, G1 = sMa - sf, G2 = 0.5f * sMv;
+    Rows R;
+    load_rows(L, lane, R);
+    const Pt p0 = eval1(R, lane, G0, G1, G2, 0.0f);
+    Pt lo = eval1(R, lane, G0, G1, G2, p0.alpha - p0.d0 / p0.d1);
+    Pt hi;
+    if (lo.d0 < p0.d0) { hi = p0; } else { hi = lo; lo = p0; }
+    bool swap = true;
+    for (int it = 0; it < Md::ls_iterations; it++) {
+      bool done = !swap;
+      done = done || ((lo.d0 < 0.0f) && (lo.d0 > -gtol));
+      done = done || ((hi.d0 > 0.0f) && (hi.d0 < gtol));
+      if (done) break;
+      // the three candidate points share one pass over the rows
+      const float al = lo.alpha - lo.d0 / lo.d1, ah = hi.alpha - hi.d0 / hi.d1, am = 0.5f * (lo.alpha + hi.alpha);
+      float a0 = 0, a1 = 0, a2 = 0, b0 = 0, b1 = 0, b2 = 0, c0 = 0, c1 = 0, c2 = 0;
+      row_quad(R, lane, al, a0, a1, a2);
+      row_quad(R, lane, ah, b0, b1, b2);
+      row_quad(R, lane, am, c0, c1, c2);
+      auto mk = [&](float alpha, float q0, float q1, float q2) {
+        q0 = tsum(q0) + G0; q1 = tsum(q1) + G1; q2 = tsum(q2) + G2;
+        Pt p;
+        p.alpha = alpha;
+        p.cost = alpha * alpha * q2 + alpha * q1 + q0;
+        p.d0 = 2.0f * alpha * q2 + q1;
+        p.d1 = 2.0f * q2;
+        return p;
+      };
+      const Pt lo_next = mk(al, a0, a1, a2), hi_next = mk(ah, b0, b1, b2), mid = mk(am, c0, c1, c2);
+      const bool s1 = (lo.d0 > 0.0f) || (lo.d0 < lo_next.d0);
+      if (s1) lo = lo_next;
+      const bool s2 = (mid.d0 < 0.0f) && (lo.d0 < mid.d0);
+      if (s2) lo = mid;
+      const bool s3 = (hi.d0 < 0.0f) || (hi.d0 > hi_next.d0);
+      if (s3) hi = hi_next;
+      const bool s4 = (mid.d0 > 0.0f) && (hi.d0 > mid.d0);
+      if (s4) hi = mid;
+      swap = s1 || s2 || s3 || s4;
+    }
+    const bool improved = (lo.cost < p0.cost) || (hi.cost < p0.cost);
+    const float alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+    if (improved)
+      for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] += L[Ly::SRCH + i] * alpha;
+    TSYNC();
+  }
+
+  // ---------------- sensors (last substep) ----------------
+  static DNI void sensors(LP L, int lane) {
+    const float com[3] = {L[Ly::COM], L[Ly::COM + 1], L[Ly::COM + 2]};
+    float cacc1[6];
+    for (int k = 0; k < 6; k++) cacc1[k] = (k >= 3) ? -Md::gravity[k - 3] : 0.0f;
+    for (int i = 0; i < 6; i++) {
+      const float v = L[Ly::QVEL + i], a = L[Ly::QACC + i];
+      for (int k = 0; k < 6; k++) {
+        const float cdd = i >= 3 ? L[Ly::CDD1 + 6 * (i - 3) + k] : 0.0f;
+        cacc1[k] += cdd * v + L[Ly::CDOF + 6 * i + k] * a;
+      }
+    }
+    for (int s = lane; s < Md::NSENSOR; s += TEAM) {
+      const int typ = Md::sensor_type[s], site = Md::sensor_objid[s], adr = Md::sensor_adr[s];
+      const int b = Md::site_bodyid[site];
+      float R[9], sp[3], sR[9], t[3], SM[9];
+      const float spos[3] = {Md::site_pos[site][0], Md::site_pos[site][1], Md::site_pos[site][2]};
+      for (int k = 0; k < 9; k++) { R[k] = L[Ly::XMAT + 9 * b + k]; SM[k] = Md::site_mat[site][k]; }
+      mulmv3(t, R, spos);
+      for (int k = 0; k < 3; k++) sp[k] = L[Ly::XPOS + 3 * b + k] + t[k];
+      mulmm3(sR, R, SM);
+      const float off[3] = {sp[0] - com[0], sp[1] - com[1], sp[2] - com[2]};
+      float ang[3] = {L[Ly::CVEL + 6 * b], L[Ly::CVEL + 6 * b + 1], L[Ly::CVEL + 6 * b + 2]}, lin[3];
+      cross3(t, ang, off);
+      for (int k = 0; k < 3; k++) lin[k] = L[Ly::CVEL + 6 * b + 3 + k] + t[k];
+      float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (typ == 0) mulmtv3(o, sR, ang);
+      else if (typ == 1) mulmtv3(o, sR, lin);
+      else if (typ == 2) {
+        float acc[3];
+        cross3(t, cacc1, off);
+        for (int k = 0; k < 3; k++) acc[k] = cacc1[3 + k] + t[k];
+        cross3(t, ang, lin);
+        for (int k = 0; k < 3; k++) acc[k] += t[k];
+        mulmtv3(o, sR, acc);
+      } else if (typ == 3) { o[0] = sR[2]; o[1] = sR[5]; o[2] = sR[8]; }
+      else if (typ == 4) { o[0] = sR[0]; o[1] = sR[3]; o[2] = sR[6]; }
+      else if (typ == 5) { o[0] = lin[0]; o[1] = lin[1]; o[2] = lin[2]; }
+      else if (typ == 6) { o[0] = ang[0]; o[1] = ang[1]; o[2] = ang[2]; }
+      else if (typ == 7) { o[0] = sp[0]; o[1] = sp[1]; o[2] = sp[2]; }
+      else if (typ == 8) {
+        const float bq[4] = {L[Ly::XQ + 4 * b], L[Ly::XQ + 4 * b + 1], L[Ly::XQ + 4 * b + 2], L[Ly::XQ + 4 * b + 3]};
+        const float sq[4] = {Md::site_quat[site][0], Md::site_quat[site][1], Md::site_quat[site][2], Md::site_quat[site][3]};
+        qmul(o, bq, sq);
+        qnormalize(o);
+      }
+      const int dim = typ == 8 ? 4 : 3;
+      for (int k = 0; k < dim; k++) L[Ly::SENS + adr + k] = o[k];
+      if (typ == 0 && site == Md::IMU_SITE) { L[Ly::IMUR] = sR[6]; L[Ly::IMUR + 1] = sR[7]; L[Ly::IMUR + 2] = sR[8]; }
+      if (typ == 7 && site == Md::LFOOT_SITE) L[Ly::FOOTZ] = sp[2];
+      if (typ == 7 && site == Md::RFOOT_SITE) L[Ly::FOOTZ + 1] = sp[2];
+    }
+    if (lane < 2) {
+      const int p = Md::PLANE_PAIR[lane];
+      const int s2 = cgeom_slot<Md>(Md::pair_geom2[p]);
+      float mn = 1e4f;
+      for (int c = 0; c < 4; c++) mn = fminf(mn, L[Ly::CDIST + 4 * p + c]);
+      L[Ly::OCON + s2 - 1] = mn < 0.0f ? 1.0f : 0.0f;
+    }
+    TSYNC();
+  }
+
+  // ---------------- semi-implicit Euler ----------------
+  static DNI void euler(LP L, int lane) {
+    const float dt = Md::timestep;
+    for (int i = lane; i < NV; i += TEAM) {
+      L[Ly::WARM + i] = L[Ly::QACC + i];
+      L[Ly::QVEL + i] += dt * L[Ly::QACC + i];
+    }
+    TSYNC();
+    if (lane == 0) {
+      for (int k = 0; k < 3; k++) L[Ly::QPOS + k] += dt * L[Ly::QVEL + k];
+      const float v[3] = {L[Ly::QVEL + 3], L[Ly::QVEL + 4], L[Ly::QVEL + 5]};
+      const float nvv = sqrtf(dot3(v, v));
+      float ax[3] = {1.0f, 0.0f, 0.0f};
+      if (nvv > 1e-15f) { ax[0] = v[0] / nvv; ax[1] = v[1] / nvv; ax[2] = v[2] / nvv; }
+      float s, c;
+      sincosf(0.5f * dt * nvv, &s, &c);
+      const float qr[4] = {c, ax[0] * s, ax[1] * s, ax[2] * s};
+      float q[4] = {L[Ly::QPOS + 3], L[Ly::QPOS + 4], L[Ly::QPOS + 5], L[Ly::QPOS + 6]};
+      qmul(q, q, qr);
+      qnormalize(q);
+      for (int k = 0; k < 4; k++) L[Ly::QPOS + 3 + k] = q[k];
+    }
+    for (int j = 1 + lane; j < NJ; j += TEAM) L[Ly::QPOS + Md::jnt_qposadr[j]] += dt * L[Ly::QVEL + Md::jnt_dofadr[j]];
+    TSYNC();
+  }
+
+  static DK void step(LP L, int lane, bool integrate, bool want_out, float* aux, int aux_stride, float* scratch,
+                      int sstride) {
+    STAGE_T0();
+    kinematics(L, lane);
+    STAGE_MARK(0);
+    com_pos(L, lane);
+    STAGE_MARK(1);
+    rne(L, lane);
+    STAGE_MARK(2);
+    crb(L, lane);
+    STAGE_MARK(3);
+    smooth(L, lane);
+    factor_H(L, lane);
+    solve_H(L, lane, Ly::FSM, Ly::QSM, 1.0f);
+    STAGE_MARK(4);
+    collision(L, lane);
+    STAGE_MARK(5);
+    make_rows(L, lane);
+    STAGE_MARK(6);
+    solve(L, lane, scratch, sstride);
+    STAGE_MARK(7);
+    if (want_out) {
+      sensors(L, lane);
+      if (aux) {
+        S1 Ls{L};
+        if (lane == 0) P1::write_aux(Ls, aux, aux_stride);
+      }
+    }
+    if (integrate) {
+      euler(L, lane);
+    } else {
+      for (int i = lane; i < NV; i += TEAM) L[Ly::WARM + i] = L[Ly::QACC + i];
+      TSYNC();
+    }
+    STAGE_MARK(8);
+  }
+};

@@ -38,7 +38,7 @@ class DuckLayout(C.Structure):
 def build(verbose: bool = False) -> str:
     """Compile libduck.so for gfx950 with hipcc (in-tree, so it travels with the repo)."""
     srcs = [os.path.join(CSRC, "duck_kernels.hip")]
-    deps = srcs + [os.path.join(CSRC, f) for f in ("duck_physics.h", "duck_math.h")] + \
+    deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
         [os.path.join(CSRC, "generated", f) for f in os.listdir(os.path.join(CSRC, "generated"))] + \
         [os.path.join(ROOT, "include", f) for f in ("duck.h", "duck_env.h", "duck_model.h")]
     if os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= max(os.path.getmtime(d) for d in deps):

@@ -53,9 +53,13 @@ def forward_errors(task, n=256, nsub=0, seed=1):
         rel = err / (1 + np.abs(b).max(axis=1))
         print(f"  {k:15s} max_abs {err.max():.3e}  p50_rel {np.median(rel):.3e}  p99_rel {np.quantile(rel, 0.99):.3e}"
               f"  frac_rel<1e-3 {np.mean(rel < 1e-3):.3f}  finite {np.isfinite(a).all()}")
+    a, b = g["qacc"].reshape(n, -1), r["qacc"].reshape(n, -1)
+    rel = np.abs(a - b).max(axis=1) / (1 + np.abs(b).max(axis=1))
+    ok = np.quantile(rel, 0.99) < 1e-3 and np.isfinite(a).all()
     worst = int(np.argmax(np.abs(g["qacc"] - r["qacc"]).max(axis=1)))
     print("  worst env", worst, "con_dist gpu", np.round(g["con_dist"][worst], 5), "ref", np.round(r["con_dist"][worst], 5))
     print("  qacc gpu", np.round(g["qacc"][worst][:8], 4), "ref", np.round(r["qacc"][worst][:8], 4))
+    return ok
 
 
 def timing(task="flat_terrain", n=4096, steps=20, imit=False):
@@ -76,10 +80,13 @@ def timing(task="flat_terrain", n=4096, steps=20, imit=False):
 
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
-    if which in ("all", "fwd"):
-        forward_errors("flat_terrain")
-        forward_errors("flat_terrain", nsub=1, seed=2)
-        forward_errors("flat_terrain_backlash")
+    if which in ("all", "fwd", "fwdcheck"):
+        ok = forward_errors("flat_terrain")
+        ok = forward_errors("flat_terrain", nsub=1, seed=2) and ok
+        ok = forward_errors("flat_terrain_backlash") and ok
+        if which == "fwdcheck" and not ok:
+            print("FORWARD PARITY FAILED")
+            sys.exit(1)
     if which in ("all", "time"):
         timing()
         timing(imit=True)
