@@ -151,20 +151,68 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
             anc_adr.append(adr[k, i])
         ldl_off.append(len(ldl))
         anc_off.append(len(anc_dof))
+    # the same LDL'/solve work packed per (pivot, round of 16 lanes) for register-resident
+    # per-lane index words: ldl word = aij | aki << 10 | akj << 20, anc word = dof | adr << 10
+    assert int(adr.max()) < 1024 and nv < 1024
+    ldl_nr, ldl_rb, ldlp = [], [], []
+    anc_nr, anc_rb, ancp = [], [], []
+    for k in range(nv):
+        ent = [int(a) | int(b) << 10 | int(c) << 20 for (a, b, c) in ldl[ldl_off[k]:ldl_off[k + 1]]]
+        nr = (len(ent) + 15) // 16
+        ldl_rb.append(len(ldlp))
+        ldl_nr.append(nr)
+        for r in range(nr):
+            row = ent[16 * r:16 * r + 16]
+            ldlp.append(row + [-1] * (16 - len(row)))
+        ent = [int(d) | int(a) << 10 for d, a in zip(anc_dof[anc_off[k]:anc_off[k + 1]], anc_adr[anc_off[k]:anc_off[k + 1]])]
+        nr = (len(ent) + 15) // 16
+        anc_rb.append(len(ancp))
+        anc_nr.append(nr)
+        for r in range(nr):
+            row = ent[16 * r:16 * r + 16]
+            ancp.append(row + [-1] * (16 - len(row)))
+    if not ldlp:
+        ldlp = [[-1] * 16]
+    if not ancp:
+        ancp = [[-1] * 16]
     pplane = [p for p in range(m.npair) if m.pair_geom1[p] == floor]
     pfoot = [p for p in range(m.npair) if m.pair_geom1[p] != floor]
     assert len(pplane) == 2 and len(pfoot) <= 1
+    # tree as a root path (bodies up to the first branching body) plus unbranched limbs
+    kids = lambda b: [c for c in range(1, nb) if m.body_parentid[c] == b and m.body_weldid[c] != 0]
+    root = [1]
+    while len(kids(root[-1])) == 1:
+        root.append(kids(root[-1])[0])
+    branches = []
+    for c in kids(root[-1]):
+        br = [c]
+        while kids(br[-1]):
+            assert len(kids(br[-1])) == 1, "limbs must be unbranched"
+            br.append(kids(br[-1])[0])
+        branches.append(br)
+    assert len(branches) <= 16
+    brlen = max(len(b) for b in branches)
+    br_arr = np.full((len(branches), brlen), -1)
+    for i, b in enumerate(branches):
+        br_arr[i, :len(b)] = b
     T = lambda name, a, t: f"__device__ const {t} {pre}_{name}{''.join(f'[{d}]' for d in np.shape(a))} = " + \
         _arr("x", np.asarray(a), t).split("= ", 1)[1]
     tabs = {"lev": (lev, "int"), "child": (child, "int"), "madr": (full, "int"), "mi": (mi, "int"), "mj": (mj, "int"),
             "ldl": (np.array(ldl).reshape(-1, 3), "int"), "ldl_off": (ldl_off, "int"), "anc_dof": (anc_dof, "int"),
-            "anc_adr": (anc_adr, "int"), "anc_off": (anc_off, "int")}
+            "anc_adr": (anc_adr, "int"), "anc_off": (anc_off, "int"),
+            "ldlp": (np.array(ldlp), "int"), "ancp": (np.array(ancp), "int"), "br": (br_arr, "int")}
     dev = [T(k, a, t) for k, (a, t) in tabs.items()]
     acc = [f"  static constexpr int T_NLEV = {nlev}, T_LEVW = {levw}, T_MAXCH = {maxch};\n",
            f"  static constexpr int T_MAXLDL = {max(ldl_off[k + 1] - ldl_off[k] for k in range(nv))}, "
            f"T_MAXANC = {max(anc_off[k + 1] - anc_off[k] for k in range(nv))};\n",
            f"  static constexpr int PLANE_PAIR[2] = {{{pplane[0]}, {pplane[1]}}};\n",
-           f"  static constexpr int FOOT_PAIR = {pfoot[0] if pfoot else -1};\n"]
+           f"  static constexpr int FOOT_PAIR = {pfoot[0] if pfoot else -1};\n",
+           f"  static constexpr int T_LDL_NRT = {len(ldlp)}, T_ANC_NRT = {len(ancp)};\n",
+           _arr("T_LDL_NR", ldl_nr, "int"), _arr("T_LDL_RB", ldl_rb, "int"),
+           _arr("T_ANC_NR", anc_nr, "int"), _arr("T_ANC_RB", anc_rb, "int"),
+           _arr("T_DIAG", [adr[i, i] for i in range(nv)], "int"),
+           f"  static constexpr int T_NROOT = {len(root)}, T_NBR = {len(branches)}, T_BRLEN = {brlen};\n",
+           _arr("T_ROOT", root, "int")]
     for k, (a, t) in tabs.items():
         shp = np.shape(a)
         if len(shp) == 1:

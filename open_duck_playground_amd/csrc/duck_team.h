@@ -79,49 +79,68 @@ struct TPhys {
   static_assert(NCON <= TEAM, "one contact slot per lane");
   static_assert(NU <= TEAM, "one actuator per lane");
 
-  // ---------------- mj_kinematics: one tree level at a time, a body per lane ----------------
-  static DNI void kinematics(LP L, int lane) {
-    const int(*LEV)[Md::T_LEVW] = Md::t_lev();
-    for (int lv = 0; lv < Md::T_NLEV; lv++) {
-      const int b = lane < Md::T_LEVW ? LEV[lv][lane] : -1;
-      if (b > 0) {
-        float p[3], q[4];
-        const int pa = Md::body_parentid[b];
-        if (b == 1) {
-          p[0] = L[Ly::QPOS + 0]; p[1] = L[Ly::QPOS + 1]; p[2] = L[Ly::QPOS + 2];
-          q[0] = L[Ly::QPOS + 3]; q[1] = L[Ly::QPOS + 4]; q[2] = L[Ly::QPOS + 5]; q[3] = L[Ly::QPOS + 6];
-        } else {
-          const float bq[4] = {Md::body_quat[b][0], Md::body_quat[b][1], Md::body_quat[b][2], Md::body_quat[b][3]};
-          const float bp[3] = {Md::body_pos[b][0], Md::body_pos[b][1], Md::body_pos[b][2]};
-          if (pa == 0) {
-            for (int k = 0; k < 3; k++) p[k] = bp[k];
-            for (int k = 0; k < 4; k++) q[k] = bq[k];
-          } else {
-            float R[9], pq[4], t[3];
-            for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * pa + k];
-            for (int k = 0; k < 4; k++) pq[k] = L[Ly::XQ + 4 * pa + k];
-            mulmv3(t, R, bp);
-            for (int k = 0; k < 3; k++) p[k] = L[Ly::XPOS + 3 * pa + k] + t[k];
-            qmul(q, pq, bq);
-          }
-          const int nj = Md::body_jntnum[b], j0 = Md::body_jntadr[b];
-          for (int jj = 0; jj < nj; jj++) {
-            const int j = j0 + jj, a = Md::jnt_qposadr[j];
-            float s, c;
-            sincosf(0.5f * (L[Ly::QPOS + a] - L[Ly::DQ0 + a]), &s, &c);
-            const float ql[4] = {c, Md::jnt_axis[j][0] * s, Md::jnt_axis[j][1] * s, Md::jnt_axis[j][2] * s};
-            qmul(q, q, ql);
-          }
-        }
-        qnormalize(q);
-        float R[9];
-        q2m(R, q);
-        for (int k = 0; k < 3; k++) L[Ly::XPOS + 3 * b + k] = p[k];
-        for (int k = 0; k < 4; k++) L[Ly::XQ + 4 * b + k] = q[k];
-        for (int k = 0; k < 9; k++) L[Ly::XMAT + 9 * b + k] = R[k];
+  // ---------------- mj_kinematics: root path on every lane, one limb per lane ----------------
+  // child pose from the parent pose held in registers
+  static DK void body_pose(LP L, int b, const float* pp, const float* pR, const float* pq, float* p, float* q,
+                           float* R) {
+    const float bq[4] = {Md::body_quat[b][0], Md::body_quat[b][1], Md::body_quat[b][2], Md::body_quat[b][3]};
+    const float bp[3] = {Md::body_pos[b][0], Md::body_pos[b][1], Md::body_pos[b][2]};
+    float t[3];
+    mulmv3(t, pR, bp);
+    for (int k = 0; k < 3; k++) p[k] = pp[k] + t[k];
+    qmul(q, pq, bq);
+    const int nj = Md::body_jntnum[b], j0 = Md::body_jntadr[b];
+#pragma unroll
+    for (int jj = 0; jj < 2; jj++) {
+      if (jj < nj) {
+        const int j = j0 + jj, a = Md::jnt_qposadr[j];
+        float sn, cs;
+        sincosf(0.5f * (L[Ly::QPOS + a] - L[Ly::DQ0 + a]), &sn, &cs);
+        const float ql[4] = {cs, Md::jnt_axis[j][0] * sn, Md::jnt_axis[j][1] * sn, Md::jnt_axis[j][2] * sn};
+        qmul(q, q, ql);
       }
-      TSYNC();
     }
+    qnormalize(q);
+    q2m(R, q);
+  }
+  static DK void store_pose(LP L, int b, const float* p, const float* q, const float* R) {
+    for (int k = 0; k < 3; k++) L[Ly::XPOS + 3 * b + k] = p[k];
+    for (int k = 0; k < 4; k++) L[Ly::XQ + 4 * b + k] = q[k];
+    for (int k = 0; k < 9; k++) L[Ly::XMAT + 9 * b + k] = R[k];
+  }
+
+  static DNI void kinematics(LP L, int lane) {
+    float p[3], q[4], R[9];
+    for (int k = 0; k < 3; k++) p[k] = L[Ly::QPOS + k];
+    for (int k = 0; k < 4; k++) q[k] = L[Ly::QPOS + 3 + k];
+    qnormalize(q);
+    q2m(R, q);
+    if (lane == 0) store_pose(L, 1, p, q, R);
+#pragma unroll
+    for (int r = 1; r < Md::T_NROOT; r++) {
+      float p2[3], q2[4], R2[9];
+      body_pose(L, Md::T_ROOT[r], p, R, q, p2, q2, R2);
+      for (int k = 0; k < 3; k++) p[k] = p2[k];
+      for (int k = 0; k < 4; k++) q[k] = q2[k];
+      for (int k = 0; k < 9; k++) R[k] = R2[k];
+      if (lane == 0) store_pose(L, Md::T_ROOT[r], p, q, R);
+    }
+    if (lane < Md::T_NBR) {
+      int bb[Md::T_BRLEN];
+#pragma unroll
+      for (int d = 0; d < Md::T_BRLEN; d++) bb[d] = Md::t_br()[lane][d];
+#pragma unroll
+      for (int d = 0; d < Md::T_BRLEN; d++) {
+        if (bb[d] < 0) break;
+        float p2[3], q2[4], R2[9];
+        body_pose(L, bb[d], p, R, q, p2, q2, R2);
+        for (int k = 0; k < 3; k++) p[k] = p2[k];
+        for (int k = 0; k < 4; k++) q[k] = q2[k];
+        for (int k = 0; k < 9; k++) R[k] = R2[k];
+        store_pose(L, bb[d], p, q, R);
+      }
+    }
+    TSYNC();
   }
 
   // ---------------- mj_comPos: subtree com (team reduction), cinert, cdof ----------------
@@ -196,70 +215,97 @@ struct TPhys {
     TSYNC();
   }
 
-  // ---------------- mj_comVel + mj_rne (flg_acc = 0) ----------------
+  // ---------------- mj_comVel + mj_rne (flg_acc = 0): root path on every lane, a limb per lane ----
+  // cvel/cacc of body b from its parent's (registers); returns cfrc_b (before subtree sums)
+  static DK void body_motion(LP L, int b, float* cv, float* ca, float* f) {
+    const int da = Md::body_dofadr[b], nd = Md::body_dofnum[b];
+    if (b == 1) {
+      for (int i = 0; i < 3; i++) {
+        const float v = L[Ly::QVEL + i];
+        for (int k = 0; k < 6; k++) cv[k] += L[Ly::CDOF + 6 * i + k] * v;
+      }
+      float cvt[6];
+      for (int k = 0; k < 6; k++) cvt[k] = cv[k];
+      for (int i = 3; i < 6; i++) {
+        float cd[6], cdd[6];
+        for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
+        cross_motion(cdd, cvt, cd);
+        const float v = L[Ly::QVEL + i];
+        for (int k = 0; k < 6; k++) { ca[k] += cdd[k] * v; cv[k] += cd[k] * v; }
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 2; jj++) {
+        if (jj < nd) {
+          const int i = da + jj;
+          float cd[6], cdd[6];
+          for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
+          cross_motion(cdd, cv, cd);
+          const float v = L[Ly::QVEL + i];
+          for (int k = 0; k < 6; k++) { ca[k] += cdd[k] * v; cv[k] += cd[k] * v; }
+        }
+      }
+    }
+    float I[10], t1[6], t2[6];
+    for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * b + k];
+    mul_inert_vec(f, I, ca);
+    mul_inert_vec(t1, I, cv);
+    cross_force(t2, cv, t1);
+    for (int k = 0; k < 6; k++) f[k] += t2[k];
+  }
+
   static DNI void rne(LP L, int lane) {
-    const int(*LEV)[Md::T_LEVW] = Md::t_lev();
-    const int(*CH)[Md::T_MAXCH] = Md::t_child();
-    for (int lv = 0; lv < Md::T_NLEV; lv++) {
-      const int b = lane < Md::T_LEVW ? LEV[lv][lane] : -1;
-      if (b > 0 && Md::body_weldid[b] != 0) {
-        const int pa = Md::body_parentid[b];
-        float cv[6], ca[6];
-        for (int k = 0; k < 6; k++) {
-          cv[k] = (pa == 0) ? 0.0f : L[Ly::CVEL + 6 * pa + k];
-          ca[k] = (pa == 0) ? ((k >= 3) ? -Md::gravity[k - 3] : 0.0f) : L[Ly::CACC + 6 * pa + k];
-        }
-        const int da = Md::body_dofadr[b];
-        if (b == 1) {
-          for (int i = 0; i < 3; i++) {
-            const float v = L[Ly::QVEL + i];
-            for (int k = 0; k < 6; k++) cv[k] += L[Ly::CDOF + 6 * i + k] * v;
-          }
-          float cvt[6];
-          for (int k = 0; k < 6; k++) cvt[k] = cv[k];
-          for (int i = 3; i < 6; i++) {
-            float cd[6], cdd[6];
-            for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
-            cross_motion(cdd, cvt, cd);
-            const float v = L[Ly::QVEL + i];
-            for (int k = 0; k < 6; k++) { L[Ly::CDD1 + 6 * (i - 3) + k] = cdd[k]; ca[k] += cdd[k] * v; cv[k] += cd[k] * v; }
-          }
-        } else {
-          const int nd = Md::body_dofnum[b];
-          for (int jj = 0; jj < nd; jj++) {
-            const int i = da + jj;
-            float cd[6], cdd[6];
-            for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
-            cross_motion(cdd, cv, cd);
-            const float v = L[Ly::QVEL + i];
-            for (int k = 0; k < 6; k++) { ca[k] += cdd[k] * v; cv[k] += cd[k] * v; }
-          }
-        }
-        float I[10], f[6], t1[6], t2[6];
-        for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * b + k];
-        mul_inert_vec(f, I, ca);
-        mul_inert_vec(t1, I, cv);
-        cross_force(t2, cv, t1);
-        for (int k = 0; k < 6; k++) {
-          L[Ly::CFRC + 6 * b + k] = f[k] + t2[k];
-          L[Ly::CVEL + 6 * b + k] = cv[k];
-          L[Ly::CACC + 6 * b + k] = ca[k];
+    constexpr int NR = Md::T_NROOT;
+    float cv[6], ca[6], fr[NR][6];
+    for (int k = 0; k < 6; k++) { cv[k] = 0.0f; ca[k] = (k >= 3) ? -Md::gravity[k - 3] : 0.0f; }
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      const int b = Md::T_ROOT[r];
+      body_motion(L, b, cv, ca, fr[r]);
+      if (lane == 0)
+        for (int k = 0; k < 6; k++) L[Ly::CVEL + 6 * b + k] = cv[k];
+    }
+    if (lane == 0) {  // free-joint cdof_dot for the accelerometer (sensors)
+      float cv1[6] = {0, 0, 0, 0, 0, 0};
+      for (int i = 0; i < 3; i++) {
+        const float v = L[Ly::QVEL + i];
+        for (int k = 0; k < 6; k++) cv1[k] += L[Ly::CDOF + 6 * i + k] * v;
+      }
+      for (int i = 3; i < 6; i++) {
+        float cd[6], cdd[6];
+        for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
+        cross_motion(cdd, cv1, cd);
+        for (int k = 0; k < 6; k++) L[Ly::CDD1 + 6 * (i - 3) + k] = cdd[k];
+      }
+    }
+    float S[6] = {0, 0, 0, 0, 0, 0};
+    if (lane < Md::T_NBR) {
+      int bb[Md::T_BRLEN];
+      float fb[Md::T_BRLEN][6];
+#pragma unroll
+      for (int d = 0; d < Md::T_BRLEN; d++) bb[d] = Md::t_br()[lane][d];
+#pragma unroll
+      for (int d = 0; d < Md::T_BRLEN; d++) {
+        if (bb[d] >= 0) {
+          body_motion(L, bb[d], cv, ca, fb[d]);
+          for (int k = 0; k < 6; k++) L[Ly::CVEL + 6 * bb[d] + k] = cv[k];
         }
       }
-      TSYNC();
-    }
-    // cfrc: children into parents, deepest level first (pull, no write conflicts)
-    for (int lv = Md::T_NLEV - 2; lv >= 0; lv--) {
-      const int b = lane < Md::T_LEVW ? LEV[lv][lane] : -1;
-      if (b > 0 && Md::body_weldid[b] != 0) {
-        for (int c = 0; c < Md::T_MAXCH; c++) {
-          const int ch = CH[b][c];
-          if (ch > 0 && Md::body_weldid[ch] != 0)
-            for (int k = 0; k < 6; k++) L[Ly::CFRC + 6 * b + k] += L[Ly::CFRC + 6 * ch + k];
+#pragma unroll
+      for (int d = Md::T_BRLEN - 1; d >= 0; d--) {
+        if (bb[d] >= 0) {
+          for (int k = 0; k < 6; k++) { S[k] += fb[d][k]; L[Ly::CFRC + 6 * bb[d] + k] = S[k]; }
         }
       }
-      TSYNC();
     }
+    for (int k = 0; k < 6; k++) S[k] = tsum(S[k]);
+#pragma unroll
+    for (int r = NR - 1; r >= 0; r--) {
+      for (int k = 0; k < 6; k++) S[k] += fr[r][k];
+      if (lane == 0)
+        for (int k = 0; k < 6; k++) L[Ly::CFRC + 6 * Md::T_ROOT[r] + k] = S[k];
+    }
+    TSYNC();
     for (int i = lane; i < NV; i += TEAM) {
       const int b = Md::dof_bodyid[i];
       float s = 0.0f;
@@ -269,21 +315,30 @@ struct TPhys {
     TSYNC();
   }
 
-  // ---------------- mj_crb: composite inertias (pull by level) and the sparse M ----------------
+  // ---------------- mj_crb: composite inertias (limb sums, then the root path) and the sparse M ----
   static DNI void crb(LP L, int lane) {
-    const int(*LEV)[Md::T_LEVW] = Md::t_lev();
-    const int(*CH)[Md::T_MAXCH] = Md::t_child();
-    for (int lv = Md::T_NLEV - 2; lv >= 0; lv--) {
-      const int b = lane < Md::T_LEVW ? LEV[lv][lane] : -1;
-      if (b > 0 && Md::body_weldid[b] != 0) {
-        for (int c = 0; c < Md::T_MAXCH; c++) {
-          const int ch = CH[b][c];
-          if (ch > 0 && Md::body_weldid[ch] != 0)
-            for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * b + k] += L[Ly::CIN + 10 * ch + k];
+    float S[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (lane < Md::T_NBR) {
+      int bb[Md::T_BRLEN];
+#pragma unroll
+      for (int d = 0; d < Md::T_BRLEN; d++) bb[d] = Md::t_br()[lane][d];
+#pragma unroll
+      for (int d = Md::T_BRLEN - 1; d >= 0; d--) {
+        if (bb[d] >= 0) {
+          for (int k = 0; k < 10; k++) { S[k] += L[Ly::CIN + 10 * bb[d] + k]; L[Ly::CIN + 10 * bb[d] + k] = S[k]; }
         }
       }
-      TSYNC();
     }
+    for (int k = 0; k < 10; k++) S[k] = tsum(S[k]);
+#pragma unroll
+    for (int r = Md::T_NROOT - 1; r >= 0; r--) {
+      const int b = Md::T_ROOT[r];
+      for (int k = 0; k < 10; k++) S[k] += L[Ly::CIN + 10 * b + k];
+      TSYNC();
+      if (lane == 0)
+        for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * b + k] = S[k];
+    }
+    TSYNC();
     for (int i = lane; i < NV; i += TEAM) {
       float cd[6], buf[6], I[10];
       for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
@@ -294,12 +349,16 @@ struct TPhys {
     TSYNC();
     const int* MI = Md::t_mi();
     const int* MJ = Md::t_mj();
-    for (int a = lane; a < Md::NM; a += TEAM) {
-      const int i = MI[a], j = MJ[a];
-      float s = 0.0f;
-      for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * j + k] * L[TL::FTMP + 6 * i + k];
-      if (i == j) s += L[Ly::DARM + i];
-      L[Ly::M + a] = s;
+#pragma unroll
+    for (int a0 = 0; a0 < Md::NM; a0 += TEAM) {
+      const int a = a0 + lane;
+      if (a < Md::NM) {
+        const int i = MI[a], j = MJ[a];
+        float s = 0.0f;
+        for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * j + k] * L[TL::FTMP + 6 * i + k];
+        if (i == j) s += L[Ly::DARM + i];
+        L[Ly::M + a] = s;
+      }
     }
     TSYNC();
   }
@@ -324,24 +383,37 @@ struct TPhys {
   }
 
   // ---------------- sparse LDL' of H in place (mj_factorM): one pivot per pass ----------------
-  // pass k updates the ancestors' block of pivot k and scales row k+1 (independent data)
+  // Each lane holds its index words for every pass in registers (loaded once, fully
+  // unrolled over pivots), so a pass is LDS loads -> FMA -> LDS store with no table latency.
+  // Pass k updates the ancestors' block of pivot k and scales row k+1 (independent data).
   static DNI void factor_H(LP L, int lane) {
-    const int(*LD)[3] = Md::t_ldl();
-    const int* LO = Md::t_ldl_off();
-    const int* AO = Md::t_anc_off();
-    const int* AA = Md::t_anc_adr();
+    constexpr int NR = Md::T_LDL_NRT, NA = Md::T_ANC_NRT;
+    int w[NR], a[NA];
+#pragma unroll
+    for (int r = 0; r < NR; r++) w[r] = Md::t_ldlp()[r][lane];
+#pragma unroll
+    for (int r = 0; r < NA; r++) a[r] = Md::t_ancp()[r][lane];
+#pragma unroll
     for (int k = NV - 1; k >= -1; k--) {
       if (k >= 0) {
-        const float inv = 1.0f / L[Ly::H + diag_adr(k)];
-        for (int p = LO[k] + lane; p < LO[k + 1]; p += TEAM) {
-          const int aij = LD[p][0], aki = LD[p][1], akj = LD[p][2];
-          L[Ly::H + aij] -= L[Ly::H + aki] * inv * L[Ly::H + akj];
+        const float inv = 1.0f / L[Ly::H + Md::T_DIAG[k]];
+#pragma unroll
+        for (int m = 0; m < Md::T_LDL_NR[k]; m++) {
+          const int v = w[Md::T_LDL_RB[k] + m];
+          if (v >= 0) {
+            const int aij = v & 1023, aki = (v >> 10) & 1023, akj = v >> 20;
+            L[Ly::H + aij] -= L[Ly::H + aki] * inv * L[Ly::H + akj];
+          }
         }
       }
-      const int s = k + 1;  // scale row s (its pass is complete)
-      if (s < NV) {
-        const float dinv = 1.0f / L[Ly::H + diag_adr(s)];
-        for (int p = AO[s] + lane; p < AO[s + 1]; p += TEAM) L[Ly::H + AA[p]] *= dinv;
+      const int sr = k + 1;  // scale row sr (its pass is complete)
+      if (sr < NV) {
+        const float dinv = 1.0f / L[Ly::H + Md::T_DIAG[sr]];
+#pragma unroll
+        for (int m = 0; m < Md::T_ANC_NR[sr]; m++) {
+          const int v = a[Md::T_ANC_RB[sr] + m];
+          if (v >= 0) L[Ly::H + (v >> 10)] *= dinv;
+        }
       }
       TSYNC();
     }
@@ -351,27 +423,37 @@ struct TPhys {
 
   // DST = sign * H^-1 SRC with H factored in place (mj_solveLD)
   static DNI void solve_H(LP L, int lane, int SRC, int DST, float sign) {
-    const int* AO = Md::t_anc_off();
-    const int* AD = Md::t_anc_dof();
-    const int* AA = Md::t_anc_adr();
+    constexpr int NA = Md::T_ANC_NRT;
+    int a[NA];
+#pragma unroll
+    for (int r = 0; r < NA; r++) a[r] = Md::t_ancp()[r][lane];
     for (int i = lane; i < NV; i += TEAM) L[DST + i] = L[SRC + i];
     TSYNC();
+#pragma unroll
     for (int k = NV - 1; k >= 0; k--) {
+      if (Md::T_ANC_NR[k] == 0) continue;
       const float xk = L[DST + k];
-      for (int p = AO[k] + lane; p < AO[k + 1]; p += TEAM) L[DST + AD[p]] -= L[Ly::H + AA[p]] * xk;
+#pragma unroll
+      for (int m = 0; m < Md::T_ANC_NR[k]; m++) {
+        const int v = a[Md::T_ANC_RB[k] + m];
+        if (v >= 0) L[DST + (v & 1023)] -= L[Ly::H + (v >> 10)] * xk;
+      }
       TSYNC();
     }
-    for (int i = lane; i < NV; i += TEAM) L[DST + i] = L[DST + i] / L[Ly::H + diag_adr(i)];
+    for (int i = lane; i < NV; i += TEAM) L[DST + i] = sign * (L[DST + i] / L[Ly::H + diag_adr(i)]);
     TSYNC();
+    // forward substitution is linear, so the sign can be applied before it
+#pragma unroll
     for (int k = 0; k < NV; k++) {
+      if (Md::T_ANC_NR[k] == 0) continue;
       float s = 0.0f;
-      for (int p = AO[k] + lane; p < AO[k + 1]; p += TEAM) s += L[Ly::H + AA[p]] * L[DST + AD[p]];
+#pragma unroll
+      for (int m = 0; m < Md::T_ANC_NR[k]; m++) {
+        const int v = a[Md::T_ANC_RB[k] + m];
+        if (v >= 0) s += L[Ly::H + (v >> 10)] * L[DST + (v & 1023)];
+      }
       s = tsum(s);
       if (lane == 0) L[DST + k] -= s;
-      TSYNC();
-    }
-    if (sign != 1.0f) {
-      for (int i = lane; i < NV; i += TEAM) L[DST + i] *= sign;
       TSYNC();
     }
   }
@@ -804,6 +886,7 @@ struct TPhys {
 
   // mjx solver.solve, iterations = 1
   static DNI void solve(LP L, int lane, float* scratch, int stride) {
+    STAGE_T0();
     mul_M(L, lane, Ly::WARM, Ly::MA);
     const float gw = gauss(L, lane, Ly::WARM, Ly::MA);
     jmul(L, lane, Ly::WARM, Ly::JA, true);
@@ -820,10 +903,13 @@ struct TPhys {
       mul_M(L, lane, Ly::QACC, Ly::MA);
     }
     const float g0 = gauss(L, lane, Ly::QACC, Ly::MA);
+    STAGE_MARK(9);
     const bool sparse_ok = newton_direction(L, lane);
+    STAGE_MARK(10);
     if (sparse_ok) {
       factor_H(L, lane);
       solve_H(L, lane, Ly::GRAD, Ly::SRCH, -1.0f);
+      STAGE_MARK(11);
     } else {
       TSYNC();
       S1 Ls{L};
@@ -844,6 +930,7 @@ struct TPhys {
     sn = tsum(sn); sMa = tsum(sMa); sf = tsum(sf); sMv = tsum(sMv);
     const float gtol = Md::tolerance * Md::ls_tolerance * sqrtf(sn) * Md::meaninertia * (float)(NV > 1 ? NV : 1);
     const float G0 = g0, G1 = sMa - sf, G2 = 0.5f * sMv;
+    STAGE_MARK(12);
     Rows R;
     load_rows(L, lane, R);
     const Pt p0 = eval1(R, lane, G0, G1, G2, 0.0f);
@@ -887,6 +974,7 @@ struct TPhys {
     if (improved)
       for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] += L[Ly::SRCH + i] * alpha;
     TSYNC();
+    STAGE_MARK(13);
   }
 
   // ---------------- sensors (last substep) ----------------

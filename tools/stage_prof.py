@@ -11,7 +11,8 @@ from open_duck_playground_amd import native  # noqa: E402
 from open_duck_playground_amd.joystick import Joystick  # noqa: E402
 
 NAMES = ["kinematics", "com_pos", "rne", "crb", "smooth+factor+solve_H", "collision", "make_rows", "solve",
-         "sensors+euler"]
+         "sensors+euler", "solve:warmstart", "solve:newton_dir", "solve:factor+solve", "solve:jmul+mulM",
+         "solve:linesearch"]
 
 
 def main():
@@ -30,7 +31,7 @@ def main():
         env.step(st, a)
     torch.cuda.synchronize()
     lib.duck_debug_stage_cycles(buf, 1)
-    tot = sum(buf[k] for k in range(len(NAMES)))
+    tot = sum(buf[k] for k in range(9))
     nwg = (n + 15) // 16
     for k, name in enumerate(NAMES):
         print(f"{name:24s} {buf[k] / (nwg * steps * 10):12.0f} cycles/substep/wave  {100 * buf[k] / tot:5.1f}%")
