@@ -57,8 +57,8 @@ template <class Md>
 struct TLay {
   using Ly = Lay<Md>;
   static constexpr int KC = Ly::TOTAL;                 // K.cdof per chain dof (6 x MAXCHAIN)
-  static constexpr int TSP = KC + 6 * Md::MAXCHAIN;    // foot spatial motions (12)
-  static constexpr int USED = TSP + 12;
+  static constexpr int TSP = KC + 6 * Md::MAXCHAIN;    // foot spatial motions (2 x 12)
+  static constexpr int USED = TSP + 24;
   static constexpr int STRIDE = ((USED + 15) / 32) * 32 + 16;  // = 16 (mod 32), >= USED
   static_assert(STRIDE >= USED && STRIDE % 32 == 16, "stride");
   static constexpr int FTMP = Ly::JA;                  // crb: F_i = I_b cdof_i (dead row storage)
@@ -109,7 +109,7 @@ struct TPhys {
     for (int k = 0; k < 9; k++) L[Ly::XMAT + 9 * b + k] = R[k];
   }
 
-  static DNI void kinematics(LP L, int lane) {
+  static DK void kinematics(LP L, int lane) {
     float p[3], q[4], R[9];
     for (int k = 0; k < 3; k++) p[k] = L[Ly::QPOS + k];
     for (int k = 0; k < 4; k++) q[k] = L[Ly::QPOS + 3 + k];
@@ -144,7 +144,7 @@ struct TPhys {
   }
 
   // ---------------- mj_comPos: subtree com (team reduction), cinert, cdof ----------------
-  static DNI void com_pos(LP L, int lane) {
+  static DK void com_pos(LP L, int lane) {
     float ms = 0.0f, cx = 0.0f, cy = 0.0f, cz = 0.0f;
     for (int b = 1 + lane; b < NB; b += TEAM) {
       if (Md::body_weldid[b] == 0) continue;
@@ -254,7 +254,7 @@ struct TPhys {
     for (int k = 0; k < 6; k++) f[k] += t2[k];
   }
 
-  static DNI void rne(LP L, int lane) {
+  static DK void rne(LP L, int lane) {
     constexpr int NR = Md::T_NROOT;
     float cv[6], ca[6], fr[NR][6];
     for (int k = 0; k < 6; k++) { cv[k] = 0.0f; ca[k] = (k >= 3) ? -Md::gravity[k - 3] : 0.0f; }
@@ -316,7 +316,7 @@ struct TPhys {
   }
 
   // ---------------- mj_crb: composite inertias (limb sums, then the root path) and the sparse M ----
-  static DNI void crb(LP L, int lane) {
+  static DK void crb(LP L, int lane) {
     float S[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (lane < Md::T_NBR) {
       int bb[Md::T_BRLEN];
@@ -364,7 +364,7 @@ struct TPhys {
   }
 
   // ---------------- actuation + passive; H = M ----------------
-  static DNI void smooth(LP L, int lane) {
+  static DK void smooth(LP L, int lane) {
     for (int i = lane; i < NV; i += TEAM) L[Ly::FSM + i] += -Md::dof_damping[i] * L[Ly::QVEL + i];
     TSYNC();
     if (lane < NU) {
@@ -386,7 +386,7 @@ struct TPhys {
   // Each lane holds its index words for every pass in registers (loaded once, fully
   // unrolled over pivots), so a pass is LDS loads -> FMA -> LDS store with no table latency.
   // Pass k updates the ancestors' block of pivot k and scales row k+1 (independent data).
-  static DNI void factor_H(LP L, int lane) {
+  static DK void factor_H(LP L, int lane) {
     constexpr int NR = Md::T_LDL_NRT, NA = Md::T_ANC_NRT;
     int w[NR], a[NA];
 #pragma unroll
@@ -422,7 +422,7 @@ struct TPhys {
   static DK int diag_adr(int i) { return Md::t_madr()[i][i]; }
 
   // DST = sign * H^-1 SRC with H factored in place (mj_solveLD)
-  static DNI void solve_H(LP L, int lane, int SRC, int DST, float sign) {
+  static DK void solve_H(LP L, int lane, int SRC, int DST, float sign) {
     constexpr int NA = Md::T_ANC_NRT;
     int a[NA];
 #pragma unroll
@@ -460,7 +460,7 @@ struct TPhys {
 
   // ---------------- collision ----------------
   // plane vs hull for both feet at once: lanes 0-7 take the first floor pair, 8-15 the second
-  static DNI void collide_planes(LP L, int lane) {
+  static DK void collide_planes(LP L, int lane) {
     constexpr int NH = Md::NHV;
     const int h = lane >> 3, sub = lane & 7;
     const int p = Md::PLANE_PAIR[0] * (1 - h) + Md::PLANE_PAIR[1] * h;
@@ -569,7 +569,7 @@ struct TPhys {
     }
   }
 
-  static DNI void collision(LP L, int lane) {
+  static DK void collision(LP L, int lane) {
     collide_planes(L, lane);
     if (Md::FOOT_PAIR >= 0) {
       constexpr int p = Md::FOOT_PAIR;
@@ -601,7 +601,7 @@ struct TPhys {
   }
 
   // ---------------- constraint rows ----------------
-  static DNI void make_rows(LP L, int lane) {
+  static DK void make_rows(LP L, int lane) {
     const float dt = Md::timestep;
     S1 Ls{L};
     if (lane < NFRIC) {
@@ -671,7 +671,7 @@ struct TPhys {
 
   // ---------------- Newton solver pieces ----------------
   // J.x for all rows -> DST (x at X); sub_aref: DST = J.x - aref
-  static DNI void jmul(LP L, int lane, int X, int DST, bool sub_aref) {
+  static DK void jmul(LP L, int lane, int X, int DST, bool sub_aref) {
     // foot spatial motions: lanes 0-5 left, 6-11 right
     if (lane < 12) {
       const int b = lane < 6 ? Md::LFOOT_BODY : Md::RFOOT_BODY, k = lane < 6 ? lane : lane - 6;
@@ -704,7 +704,7 @@ struct TPhys {
   }
 
   // Y = M X (sparse symmetric)
-  static DNI void mul_M(LP L, int lane, int X, int Y) {
+  static DK void mul_M(LP L, int lane, int X, int Y) {
     const int(*MA)[NV] = Md::t_madr();
     for (int i = lane; i < NV; i += TEAM) {
       float acc = 0.0f;
@@ -724,7 +724,7 @@ struct TPhys {
   }
 
   // constraint cost of all rows for Jaref at JA
-  static DNI float cost_rows(LP L, int lane) {
+  static DK float cost_rows(LP L, int lane) {
     float cost = 0.0f;
     if (lane < NFRIC) {
       const int r = lane;
@@ -741,7 +741,7 @@ struct TPhys {
 
   // gradient and H = M + J' D J at JA; SRCH = -H^-1 grad. Returns false when the
   // foot/foot rows are active (the caller takes the single-lane dense path).
-  static DNI bool newton_direction(LP L, int lane) {
+  static DK bool newton_direction(LP L, int lane) {
     for (int i = lane; i < NV; i += TEAM) L[Ly::GRAD + i] = L[Ly::MA + i] - L[Ly::FSM + i];
     for (int k = lane; k < Md::NM; k += TEAM) L[Ly::H + k] = L[Ly::M + k];
     TSYNC();
@@ -884,25 +884,131 @@ struct TPhys {
     return p;
   }
 
+  // ---- fused solver passes ----
+  // foot spatial motions of X (and X2) into TSP[0..11] (and TSP[12..23]); Y = M X (and Y2 = M X2)
+  static DK void spatial_and_M(LP L, int lane, int X, int Y, int X2, int Y2) {
+    if (lane < 12) {
+      const int b = lane < 6 ? Md::LFOOT_BODY : Md::RFOOT_BODY, k = lane < 6 ? lane : lane - 6;
+      const int(*CHN)[Md::MAXCHAIN] = Md::chain_d();
+      float s = 0.0f, s2 = 0.0f;
+#pragma unroll
+      for (int c = 0; c < Md::MAXCHAIN; c++) {
+        const int i = CHN[b][c];
+        if (i >= 0) {
+          const float cd = L[Ly::CDOF + 6 * i + k];
+          s += cd * L[X + i];
+          if (X2 >= 0) s2 += cd * L[X2 + i];
+        }
+      }
+      L[TL::TSP + lane] = s;
+      if (X2 >= 0) L[TL::TSP + 12 + lane] = s2;
+    }
+    const int(*MA)[NV] = Md::t_madr();
+    for (int i = lane; i < NV; i += TEAM) {
+      float acc = 0.0f, acc2 = 0.0f;
+#pragma unroll
+      for (int j = 0; j < NV; j++) {
+        const int a = MA[i][j];
+        if (a >= 0) {
+          const float m = L[Ly::M + a];
+          acc += m * L[X + j];
+          if (X2 >= 0) acc2 += m * L[X2 + j];
+        }
+      }
+      L[Y + i] = acc;
+      if (X2 >= 0) L[Y2 + i] = acc2;
+    }
+  }
+
+  static DK float fric_cost(float D, float x, float f) {
+    const float rf = f / D;
+    return x <= -rf ? (-f * x - 0.5f * rf * f) : (x >= rf ? (f * x - 0.5f * rf * f) : 0.5f * D * x * x);
+  }
+
+  // the lane's constraint rows for the line search: its friction row, limit rows, and the
+  // 4 edges of its contact slot (the same rows the lane computes J.x for)
+  static constexpr int NLR = (NLIM + TEAM - 1) / TEAM;
+  struct Rows2 {
+    float fD, fja, fv, ff;
+    float lD[NLR], lja[NLR], lv[NLR];
+    float cD[4], cja[4], cv[4];
+  };
+
+  static DK void quad2(const Rows2& R, int lane, float alpha, float& q0, float& q1, float& q2) {
+    if (lane < NFRIC) {
+      const float D = R.fD, ja = R.fja, v = R.fv, f = R.ff;
+      const float rf = f / D, x = ja + alpha * v;
+      if (x <= -rf) { q0 += -0.5f * rf * f - f * ja; q1 += -f * v; }
+      else if (x >= rf) { q0 += -0.5f * rf * f + f * ja; q1 += f * v; }
+      else { q0 += 0.5f * D * ja * ja; q1 += D * v * ja; q2 += 0.5f * D * v * v; }
+    }
+    auto one = [&](float D, float ja, float v) {
+      const float x = ja + alpha * v;
+      if (x < 0.0f) { q0 += 0.5f * D * ja * ja; q1 += D * v * ja; q2 += 0.5f * D * v * v; }
+    };
+#pragma unroll
+    for (int m = 0; m < NLR; m++) one(R.lD[m], R.lja[m], R.lv[m]);
+#pragma unroll
+    for (int e = 0; e < 4; e++) one(R.cD[e], R.cja[e], R.cv[e]);
+  }
+
   // mjx solver.solve, iterations = 1
-  static DNI void solve(LP L, int lane, float* scratch, int stride) {
+  static DK void solve(LP L, int lane, float* scratch, int stride) {
     STAGE_T0();
-    mul_M(L, lane, Ly::WARM, Ly::MA);
-    const float gw = gauss(L, lane, Ly::WARM, Ly::MA);
-    jmul(L, lane, Ly::WARM, Ly::JA, true);
-    const float cw = gw + cost_rows(L, lane);
-    jmul(L, lane, Ly::QSM, Ly::JA, true);
-    const float cs = cost_rows(L, lane);
+    // warm start vs smooth acceleration: J and M products of both in one pass
+    spatial_and_M(L, lane, Ly::WARM, Ly::MA, Ly::QSM, Ly::GRAD);
+    TSYNC();
+    float cwp = 0.0f, csp = 0.0f, gwp = 0.0f;
+    if (lane < NFRIC) {
+      const int r = lane, i = Md::fric_dof[r];
+      const float D = L[Ly::RD + r], f = L[Ly::DFRIC + i], ar = L[Ly::AREF + r];
+      const float jw = L[Ly::WARM + i] - ar, js = L[Ly::QSM + i] - ar;
+      cwp += fric_cost(D, jw, f);
+      csp += fric_cost(D, js, f);
+      L[Ly::JA + r] = jw;
+      L[Ly::JV + r] = js;
+    }
+    for (int r = lane; r < NLIM; r += TEAM) {
+      const int i = Md::jnt_dofadr[Md::lim_jnt[r]], row = R_LIM + r;
+      const float D = L[Ly::RD + row], sg = L[Ly::LSGN + r], ar = L[Ly::AREF + row];
+      const float jw = sg * L[Ly::WARM + i] - ar, js = sg * L[Ly::QSM + i] - ar;
+      cwp += jw < 0.0f ? 0.5f * D * jw * jw : 0.0f;
+      csp += js < 0.0f ? 0.5f * D * js * js : 0.0f;
+      L[Ly::JA + row] = jw;
+      L[Ly::JV + row] = js;
+    }
+    if (lane < NCON) {
+      float SL[6], SR[6], SL2[6], SR2[6], vw[4], vs[4];
+      for (int k = 0; k < 6; k++) {
+        SL[k] = L[TL::TSP + k]; SR[k] = L[TL::TSP + 6 + k];
+        SL2[k] = L[TL::TSP + 12 + k]; SR2[k] = L[TL::TSP + 18 + k];
+      }
+      contact_jx(L, lane >> 2, lane, SL, SR, vw);
+      contact_jx(L, lane >> 2, lane, SL2, SR2, vs);
+      for (int e = 0; e < 4; e++) {
+        const int row = R_CON + 4 * lane + e;
+        const float D = L[Ly::RD + row], ar = L[Ly::AREF + row];
+        const float jw = vw[e] - ar, js = vs[e] - ar;
+        cwp += jw < 0.0f ? 0.5f * D * jw * jw : 0.0f;
+        csp += js < 0.0f ? 0.5f * D * js * js : 0.0f;
+        L[Ly::JA + row] = jw;
+        L[Ly::JV + row] = js;
+      }
+    }
+    for (int i = lane; i < NV; i += TEAM)
+      gwp += 0.5f * (L[Ly::MA + i] - L[Ly::FSM + i]) * (L[Ly::WARM + i] - L[Ly::QSM + i]);
+    const float gw = tsum(gwp);
+    const float cw = gw + tsum(cwp), cs = tsum(csp);
+    float g0;
     if (cw < cs) {
       for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] = L[Ly::WARM + i];
-      TSYNC();
-      jmul(L, lane, Ly::QACC, Ly::JA, true);
+      g0 = gw;
     } else {
-      for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] = L[Ly::QSM + i];
-      TSYNC();
-      mul_M(L, lane, Ly::QACC, Ly::MA);
+      for (int i = lane; i < NV; i += TEAM) { L[Ly::QACC + i] = L[Ly::QSM + i]; L[Ly::MA + i] = L[Ly::GRAD + i]; }
+      for (int r = lane; r < NROW; r += TEAM) L[Ly::JA + r] = L[Ly::JV + r];
+      g0 = 0.0f;  // gauss(qacc_smooth) = 0.5 (M qs - f).(qs - qs) = 0
     }
-    const float g0 = gauss(L, lane, Ly::QACC, Ly::MA);
+    TSYNC();
     STAGE_MARK(9);
     const bool sparse_ok = newton_direction(L, lane);
     STAGE_MARK(10);
@@ -917,24 +1023,68 @@ struct TPhys {
       P1::dense_direction(Ls, scratch, stride);
       TSYNC();
     }
-    jmul(L, lane, Ly::SRCH, Ly::JV, false);
-    mul_M(L, lane, Ly::SRCH, Ly::GRAD);
+    // J.search and M.search in one pass; rows go straight to registers
+    spatial_and_M(L, lane, Ly::SRCH, Ly::GRAD, -1, -1);
+    TSYNC();
+    Rows2 R;
+    R.fD = R.fja = R.fv = R.ff = 0.0f;
+    if (lane < NFRIC) {
+      const int r = lane, i = Md::fric_dof[r];
+      R.fD = L[Ly::RD + r]; R.fja = L[Ly::JA + r]; R.fv = L[Ly::SRCH + i]; R.ff = L[Ly::DFRIC + i];
+    }
+#pragma unroll
+    for (int m = 0; m < NLR; m++) {
+      const int r = lane + TEAM * m;
+      R.lD[m] = R.lja[m] = R.lv[m] = 0.0f;
+      if (r < NLIM) {
+        const int i = Md::jnt_dofadr[Md::lim_jnt[r]], row = R_LIM + r;
+        R.lD[m] = L[Ly::RD + row]; R.lja[m] = L[Ly::JA + row]; R.lv[m] = L[Ly::LSGN + r] * L[Ly::SRCH + i];
+      }
+    }
+    for (int e = 0; e < 4; e++) R.cD[e] = R.cja[e] = R.cv[e] = 0.0f;
+    if (lane < NCON) {
+      float SL[6], SR[6], v[4];
+      for (int k = 0; k < 6; k++) { SL[k] = L[TL::TSP + k]; SR[k] = L[TL::TSP + 6 + k]; }
+      contact_jx(L, lane >> 2, lane, SL, SR, v);
+      for (int e = 0; e < 4; e++) {
+        const int row = R_CON + 4 * lane + e;
+        R.cD[e] = L[Ly::RD + row]; R.cja[e] = L[Ly::JA + row]; R.cv[e] = v[e];
+      }
+    }
     float sn = 0.0f, sMa = 0.0f, sf = 0.0f, sMv = 0.0f;
     for (int i = lane; i < NV; i += TEAM) {
-      const float s = L[Ly::SRCH + i];
-      sn += s * s;
-      sMa += s * L[Ly::MA + i];
-      sf += s * L[Ly::FSM + i];
-      sMv += s * L[Ly::GRAD + i];
+      const float sv = L[Ly::SRCH + i];
+      sn += sv * sv;
+      sMa += sv * L[Ly::MA + i];
+      sf += sv * L[Ly::FSM + i];
+      sMv += sv * L[Ly::GRAD + i];
     }
     sn = tsum(sn); sMa = tsum(sMa); sf = tsum(sf); sMv = tsum(sMv);
+    STAGE_MARK(12);
     const float gtol = Md::tolerance * Md::ls_tolerance * sqrtf(sn) * Md::meaninertia * (float)(NV > 1 ? NV : 1);
     const float G0 = g0, G1 = sMa - sf, G2 = 0.5f * sMv;
-    STAGE_MARK(12);
-    Rows R;
-    load_rows(L, lane, R);
-    const Pt p0 = eval1(R, lane, G0, G1, G2, 0.0f);
-    Pt lo = eval1(R, lane, G0, G1, G2, p0.alpha - p0.d0 / p0.d1);
+    auto mk = [&](float alpha, float q0, float q1, float q2) {
+      q0 = tsum(q0) + G0; q1 = tsum(q1) + G1; q2 = tsum(q2) + G2;
+      Pt p;
+      p.alpha = alpha;
+      p.cost = alpha * alpha * q2 + alpha * q1 + q0;
+      p.d0 = 2.0f * alpha * q2 + q1;
+      p.d1 = 2.0f * q2;
+      return p;
+    };
+    Pt p0;
+    {
+      float q0 = 0, q1 = 0, q2 = 0;
+      quad2(R, lane, 0.0f, q0, q1, q2);
+      p0 = mk(0.0f, q0, q1, q2);
+    }
+    Pt lo;
+    {
+      const float a1 = p0.alpha - p0.d0 / p0.d1;
+      float q0 = 0, q1 = 0, q2 = 0;
+      quad2(R, lane, a1, q0, q1, q2);
+      lo = mk(a1, q0, q1, q2);
+    }
     Pt hi;
     if (lo.d0 < p0.d0) { hi = p0; } else { hi = lo; lo = p0; }
     bool swap = true;
@@ -943,21 +1093,11 @@ struct TPhys {
       done = done || ((lo.d0 < 0.0f) && (lo.d0 > -gtol));
       done = done || ((hi.d0 > 0.0f) && (hi.d0 < gtol));
       if (done) break;
-      // the three candidate points share one pass over the rows
       const float al = lo.alpha - lo.d0 / lo.d1, ah = hi.alpha - hi.d0 / hi.d1, am = 0.5f * (lo.alpha + hi.alpha);
       float a0 = 0, a1 = 0, a2 = 0, b0 = 0, b1 = 0, b2 = 0, c0 = 0, c1 = 0, c2 = 0;
-      row_quad(R, lane, al, a0, a1, a2);
-      row_quad(R, lane, ah, b0, b1, b2);
-      row_quad(R, lane, am, c0, c1, c2);
-      auto mk = [&](float alpha, float q0, float q1, float q2) {
-        q0 = tsum(q0) + G0; q1 = tsum(q1) + G1; q2 = tsum(q2) + G2;
-        Pt p;
-        p.alpha = alpha;
-        p.cost = alpha * alpha * q2 + alpha * q1 + q0;
-        p.d0 = 2.0f * alpha * q2 + q1;
-        p.d1 = 2.0f * q2;
-        return p;
-      };
+      quad2(R, lane, al, a0, a1, a2);
+      quad2(R, lane, ah, b0, b1, b2);
+      quad2(R, lane, am, c0, c1, c2);
       const Pt lo_next = mk(al, a0, a1, a2), hi_next = mk(ah, b0, b1, b2), mid = mk(am, c0, c1, c2);
       const bool s1 = (lo.d0 > 0.0f) || (lo.d0 < lo_next.d0);
       if (s1) lo = lo_next;
@@ -978,7 +1118,7 @@ struct TPhys {
   }
 
   // ---------------- sensors (last substep) ----------------
-  static DNI void sensors(LP L, int lane) {
+  static DK void sensors(LP L, int lane) {
     const float com[3] = {L[Ly::COM], L[Ly::COM + 1], L[Ly::COM + 2]};
     float cacc1[6];
     for (int k = 0; k < 6; k++) cacc1[k] = (k >= 3) ? -Md::gravity[k - 3] : 0.0f;
@@ -1040,7 +1180,7 @@ struct TPhys {
   }
 
   // ---------------- semi-implicit Euler ----------------
-  static DNI void euler(LP L, int lane) {
+  static DK void euler(LP L, int lane) {
     const float dt = Md::timestep;
     for (int i = lane; i < NV; i += TEAM) {
       L[Ly::WARM + i] = L[Ly::QACC + i];
