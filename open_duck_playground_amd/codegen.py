@@ -175,6 +175,15 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         ldlp = [[-1] * 16]
     if not ancp:
         ancp = [[-1] * 16]
+    # register-resident LDL': lane l of column set s owns column c = 16 s + l; bit k of its
+    # descendant mask is set when c is a strict ancestor of dof k
+    assert nv <= 32
+    nc = (nv + 15) // 16
+    desc = np.zeros((nc, 16), dtype=np.int64)
+    for k in range(nv):
+        for i in _ancestors(m, k, False):
+            desc[i // 16, i % 16] |= 1 << k
+    desc = np.where(desc >= 2 ** 31, desc - 2 ** 32, desc)
     pplane = [p for p in range(m.npair) if m.pair_geom1[p] == floor]
     pfoot = [p for p in range(m.npair) if m.pair_geom1[p] != floor]
     assert len(pplane) == 2 and len(pfoot) <= 1
@@ -200,7 +209,8 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     tabs = {"lev": (lev, "int"), "child": (child, "int"), "madr": (full, "int"), "mi": (mi, "int"), "mj": (mj, "int"),
             "ldl": (np.array(ldl).reshape(-1, 3), "int"), "ldl_off": (ldl_off, "int"), "anc_dof": (anc_dof, "int"),
             "anc_adr": (anc_adr, "int"), "anc_off": (anc_off, "int"),
-            "ldlp": (np.array(ldlp), "int"), "ancp": (np.array(ancp), "int"), "br": (br_arr, "int")}
+            "ldlp": (np.array(ldlp), "int"), "ancp": (np.array(ancp), "int"), "br": (br_arr, "int"),
+            "desc": (desc, "int")}
     dev = [T(k, a, t) for k, (a, t) in tabs.items()]
     acc = [f"  static constexpr int T_NLEV = {nlev}, T_LEVW = {levw}, T_MAXCH = {maxch};\n",
            f"  static constexpr int T_MAXLDL = {max(ldl_off[k + 1] - ldl_off[k] for k in range(nv))}, "

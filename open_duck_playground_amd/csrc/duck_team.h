@@ -12,6 +12,8 @@
 // so the two teams of a 32-lane half hit disjoint banks. Rare paths (foot/foot contact)
 // fall back to the single-lane code of duck_physics.h executed identically by all 16 lanes.
 #pragma once
+#include <utility>
+
 #include "duck_physics.h"
 
 constexpr int TEAM = 16;
@@ -378,7 +380,6 @@ struct TPhys {
       L[Ly::AF + a] = f;
       L[Ly::FSM + Md::actuator_dof[a]] += g * f;
     }
-    for (int k = lane; k < Md::NM; k += TEAM) L[Ly::H + k] = L[Ly::M + k];
     TSYNC();
   }
 
@@ -456,6 +457,100 @@ struct TPhys {
       if (lane == 0) L[DST + k] -= s;
       TSYNC();
     }
+  }
+
+  // ---------------- register-resident LDL' (mj_factorM + mj_solveLD) ----------------
+  // Lane l holds column c = 16 s + l of the matrix densely in registers (col[s][row]); a pivot
+  // reads H[K][I] from the lane owning column I with a DPP row broadcast (row_newbcast), so
+  // a pass is a handful of broadcasts and FMAs with no memory traffic. Entries above the
+  // diagonal may collect garbage; they are never read unmasked (descendant masks).
+  static constexpr int NC = (NV + TEAM - 1) / TEAM;
+  struct Fac {
+    float col[NC][NV];
+    float dg[NC];
+    unsigned desc[NC];
+  };
+  template <int SRC>
+  static DK float bc(float v) { return dppf<0x150 + SRC>(v); }
+
+  template <int K, int I>
+  static DK void fac_anc(Fac& F, float inv) {
+    if constexpr (I >= 0) {
+      const float hki = bc<I % TEAM>(F.col[I / TEAM][K]);  // H[K][I], unscaled
+#pragma unroll
+      for (int s = 0; s < NC; s++) F.col[s][I] -= hki * inv * F.col[s][K];
+      fac_anc<K, Md::dof_parentid[I]>(F, inv);
+    }
+  }
+  template <int K>
+  static DK void fac_pass(Fac& F, int lane) {
+    constexpr int ks = K / TEAM, kl = K % TEAM;
+    const float dk = bc<kl>(F.col[ks][K]);
+    F.dg[ks] = lane == kl ? F.col[ks][K] : F.dg[ks];
+    const float inv = 1.0f / dk;
+    fac_anc<K, Md::dof_parentid[K]>(F, inv);
+#pragma unroll
+    for (int s = 0; s < NC; s++) F.col[s][K] = (s == ks && lane == kl) ? F.col[s][K] : F.col[s][K] * inv;
+  }
+  template <int K>
+  static DK void sol_back(const Fac& F, float* x) {
+    const float xk = bc<K % TEAM>(x[K / TEAM]);
+#pragma unroll
+    for (int s = 0; s < NC; s++) x[s] -= ((F.desc[s] >> K) & 1u) ? F.col[s][K] * xk : 0.0f;
+  }
+  template <int K>
+  static DK void sol_fwd(const Fac& F, float* x, int lane) {
+    float p = 0.0f;
+#pragma unroll
+    for (int s = 0; s < NC; s++) p += ((F.desc[s] >> K) & 1u) ? F.col[s][K] * x[s] : 0.0f;
+    p = tsum(p);
+    if (lane == K % TEAM) x[K / TEAM] -= p;
+  }
+  template <int... J>
+  static DK void fac_all(Fac& F, int lane, std::integer_sequence<int, J...>) {
+    (fac_pass<NV - 1 - J>(F, lane), ...);
+  }
+  template <int... J>
+  static DK void back_all(const Fac& F, float* x, std::integer_sequence<int, J...>) {
+    (sol_back<NV - 1 - J>(F, x), ...);
+  }
+  template <int... J>
+  static DK void fwd_all(const Fac& F, float* x, int lane, std::integer_sequence<int, J...>) {
+    (sol_fwd<J>(F, x, lane), ...);
+  }
+
+  // DST = sign * A^-1 SRC for the tree-sparse SPD matrix A stored at HOFF (M_adr pattern)
+  static DK void solve_regs(LP L, int lane, int HOFF, int SRC, int DST, float sign) {
+    Fac F;
+    const int(*MA)[NV] = Md::t_madr();
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane;
+      F.desc[s] = c < NV ? (unsigned)Md::t_desc()[s][lane] : 0u;
+      F.dg[s] = 1.0f;
+#pragma unroll
+      for (int r = 0; r < NV; r++) {
+        const int a = (c < NV && r >= c) ? MA[r][c < NV ? c : 0] : -1;
+        F.col[s][r] = a >= 0 ? L[HOFF + a] : 0.0f;
+      }
+    }
+    fac_all(F, lane, std::make_integer_sequence<int, NV>{});
+    float x[NC];
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane;
+      x[s] = c < NV ? L[SRC + c] : 0.0f;
+    }
+    back_all(F, x, std::make_integer_sequence<int, NV>{});
+#pragma unroll
+    for (int s = 0; s < NC; s++) x[s] = x[s] / F.dg[s];
+    fwd_all(F, x, lane, std::make_integer_sequence<int, NV>{});
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane;
+      if (c < NV) L[DST + c] = sign * x[s];
+    }
+    TSYNC();
   }
 
   // ---------------- collision ----------------
@@ -1013,8 +1108,7 @@ struct TPhys {
     const bool sparse_ok = newton_direction(L, lane);
     STAGE_MARK(10);
     if (sparse_ok) {
-      factor_H(L, lane);
-      solve_H(L, lane, Ly::GRAD, Ly::SRCH, -1.0f);
+      solve_regs(L, lane, Ly::H, Ly::GRAD, Ly::SRCH, -1.0f);
       STAGE_MARK(11);
     } else {
       TSYNC();
@@ -1217,8 +1311,7 @@ struct TPhys {
     crb(L, lane);
     STAGE_MARK(3);
     smooth(L, lane);
-    factor_H(L, lane);
-    solve_H(L, lane, Ly::FSM, Ly::QSM, 1.0f);
+    solve_regs(L, lane, Ly::M, Ly::FSM, Ly::QSM, 1.0f);
     STAGE_MARK(4);
     collision(L, lane);
     STAGE_MARK(5);
