@@ -286,6 +286,8 @@ def model_header(m: Model, variant: str) -> str:
            f"  static constexpr int FLOOR_GEOM = {floor}, LFOOT_GEOM = {lfoot}, RFOOT_GEOM = {rfoot};\n",
            f"  static constexpr int LFOOT_BODY = {m.geom_bodyid[lfoot]}, RFOOT_BODY = {m.geom_bodyid[rfoot]};\n",
            f"  static constexpr int FLOOR_TYPE = {m.geom_type[floor]};\n",
+           f"  static constexpr int HF_NROW = {int(m.hfield_nrow)}, HF_NCOL = {int(m.hfield_ncol)};\n",
+           f"  static constexpr float HF_SIZE[4] = {{{', '.join(_f(x) for x in m.hfield_size)}}};\n",
            f"  static constexpr float timestep = {_f(m.opt_timestep)}, impratio = {_f(m.opt_impratio)};\n",
            f"  static constexpr float tolerance = {_f(m.opt_tolerance)}, ls_tolerance = {_f(m.opt_ls_tolerance)};\n",
            f"  static constexpr float meaninertia = {_f(m.stat_meaninertia)};\n",
@@ -361,7 +363,8 @@ def model_header(m: Model, variant: str) -> str:
 def main():
     gen = os.path.join(HERE, "csrc", "generated")
     os.makedirs(gen, exist_ok=True)
-    for variant, task in (("flat", "flat_terrain"), ("backlash", "flat_terrain_backlash")):
+    for variant, task in (("flat", "flat_terrain"), ("backlash", "flat_terrain_backlash"),
+                          ("rough", "rough_terrain"), ("rough_backlash", "rough_terrain_backlash")):
         m = Model.load(os.path.join(HERE, "assets", f"{task}.npz"))
         with open(os.path.join(gen, f"duck_model_{variant}.h"), "w") as f:
             f.write(model_header(m, variant))

@@ -1,0 +1,148 @@
+// duck_capi.hip — the C ABI of libduck.so (include/duck.h): argument checks, handle
+// lifetime, device uploads of the shared tables, and dispatch to the compiled model
+// variant (variant_*.hip). Every entry returns DUCK_OK or a negative code with a
+// thread-local message; no entry allocates, synchronises or throws on the step path.
+#include "duck_common.h"
+
+const VariantOps* duck_variant_flat();
+const VariantOps* duck_variant_backlash();
+const VariantOps* duck_variant_rough();
+const VariantOps* duck_variant_rough_backlash();
+static const VariantOps* const kVariants[] = {duck_variant_flat(), duck_variant_backlash(), duck_variant_rough(),
+                                              duck_variant_rough_backlash()};
+static constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+static thread_local std::string g_err;
+int duck_fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+extern "C" {
+
+int duck_version(void) { return DUCK_VERSION; }
+const char* duck_last_error(void) { return g_err.c_str(); }
+
+int duck_layout_get(int nq, int nv, int nu, int imitation, duck_layout* out) {
+  if (!out) return duck_fail(DUCK_EINVAL, "null out");
+  *out = duck_layout_make(nq, nv, nu, imitation);
+  return DUCK_OK;
+}
+
+int duck_aux_size(const duck_sim* sim) {
+  if (!sim) return duck_fail(DUCK_EINVAL, "null sim");
+  return kVariants[sim->variant]->aux_size();
+}
+
+void duck_destroy(duck_sim* s) {
+  if (!s) return;
+  if (s->frames_d) (void)hipFree(s->frames_d);
+  if (s->hfield_d) (void)hipFree(s->hfield_d);
+  delete s;
+}
+
+int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const duck_refmotion* ref, int device,
+                duck_sim** out) {
+  g_err.clear();
+  if (!model || !cfg || !out) return duck_fail(DUCK_EINVAL, "null argument");
+  int v = -1;
+  for (int i = 0; i < kNumVariants && v < 0; i++)
+    if (kVariants[i]->matches(model)) v = i;
+  if (v < 0)
+    return duck_fail(DUCK_EUNSUPPORTED,
+                     "model does not match a compiled Open Duck variant (flat / flat_backlash / rough / rough_backlash)");
+  if (cfg->use_imitation && !ref) return duck_fail(DUCK_EINVAL, "use_imitation requires a reference-motion table");
+  if (cfg->n_substeps < 1 || cfg->action_max_delay < 1 || cfg->action_max_delay > 3)
+    return duck_fail(DUCK_EINVAL, "bad config (n_substeps >= 1, 1 <= action_max_delay <= 3)");
+  if (kVariants[v]->lds_bytes() > 160 * 1024) return duck_fail(DUCK_EUNSUPPORTED, "per-workgroup LDS over 160 KiB");
+  HIPCHECK(hipSetDevice(device));
+  duck_sim* s = new duck_sim();
+  memset(s, 0, sizeof(*s));
+  s->device = device;
+  s->variant = v;
+  s->cfg = *cfg;
+  s->nq = model->nq; s->nv = model->nv; s->nu = model->nu;
+  s->lay = duck_layout_make(model->nq, model->nv, model->nu, cfg->use_imitation);
+  s->drl = duck_dr_layout_make(model->nbody, model->nu);
+  if (ref) {
+    if (ref->n_dim != 40 || ref->n_dx > 16 || ref->n_dy > 16 || ref->n_dtheta > 16 || ref->nb_steps_in_period < 1 ||
+        !ref->frames) {
+      delete s;
+      return duck_fail(DUCK_EINVAL, "reference-motion table must be [<=16][<=16][<=16][nb][40] frames");
+    }
+    s->ref.n_dx = ref->n_dx; s->ref.n_dy = ref->n_dy; s->ref.n_dtheta = ref->n_dtheta;
+    s->ref.n_dim = ref->n_dim; s->ref.n_coef = ref->n_coef; s->ref.nb = ref->nb_steps_in_period;
+    memcpy(s->ref.dxs, ref->dxs, sizeof(ref->dxs)); memcpy(s->ref.dys, ref->dys, sizeof(ref->dys));
+    memcpy(s->ref.dthetas, ref->dthetas, sizeof(ref->dthetas));
+    memcpy(s->ref.dx_range, ref->dx_range, 8); memcpy(s->ref.dy_range, ref->dy_range, 8);
+    memcpy(s->ref.dtheta_range, ref->dtheta_range, 8);
+    const size_t nbytes =
+        sizeof(float) * (size_t)ref->n_dx * ref->n_dy * ref->n_dtheta * ref->nb_steps_in_period * ref->n_dim;
+    hipError_t e = hipMalloc(&s->frames_d, nbytes);
+    if (e == hipSuccess) e = hipMemcpy(s->frames_d, ref->frames, nbytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      duck_destroy(s);
+      return duck_fail(DUCK_EHIP, std::string("reference table upload: ") + hipGetErrorString(e));
+    }
+  }
+  if (kVariants[v]->floor_type == 1) {  // height field elevation, [nrow][ncol] in [0, 1]
+    const size_t nn = (size_t)model->hfield_nrow * model->hfield_ncol;
+    float* h = new float[nn];
+    for (size_t i = 0; i < nn; i++) h[i] = (float)model->hfield_data[i];
+    hipError_t e = hipMalloc(&s->hfield_d, nn * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(s->hfield_d, h, nn * sizeof(float), hipMemcpyHostToDevice);
+    delete[] h;
+    if (e != hipSuccess) {
+      duck_destroy(s);
+      return duck_fail(DUCK_EHIP, std::string("height field upload: ") + hipGetErrorString(e));
+    }
+  }
+  *out = s;
+  return DUCK_OK;
+}
+
+int duck_reset(duck_sim* s, int n, float* fstate, int32_t* istate, const uint8_t* mask, uint64_t seed,
+               int64_t env_offset, const float* dr, float* obs, float* priv, void* stream) {
+  g_err.clear();
+  if (!s || n < 0 || !fstate || !istate || !obs || !priv) return duck_fail(DUCK_EINVAL, "bad argument");
+  if (n == 0) return DUCK_OK;
+  HIPCHECK(hipSetDevice(s->device));
+  return kVariants[s->variant]->reset(s, n, fstate, istate, mask, seed, env_offset, dr, obs, priv,
+                                      (hipStream_t)stream);
+}
+
+int duck_step(duck_sim* s, int n, float* fstate, int32_t* istate, const float* dr, const float* action, float* obs,
+              float* priv, float* reward, float* done, float* scratch, void* stream) {
+  g_err.clear();
+  if (!s || n < 0 || !fstate || !istate || !action || !obs || !priv || !reward || !done)
+    return duck_fail(DUCK_EINVAL, "bad argument");
+  if (n == 0) return DUCK_OK;
+  HIPCHECK(hipSetDevice(s->device));
+  return kVariants[s->variant]->step(s, n, fstate, istate, dr, action, obs, priv, reward, done, scratch,
+                                     (hipStream_t)stream);
+}
+
+int duck_randomize(duck_sim* s, int n, float* dr, uint64_t seed, int64_t env_offset, void* stream) {
+  g_err.clear();
+  if (!s || n < 0 || !dr) return duck_fail(DUCK_EINVAL, "bad argument");
+  if (n == 0) return DUCK_OK;
+  HIPCHECK(hipSetDevice(s->device));
+  return kVariants[s->variant]->randomize(s, n, dr, seed, env_offset, (hipStream_t)stream);
+}
+
+int duck_physics_step(duck_sim* s, int n, float* qpos, float* qvel, float* warm, const float* ctrl, const float* dr,
+                      int nsub, float* aux, float* scratch, void* stream) {
+  g_err.clear();
+  if (!s || n < 0 || !qpos || !qvel || !warm || !ctrl || nsub < 0) return duck_fail(DUCK_EINVAL, "bad argument");
+  if (n == 0) return DUCK_OK;
+  HIPCHECK(hipSetDevice(s->device));
+  return kVariants[s->variant]->physics(s, n, qpos, qvel, warm, ctrl, dr, nsub, aux, scratch, (hipStream_t)stream);
+}
+
+// debug: per-stage cycle counters of a -DDUCK_STAGE_PROF build (DUCK_EUNSUPPORTED otherwise)
+int duck_debug_stage_cycles(const duck_sim* s, unsigned long long* out, int reset) {
+  if (!s || !out) return duck_fail(DUCK_EINVAL, "bad argument");
+  return kVariants[s->variant]->stage_cycles(out, reset);
+}
+
+}  // extern "C"

@@ -1,36 +1,18 @@
-// duck_kernels.hip — Joystick env kernels + C ABI (include/duck.h) for MI355X (gfx950).
+// duck_env_kernels.h — Joystick env kernels for MI355X (gfx950), templated on the model.
 //
-// One env per lane; one launch per env-step runs the whole of Joystick.step
-// (joystick.py:323-481): imitation phase + reference motion, action delay, push,
-// motor-target rate limit, 10 fused physics substeps (duck_physics.h), contacts, obs,
-// termination, rewards, info bookkeeping, and (optionally) the training wrappers
-// EpisodeWrapper + BraxAutoResetWrapper. Per-env state never leaves the lane between
-// substeps; HBM sees one coalesced read and one write of the state per env-step.
-#include <hip/hip_runtime.h>
-#include <math.h>
-#include <stdio.h>
-#include <string.h>
-
-#include <string>
-
-#include "../../include/duck.h"
+// One launch per env-step runs the whole of Joystick.step (joystick.py:323-481):
+// imitation phase + reference motion, action delay, push, motor-target rate limit, 10
+// fused physics substeps (duck_team.h: 16 lanes per env; duck_physics.h: one lane per env),
+// contacts, obs, termination, rewards, info bookkeeping, and (optionally) the training
+// wrappers EpisodeWrapper + BraxAutoResetWrapper. Per-env state never leaves LDS between
+// substeps; HBM sees one read and one write of the state per env-step.
+//
+// Included by one variant_*.hip per compiled model (after its generated header), which
+// instantiates the kernels and exports a VariantOps table; duck_capi.hip dispatches.
+#pragma once
+#include "duck_common.h"
 #include "duck_physics.h"
 #include "duck_team.h"
-#include "generated/duck_model_backlash.h"
-#include "generated/duck_model_flat.h"
-
-#define DUCK_VERSION 100  // 0.1.0
-
-static thread_local std::string g_err;
-static int fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
-#define HIPCHECK(x)                                                                      \
-  do {                                                                                   \
-    hipError_t _e = (x);                                                                 \
-    if (_e != hipSuccess) return fail(DUCK_EHIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
-  } while (0)
 
 // per-step RNG slot map (identical to oracle/duck_oracle.c)
 enum { SLOT_ACTION_DELAY = 0, SLOT_PUSH_THETA = 1, SLOT_PUSH_MAG = 2, SLOT_GYRO = 3, SLOT_ACCEL = 6,
@@ -40,12 +22,6 @@ enum { RSLOT_DXY = 0, RSLOT_YAW = 2, RSLOT_QSCALE = 3, RSLOT_QVEL = 19, RSLOT_CM
 #define KEY_TAG_ENV 0x5EEDu
 #define KEY_TAG_DR 0xD0D0u
 #define PI_F 3.14159265358979323846f
-
-struct RefMeta {
-  int n_dx, n_dy, n_dtheta, n_dim, n_coef, nb;
-  float dxs[16], dys[16], dthetas[16];
-  float dx_range[2], dy_range[2], dtheta_range[2];
-};
 
 struct KArgs {
   int n;
@@ -62,6 +38,7 @@ struct KArgs {
   uint64_t seed;
   int64_t env_offset;
   const float* frames;
+  const float* hfield;
   RefMeta ref;
   duck_env_config cfg;
   duck_layout lay;
@@ -117,10 +94,12 @@ DK Slice<SW> env_slice(float* lds, int t) {
 
 template <class Md>
 DK void phys_step(Slice<SW> L, int lane, bool integrate, bool want_out, float* aux, int aux_stride, float* scratch,
-                  int sstride) {
+                  int sstride, const float* hfield) {
 #if DUCK_TEAM
-  TPhys<Md>::step(L.p, lane, integrate, want_out, aux, aux_stride, scratch, sstride);
+  TPhys<Md>::step(L.p, lane, integrate, want_out, aux, aux_stride, scratch, sstride, hfield);
 #else
+  static_assert(Md::FLOOR_TYPE == 0, "the single-lane build supports plane floors only");
+  (void)hfield;
   Phys<Md, WG>::step(L, integrate, want_out, aux, aux_stride, scratch, sstride);
 #endif
 }
@@ -329,7 +308,7 @@ __global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
   for (int a = 0; a < NU; a++) L[Ly::QPOS + c.actuator_qposadr[a]] *= r.uniform(RSLOT_QSCALE + a, 0.5f, 1.5f);
   for (int k = 0; k < 6; k++) L[Ly::QVEL + k] = r.uniform(RSLOT_QVEL + k, -0.05f, 0.05f);
   for (int a = 0; a < NU; a++) L[Ly::CTRL + a] = L[Ly::QPOS + c.actuator_qposadr[a]];
-  phys_step<Md>(L, lane, false, true, nullptr, 0, A.scratch ? A.scratch + e : nullptr, A.n);
+  phys_step<Md>(L, lane, false, true, nullptr, 0, A.scratch ? A.scratch + e : nullptr, A.n, A.hfield);
   float cmd[7];
   sample_command(c, r, RSLOT_CMD, cmd);
   const float push_interval = r.uniform(RSLOT_PUSH, c.push_interval_range[0], c.push_interval_range[1]);
@@ -424,7 +403,8 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   load_dyn<Md, SW>(A, e, L);
   // physics (joystick.py:420)
   float* scr = A.scratch ? A.scratch + e : nullptr;
-  for (int s = 0; s < c.n_substeps; s++) phys_step<Md>(L, lane, true, s == c.n_substeps - 1, nullptr, 0, scr, n);
+  for (int s = 0; s < c.n_substeps; s++)
+    phys_step<Md>(L, lane, true, s == c.n_substeps - 1, nullptr, 0, scr, n, A.hfield);
   for (int a = 0; a < NU; a++) { F[Lo.motor_targets + a] = L[Ly::CTRL + a]; F[Lo.ctrl + a] = L[Ly::CTRL + a]; }
   const float con[2] = {L[Ly::OCON], L[Ly::OCON + 1]};
   // feet bookkeeping (joystick.py:424-435)
@@ -563,9 +543,9 @@ __global__ void __launch_bounds__(TPB) physics_kernel(KArgs A, float* qpos_g, fl
   float* ax = aux ? aux + e : nullptr;
   float* scr = A.scratch ? A.scratch + e : nullptr;
   if (nsub == 0) {
-    phys_step<Md>(L, lane, false, true, ax, n, scr, n);
+    phys_step<Md>(L, lane, false, true, ax, n, scr, n, A.hfield);
   } else {
-    for (int s = 0; s < nsub; s++) phys_step<Md>(L, lane, true, s == nsub - 1, ax, n, scr, n);
+    for (int s = 0; s < nsub; s++) phys_step<Md>(L, lane, true, s == nsub - 1, ax, n, scr, n, A.hfield);
   }
   for (int i = 0; i < Md::NQ; i++) qpos_g[(size_t)i * n + e] = L[Ly::QPOS + i];
   for (int i = 0; i < Md::NV; i++) { qvel_g[(size_t)i * n + e] = L[Ly::QVEL + i]; warm_g[(size_t)i * n + e] = L[Ly::WARM + i]; }
@@ -603,19 +583,6 @@ __global__ void randomize_kernel(int n, float* dr, duck_dr_layout D, uint64_t se
 // --------------------------------------------------------------------------------------
 // host side
 // --------------------------------------------------------------------------------------
-enum Variant { V_FLAT = 0, V_BACKLASH = 1 };
-
-struct duck_sim {
-  int device;
-  Variant variant;
-  duck_env_config cfg;
-  duck_layout lay;
-  duck_dr_layout drl;
-  RefMeta ref;
-  float* frames_d;
-  int nq, nv, nu;
-};
-
 template <class Md>
 static bool matches(const duck_model_desc* m) {
   if (m->nq != Md::NQ || m->nv != Md::NV || m->nu != Md::NU || m->nbody != Md::NB || m->njnt != Md::NJ) return false;
@@ -633,7 +600,13 @@ static bool matches(const duck_model_desc* m) {
     if (m->pair_geom1[p] != Md::pair_geom1[p] || m->pair_geom2[p] != Md::pair_geom2[p] ||
         !close(m->pair_friction[5 * p], Md::pair_friction[p][0]))
       return false;
-  if (m->geom_type[m->pair_geom1[1]] != 0) return false;  // plane floor (hfield: not yet supported)
+  // floor: mjGEOM_PLANE (0) or mjGEOM_HFIELD (1) with the baked grid size
+  if (m->geom_type[Md::FLOOR_GEOM] != Md::FLOOR_TYPE) return false;
+  if (Md::FLOOR_TYPE == 1) {
+    if (m->hfield_nrow != Md::HF_NROW || m->hfield_ncol != Md::HF_NCOL || !m->hfield_data) return false;
+    for (int k = 0; k < 4; k++)
+      if (!close(m->hfield_size[k], Md::HF_SIZE[k])) return false;
+  }
   return true;
 }
 
@@ -646,6 +619,11 @@ static size_t lds_bytes() {
 #endif
 }
 
+template <class Md>
+static int aux_size_of() {
+  return aux_size<Md>();
+}
+
 static KArgs make_args(duck_sim* s, int n) {
   KArgs A;
   memset(&A, 0, sizeof(A));
@@ -655,11 +633,16 @@ static KArgs make_args(duck_sim* s, int n) {
   A.drl = s->drl;
   A.ref = s->ref;
   A.frames = s->frames_d;
+  A.hfield = s->hfield_d;
   return A;
 }
 
 template <class Md>
-static int launch_reset(duck_sim* s, KArgs& A, hipStream_t st) {
+static int launch_reset(duck_sim* s, int n, float* fs, int32_t* is, const uint8_t* mask, uint64_t seed,
+                        int64_t env_offset, const float* dr, float* obs, float* priv, hipStream_t st) {
+  KArgs A = make_args(s, n);
+  A.fs = fs; A.is = is; A.mask = mask; A.seed = seed; A.env_offset = env_offset; A.dr = dr;
+  A.obs = obs; A.priv = priv;
   const dim3 grid((A.n + WG - 1) / WG), block(TPB);
   hipLaunchKernelGGL((reset_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A);
   HIPCHECK(hipGetLastError());
@@ -667,9 +650,21 @@ static int launch_reset(duck_sim* s, KArgs& A, hipStream_t st) {
 }
 
 template <class Md>
-static int launch_step(duck_sim* s, KArgs& A, hipStream_t st) {
+static int launch_step(duck_sim* s, int n, float* fs, int32_t* is, const float* dr, const float* action, float* obs,
+                       float* priv, float* reward, float* done, float* scratch, hipStream_t st) {
+  KArgs A = make_args(s, n);
+  A.fs = fs; A.is = is; A.dr = dr; A.action = action; A.obs = obs; A.priv = priv;
+  A.reward = reward; A.done = done; A.scratch = scratch;
   const dim3 grid((A.n + WG - 1) / WG), block(TPB);
   hipLaunchKernelGGL((step_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A);
+  HIPCHECK(hipGetLastError());
+  return DUCK_OK;
+}
+
+template <class Md>
+static int launch_randomize(duck_sim* s, int n, float* dr, uint64_t seed, int64_t env_offset, hipStream_t st) {
+  const dim3 grid((n + 255) / 256), block(256);
+  hipLaunchKernelGGL((randomize_kernel<Md>), grid, block, 0, st, n, dr, s->drl, seed, env_offset);
   HIPCHECK(hipGetLastError());
   return DUCK_OK;
 }
@@ -686,148 +681,27 @@ static int launch_physics(duck_sim* s, int n, float* qpos, float* qvel, float* w
   return DUCK_OK;
 }
 
-extern "C" {
-
-int duck_version(void) { return DUCK_VERSION; }
-const char* duck_last_error(void) { return g_err.c_str(); }
-
-int duck_layout_get(int nq, int nv, int nu, int imitation, duck_layout* out) {
-  if (!out) return fail(DUCK_EINVAL, "null out");
-  *out = duck_layout_make(nq, nv, nu, imitation);
-  return DUCK_OK;
-}
-
-int duck_aux_size(const duck_sim* sim) {
-  if (!sim) return fail(DUCK_EINVAL, "null sim");
-  return sim->variant == V_FLAT ? aux_size<DuckModel_flat>() : aux_size<DuckModel_backlash>();
-}
-
-int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const duck_refmotion* ref, int device,
-                duck_sim** out) {
-  g_err.clear();
-  if (!model || !cfg || !out) return fail(DUCK_EINVAL, "null argument");
-  Variant v;
-  if (matches<DuckModel_flat>(model)) v = V_FLAT;
-  else if (matches<DuckModel_backlash>(model)) v = V_BACKLASH;
-  else return fail(DUCK_EUNSUPPORTED, "model does not match a compiled Open Duck variant (flat / flat_backlash)");
-  if (cfg->use_imitation && !ref) return fail(DUCK_EINVAL, "use_imitation requires a reference-motion table");
-  if (cfg->n_substeps < 1 || cfg->action_max_delay < 1 || cfg->action_max_delay > 3)
-    return fail(DUCK_EINVAL, "bad config (n_substeps >= 1, 1 <= action_max_delay <= 3)");
-  HIPCHECK(hipSetDevice(device));
-  duck_sim* s = new duck_sim();
-  s->device = device;
-  s->variant = v;
-  s->cfg = *cfg;
-  s->nq = model->nq; s->nv = model->nv; s->nu = model->nu;
-  s->lay = duck_layout_make(model->nq, model->nv, model->nu, cfg->use_imitation);
-  s->drl = duck_dr_layout_make(model->nbody, model->nu);
-  memset(&s->ref, 0, sizeof(s->ref));
-  s->frames_d = nullptr;
-  if (ref) {
-    if (ref->n_dim != 40 || ref->n_dx > 16 || ref->n_dy > 16 || ref->n_dtheta > 16 || ref->nb_steps_in_period < 1 ||
-        !ref->frames) {
-      delete s;
-      return fail(DUCK_EINVAL, "reference-motion table must be [<=16][<=16][<=16][nb][40] frames");
-    }
-    s->ref.n_dx = ref->n_dx; s->ref.n_dy = ref->n_dy; s->ref.n_dtheta = ref->n_dtheta;
-    s->ref.n_dim = ref->n_dim; s->ref.n_coef = ref->n_coef; s->ref.nb = ref->nb_steps_in_period;
-    memcpy(s->ref.dxs, ref->dxs, sizeof(ref->dxs)); memcpy(s->ref.dys, ref->dys, sizeof(ref->dys));
-    memcpy(s->ref.dthetas, ref->dthetas, sizeof(ref->dthetas));
-    memcpy(s->ref.dx_range, ref->dx_range, 8); memcpy(s->ref.dy_range, ref->dy_range, 8);
-    memcpy(s->ref.dtheta_range, ref->dtheta_range, 8);
-    const size_t nbytes =
-        sizeof(float) * (size_t)ref->n_dx * ref->n_dy * ref->n_dtheta * ref->nb_steps_in_period * ref->n_dim;
-    hipError_t e = hipMalloc(&s->frames_d, nbytes);
-    if (e == hipSuccess) e = hipMemcpy(s->frames_d, ref->frames, nbytes, hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-      if (s->frames_d) (void)hipFree(s->frames_d);
-      delete s;
-      return fail(DUCK_EHIP, std::string("reference table upload: ") + hipGetErrorString(e));
-    }
-  }
-  // LDS budget
-  const size_t need = v == V_FLAT ? lds_bytes<DuckModel_flat>() : lds_bytes<DuckModel_backlash>();
-  if (need > 160 * 1024) {
-    duck_destroy(s);
-    return fail(DUCK_EUNSUPPORTED, "per-workgroup LDS over 160 KiB");
-  }
-  *out = s;
-  return DUCK_OK;
-}
-
-void duck_destroy(duck_sim* s) {
-  if (!s) return;
-  if (s->frames_d) (void)hipFree(s->frames_d);
-  delete s;
-}
-
-
-
-
-int duck_reset(duck_sim* s, int n, float* fstate, int32_t* istate, const uint8_t* mask, uint64_t seed,
-               int64_t env_offset, const float* dr, float* obs, float* priv, void* stream) {
-  g_err.clear();
-  if (!s || n < 0 || !fstate || !istate || !obs || !priv) return fail(DUCK_EINVAL, "bad argument");
-  if (n == 0) return DUCK_OK;
-  HIPCHECK(hipSetDevice(s->device));
-  KArgs A = make_args(s, n);
-  A.fs = fstate; A.is = istate; A.mask = mask; A.seed = seed; A.env_offset = env_offset; A.dr = dr;
-  A.obs = obs; A.priv = priv;
-  hipStream_t st = (hipStream_t)stream;
-  return s->variant == V_FLAT ? launch_reset<DuckModel_flat>(s, A, st) : launch_reset<DuckModel_backlash>(s, A, st);
-}
-
-int duck_step(duck_sim* s, int n, float* fstate, int32_t* istate, const float* dr, const float* action, float* obs,
-              float* priv, float* reward, float* done, float* scratch, void* stream) {
-  g_err.clear();
-  if (!s || n < 0 || !fstate || !istate || !action || !obs || !priv || !reward || !done)
-    return fail(DUCK_EINVAL, "bad argument");
-  if (n == 0) return DUCK_OK;
-  HIPCHECK(hipSetDevice(s->device));
-  KArgs A = make_args(s, n);
-  A.fs = fstate; A.is = istate; A.dr = dr; A.action = action; A.obs = obs; A.priv = priv;
-  A.reward = reward; A.done = done; A.scratch = scratch;
-  hipStream_t st = (hipStream_t)stream;
-  return s->variant == V_FLAT ? launch_step<DuckModel_flat>(s, A, st) : launch_step<DuckModel_backlash>(s, A, st);
-}
-
-int duck_randomize(duck_sim* s, int n, float* dr, uint64_t seed, int64_t env_offset, void* stream) {
-  g_err.clear();
-  if (!s || n < 0 || !dr) return fail(DUCK_EINVAL, "bad argument");
-  if (n == 0) return DUCK_OK;
-  HIPCHECK(hipSetDevice(s->device));
-  hipStream_t st = (hipStream_t)stream;
-  const dim3 grid((n + 255) / 256), block(256);
-  if (s->variant == V_FLAT)
-    hipLaunchKernelGGL((randomize_kernel<DuckModel_flat>), grid, block, 0, st, n, dr, s->drl, seed, env_offset);
-  else
-    hipLaunchKernelGGL((randomize_kernel<DuckModel_backlash>), grid, block, 0, st, n, dr, s->drl, seed, env_offset);
-  HIPCHECK(hipGetLastError());
-  return DUCK_OK;
-}
-
-
-int duck_physics_step(duck_sim* s, int n, float* qpos, float* qvel, float* warm, const float* ctrl, const float* dr,
-                      int nsub, float* aux, float* scratch, void* stream) {
-  g_err.clear();
-  if (!s || n < 0 || !qpos || !qvel || !warm || !ctrl || nsub < 0) return fail(DUCK_EINVAL, "bad argument");
-  if (n == 0) return DUCK_OK;
-  HIPCHECK(hipSetDevice(s->device));
-  hipStream_t st = (hipStream_t)stream;
-  return s->variant == V_FLAT
-             ? launch_physics<DuckModel_flat>(s, n, qpos, qvel, warm, ctrl, dr, nsub, aux, scratch, st)
-             : launch_physics<DuckModel_backlash>(s, n, qpos, qvel, warm, ctrl, dr, nsub, aux, scratch, st);
-}
-
-}  // extern "C"
-
+static int stage_cycles_of(unsigned long long* out, int reset) {
 #ifdef DUCK_STAGE_PROF
-extern "C" int duck_debug_stage_cycles(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), sizeof(unsigned long long) * 16);
   if (e == hipSuccess && reset) {
     unsigned long long z[16] = {0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, sizeof(z));
   }
-  return e == hipSuccess ? 0 : -3;
-}
+  return e == hipSuccess ? 0 : DUCK_EHIP;
+#else
+  (void)out;
+  (void)reset;
+  return DUCK_EUNSUPPORTED;
 #endif
+}
+
+// one VariantOps table per compiled model (a host function, so the device pass skips it)
+#define DUCK_DEFINE_VARIANT(NAME, MODEL)                                                        \
+  const VariantOps* duck_variant_##NAME() {                                                     \
+    static const VariantOps ops = {#NAME,               matches<MODEL>,         aux_size_of<MODEL>, \
+                                   lds_bytes<MODEL>,    MODEL::FLOOR_TYPE,      launch_reset<MODEL>, \
+                                   launch_step<MODEL>,  launch_randomize<MODEL>, launch_physics<MODEL>, \
+                                   stage_cycles_of};                                            \
+    return &ops;                                                                                \
+  }

@@ -554,8 +554,43 @@ struct TPhys {
   }
 
   // ---------------- collision ----------------
-  // plane vs hull for both feet at once: lanes 0-7 take the first floor pair, 8-15 the second
-  static DK void collide_planes(LP L, int lane) {
+  // height-field terrain under a point (hfield frame): elevation of MuJoCo's triangulated
+  // grid (cell split along its (0,0)-(1,1) diagonal) and the triangle's unit normal
+  static DK float hf_point(const float* hf, float x, float y, float* nrm) {
+    constexpr int NR = Md::HF_NROW > 1 ? Md::HF_NROW : 2, NCc = Md::HF_NCOL > 1 ? Md::HF_NCOL : 2;
+    constexpr float sx = Md::HF_SIZE[0], sy = Md::HF_SIZE[1], sz = Md::HF_SIZE[2];
+    constexpr float dx = 2.0f * sx / (NCc - 1), dy = 2.0f * sy / (NR - 1);
+    const float fx = (x + sx) / dx, fy = (y + sy) / dy;
+    const int c = min(max((int)floorf(fx), 0), NCc - 2), r = min(max((int)floorf(fy), 0), NR - 2);
+    const float u = fminf(fmaxf(fx - (float)c, 0.0f), 1.0f), w = fminf(fmaxf(fy - (float)r, 0.0f), 1.0f);
+    const float z00 = sz * hf[r * NCc + c], z10 = sz * hf[r * NCc + c + 1];
+    const float z01 = sz * hf[(r + 1) * NCc + c], z11 = sz * hf[(r + 1) * NCc + c + 1];
+    float z;
+    if (u >= w) {
+      z = z00 + u * (z10 - z00) + w * (z11 - z10);
+      nrm[0] = -(z10 - z00) * dy; nrm[1] = dx * (z10 - z11); nrm[2] = dx * dy;
+    } else {
+      z = z00 + w * (z01 - z00) + u * (z11 - z01);
+      nrm[0] = dy * (z01 - z11); nrm[1] = -dx * (z01 - z00); nrm[2] = dx * dy;
+    }
+    const float inv = 1.0f / sqrtf(nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2]);
+    nrm[0] *= inv; nrm[1] *= inv; nrm[2] *= inv;
+    return z;
+  }
+  // signed distance of a world point to the terrain (triangle plane under it) and the
+  // terrain normal in world coordinates
+  static DK float hf_dist(const float* hf, const float* pp, const float* PR, const float* vw, float* nw) {
+    const float d[3] = {vw[0] - pp[0], vw[1] - pp[1], vw[2] - pp[2]};
+    float pl[3], nl[3];
+    mulmtv3(pl, PR, d);
+    const float z = hf_point(hf, pl[0], pl[1], nl);
+    mulmv3(nw, PR, nl);
+    return (pl[2] - z) * nl[2];
+  }
+
+  // floor (plane or height field) vs hull for both feet at once: lanes 0-7 take the first
+  // floor pair, 8-15 the second
+  static DK void collide_planes(LP L, int lane, const float* hf) {
     constexpr int NH = Md::NHV;
     const int h = lane >> 3, sub = lane & 7;
     const int p = Md::PLANE_PAIR[0] * (1 - h) + Md::PLANE_PAIR[1] * h;
@@ -578,7 +613,15 @@ struct TPhys {
       const int k = sub + 8 * r;
       const bool ok = k < NH;
       vx[r] = ok ? HV[k][0] : 0.0f; vy[r] = ok ? HV[k][1] : 0.0f; vz[r] = ok ? HV[k][2] : 0.0f;
-      sup[r] = ok ? (pl[0] - vx[r]) * nl[0] + (pl[1] - vy[r]) * nl[1] + (pl[2] - vz[r]) * nl[2] : -1e30f;
+      if constexpr (Md::FLOOR_TYPE == 0) {
+        sup[r] = ok ? (pl[0] - vx[r]) * nl[0] + (pl[1] - vy[r]) * nl[1] + (pl[2] - vz[r]) * nl[2] : -1e30f;
+      } else {
+        const float v[3] = {vx[r], vy[r], vz[r]};
+        float vw[3], nw[3];
+        mulmv3(vw, CR, v);
+        for (int q = 0; q < 3; q++) vw[q] += cp[q];
+        sup[r] = ok ? -hf_dist(hf, pp, PR, vw, nw) : -1e30f;
+      }
       smax = fmaxf(smax, sup[r]);
     }
     smax = hmax8(smax);
@@ -599,6 +642,16 @@ struct TPhys {
       return best < NH ? best : NH - 1;  // argmax_tol's default (also for NaN data)
     };
     auto vert = [&](int k, float* o) { o[0] = HV[k][0]; o[1] = HV[k][1]; o[2] = HV[k][2]; };
+    if constexpr (Md::FLOOR_TYPE == 1) {
+      // manifold plane: the terrain normal under the deepest vertex, in the hull frame
+      const int kd = argmax(sup, 0.0f);
+      float v[3], vw[3], nw[3];
+      vert(kd, v);
+      mulmv3(vw, CR, v);
+      for (int q = 0; q < 3; q++) vw[q] += cp[q];
+      (void)hf_dist(hf, pp, PR, vw, nw);
+      mulmtv3(nl, CR, nw);
+    }
     float s[R];
     const int a = argmax(dm, 0.0f);
     float pa[3];
@@ -647,25 +700,32 @@ struct TPhys {
       d = d < 2 * NH ? d : 2 * NH - 1;
       d = d >= NH ? d - NH : d;
     }
-    float fr[9];
-    make_frame(fr, n);
     if (sub < 4) {
       const int idx[4] = {a, b, c, d};
       const int me = idx[sub];
       bool unique = true;
       for (int e = 0; e < 4; e++) unique = unique && !(e < sub && idx[e] == me);
-      float v[3], vw[3], pos[3];
+      float v[3], vw[3], pos[3], nw[3], fr[9];
       vert(me, v);
-      const float sp = (pl[0] - v[0]) * nl[0] + (pl[1] - v[1]) * nl[1] + (pl[2] - v[2]) * nl[2];
-      const float dist = unique ? -sp : 1.0f;
       mulmv3(vw, CR, v);
-      for (int q = 0; q < 3; q++) pos[q] = cp[q] + vw[q] - 0.5f * dist * n[q];
+      float sp;
+      if constexpr (Md::FLOOR_TYPE == 0) {
+        sp = (pl[0] - v[0]) * nl[0] + (pl[1] - v[1]) * nl[1] + (pl[2] - v[2]) * nl[2];
+        nw[0] = n[0]; nw[1] = n[1]; nw[2] = n[2];
+        for (int q = 0; q < 3; q++) vw[q] += cp[q];
+      } else {
+        for (int q = 0; q < 3; q++) vw[q] += cp[q];
+        sp = -hf_dist(hf, pp, PR, vw, nw);
+      }
+      const float dist = unique ? -sp : 1.0f;
+      for (int q = 0; q < 3; q++) pos[q] = vw[q] - 0.5f * dist * nw[q];
+      make_frame(fr, nw);
       P1::store_contact(Ls, 4 * p + sub, dist, pos, fr);
     }
   }
 
-  static DK void collision(LP L, int lane) {
-    collide_planes(L, lane);
+  static DK void collision(LP L, int lane, const float* hf) {
+    collide_planes(L, lane, hf);
     if (Md::FOOT_PAIR >= 0) {
       constexpr int p = Md::FOOT_PAIR;
       const int s1 = cgeom_slot<Md>(Md::pair_geom1[p]), s2 = cgeom_slot<Md>(Md::pair_geom2[p]);
@@ -1300,7 +1360,7 @@ struct TPhys {
   }
 
   static DK void step(LP L, int lane, bool integrate, bool want_out, float* aux, int aux_stride, float* scratch,
-                      int sstride) {
+                      int sstride, const float* hf) {
     STAGE_T0();
     kinematics(L, lane);
     STAGE_MARK(0);
@@ -1313,7 +1373,7 @@ struct TPhys {
     smooth(L, lane);
     solve_regs(L, lane, Ly::M, Ly::FSM, Ly::QSM, 1.0f);
     STAGE_MARK(4);
-    collision(L, lane);
+    collision(L, lane, hf);
     STAGE_MARK(5);
     make_rows(L, lane);
     STAGE_MARK(6);

@@ -18,6 +18,7 @@ CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 
 EXPORTS = ["duck_version", "duck_last_error", "duck_layout_get", "duck_aux_size", "duck_create", "duck_destroy",
+           "duck_debug_stage_cycles",
            "duck_reset", "duck_step", "duck_randomize", "duck_physics_step"]
 
 
@@ -35,20 +36,35 @@ class DuckLayout(C.Structure):
         "rng_key", "rng_ctr", "step", "push_step", "push_interval", "imitation_i", "ep_steps", "nint")]
 
 
-def build(verbose: bool = False) -> str:
-    """Compile libduck.so for gfx950 with hipcc (in-tree, so it travels with the repo)."""
-    srcs = [os.path.join(CSRC, "duck_kernels.hip")]
+def build(verbose: bool = False, defines=(), out: str = None) -> str:
+    """Compile libduck.so for gfx950 with hipcc (in-tree, so it travels with the repo).
+
+    One translation unit per model variant (variant_*.hip) plus the C ABI (duck_capi.hip),
+    compiled in parallel and linked into one shared library."""
+    out = out or LIB_PATH
+    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
         [os.path.join(CSRC, "generated", f) for f in os.listdir(os.path.join(CSRC, "generated"))] + \
         [os.path.join(ROOT, "include", f) for f in ("duck.h", "duck_env.h", "duck_model.h")]
-    if os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= max(os.path.getmtime(d) for d in deps):
-        return LIB_PATH
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", LIB_PATH + ".tmp"] + srcs
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd, cwd=CSRC)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    if not defines and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
+        return out
+    import tempfile
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"] + [f"-D{d}" for d in defines]
+    with tempfile.TemporaryDirectory() as tmp:
+        objs, procs = [], []
+        for src in srcs:
+            obj = os.path.join(tmp, os.path.basename(src) + ".o")
+            cmd = ["hipcc"] + flags + ["-c", "-o", obj, src]
+            if verbose:
+                print(" ".join(cmd))
+            procs.append((src, subprocess.Popen(cmd, cwd=CSRC)))
+            objs.append(obj)
+        bad = [src for src, p in procs if p.wait() != 0]
+        if bad:
+            raise DuckError(f"hipcc failed on {bad}")
+        subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-shared", "-o", out + ".tmp"] + objs, cwd=CSRC)
+    os.replace(out + ".tmp", out)
+    return out
 
 
 _lib = None

@@ -600,6 +600,87 @@ static void collide_plane_convex(const oracle_model* m, oracle_data* d, int g1, 
   }
 }
 
+/* height field: elevation of MuJoCo's triangulated grid at (x, y) in the hfield frame (each
+ * cell split along its (0,0)-(1,1) diagonal; outside the grid the border cells extend) and
+ * the unit normal of that triangle. Row r <-> y, column c <-> x. */
+static double hfield_point(const oracle_model* m, double x, double y, double nrm[3]) {
+  const int nr = m->hfield_nrow, nc = m->hfield_ncol;
+  const double sx = m->hfield_size[0], sy = m->hfield_size[1], sz = m->hfield_size[2];
+  const double dx = 2.0 * sx / (nc - 1), dy = 2.0 * sy / (nr - 1);
+  const double fx = (x + sx) / dx, fy = (y + sy) / dy;
+  int c = (int)floor(fx), r = (int)floor(fy);
+  if (!(fx == fx)) c = 0;
+  if (!(fy == fy)) r = 0;
+  c = c < 0 ? 0 : (c > nc - 2 ? nc - 2 : c);
+  r = r < 0 ? 0 : (r > nr - 2 ? nr - 2 : r);
+  double u = fx - c, w = fy - r;
+  u = u < 0 ? 0 : (u > 1 ? 1 : u);
+  w = w < 0 ? 0 : (w > 1 ? 1 : w);
+  const double* h = m->hfield_data;
+  const double z00 = sz * h[r * nc + c], z10 = sz * h[r * nc + c + 1];
+  const double z01 = sz * h[(r + 1) * nc + c], z11 = sz * h[(r + 1) * nc + c + 1];
+  double z;
+  if (u >= w) {
+    z = z00 + u * (z10 - z00) + w * (z11 - z10);
+    nrm[0] = -(z10 - z00) * dy; nrm[1] = dx * (z10 - z11); nrm[2] = dx * dy;
+  } else {
+    z = z00 + w * (z01 - z00) + u * (z11 - z01);
+    nrm[0] = dy * (z01 - z11); nrm[1] = -dx * (z01 - z00); nrm[2] = dx * dy;
+  }
+  const double nn = norm3(nrm);
+  nrm[0] /= nn; nrm[1] /= nn; nrm[2] /= nn;
+  return z;
+}
+
+/* signed distance of world point vw to the terrain triangle plane under it; world normal */
+static double hfield_dist(const oracle_model* m, const double* hp, const double* HR, const double* vw, double nw[3]) {
+  double d[3] = {vw[0] - hp[0], vw[1] - hp[1], vw[2] - hp[2]}, pl[3], nl[3];
+  mulmtv3(pl, HR, d);
+  const double z = hfield_point(m, pl[0], pl[1], nl);
+  mulmv3(nw, HR, nl);
+  return (pl[2] - z) * nl[2];
+}
+
+/* height field (g1) vs convex hull (g2). Every hull vertex is measured against the terrain
+ * triangle under it; the 4 contacts are the plane-convex manifold (same masks and argmax
+ * rules) taken with the terrain normal under the deepest vertex, each contact carrying its
+ * own vertex's distance and triangle normal. Declared stand-in for mjx's prism
+ * decomposition; on a flat field it equals collide_plane_convex. */
+static void collide_hfield_convex(const oracle_model* m, oracle_data* d, int g1, int g2, int slot0) {
+  const double* hp = d->geom_xpos[g1];
+  const double* HR = d->geom_xmat[g1];
+  const double* cp = d->geom_xpos[g2];
+  const double* CR = d->geom_xmat[g2];
+  int nv = m->hull_nvert;
+  double support[DUCK_MAXHULLV], vw[DUCK_MAXHULLV][3], nw[DUCK_MAXHULLV][3];
+  double smax = -1e30;
+  for (int k = 0; k < nv; k++) {
+    mulmv3(vw[k], CR, m->hull_vert[k]);
+    for (int a = 0; a < 3; a++) vw[k][a] += cp[a];
+    support[k] = -hfield_dist(m, hp, HR, vw[k], nw[k]);
+    if (support[k] > smax) smax = support[k];
+  }
+  double thr = smax - 1e-3 > 0 ? smax - 1e-3 : 0;
+  int mask[DUCK_MAXHULLV];
+  for (int k = 0; k < nv; k++) mask[k] = support[k] > thr;
+  const int kd = argmax_tol(support, nv, 0.0);
+  double n_local[3];
+  mulmtv3(n_local, CR, nw[kd]);
+  int idx[4];
+  manifold_points((const double(*)[3])m->hull_vert, mask, nv, n_local, idx);
+  for (int c = 0; c < 4; c++) {
+    int k = idx[c], unique = 1;
+    for (int e = 0; e < c; e++)
+      if (idx[e] == k) unique = 0;
+    double dist = unique ? -support[k] : 1.0;
+    int s = slot0 + c;
+    for (int a = 0; a < 3; a++) d->con_pos[s][a] = vw[k][a] - 0.5 * dist * nw[k][a];
+    d->con_dist[s] = dist;
+    make_frame(d->con_frame[s], nw[k]);
+    d->con_geom1[s] = g1; d->con_geom2[s] = g2;
+  }
+}
+
 /* convex hull (g1) vs convex hull (g2): separating-axis test over face normals and edge
  * pairs; on overlap, a 4-point manifold against the reference face (or one edge-edge
  * point). Declared simplification of mjx's convex-convex clipping. */
@@ -719,9 +800,10 @@ static void collision(const oracle_model* m, oracle_data* d) {
     int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p], t1 = m->geom_type[g1], t2 = m->geom_type[g2];
     int s0 = p * DUCK_CON_PER_PAIR;
     if (t1 == DUCK_GEOM_PLANE && t2 == DUCK_GEOM_MESH) collide_plane_convex(m, d, g1, g2, s0);
+    else if (t1 == DUCK_GEOM_HFIELD && t2 == DUCK_GEOM_MESH && m->hfield_data) collide_hfield_convex(m, d, g1, g2, s0);
     else if (t1 == DUCK_GEOM_MESH && t2 == DUCK_GEOM_MESH) collide_convex_convex(m, d, g1, g2, s0);
     else
-      for (int c = 0; c < 4; c++) set_inactive(d, s0 + c, g1, g2); /* hfield: not yet supported */
+      for (int c = 0; c < 4; c++) set_inactive(d, s0 + c, g1, g2);
   }
 }
 

@@ -71,9 +71,11 @@ def test_autoreset_and_episode(gpu):
     assert torch.all(st.info["steps"] == 1)
 
 
-def test_domain_randomization_parity(gpu):
+@pytest.mark.parametrize("task", ["flat_terrain", "rough_terrain", "rough_terrain_backlash"])
+def test_domain_randomization_parity(task, gpu):
+    """C4 (rough + DR) and C5's per-GPU shard (rough + DR + backlash) against the oracle."""
     n = 48
-    env = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
+    env = Joystick(task, num_envs=n, device=gpu, use_imitation=False)
     dr = domain_randomize(env, rng=11)
     st = env.reset(rng=5)
     base = OracleModel(env.mj_model)

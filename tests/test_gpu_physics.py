@@ -52,7 +52,10 @@ def _run(task, n, nsub, seed, gpu, **kw):
     return m, g, ref
 
 
-@pytest.mark.parametrize("task", ["flat_terrain", "flat_terrain_backlash"])
+TASKS = ["flat_terrain", "flat_terrain_backlash", "rough_terrain", "rough_terrain_backlash"]
+
+
+@pytest.mark.parametrize("task", TASKS)
 def test_forward_parity(task, gpu):
     m, g, r = _run(task, 512, 0, seed=1, gpu=gpu)
     np.testing.assert_allclose(g["Mdense"], r["M"], rtol=1e-4, atol=2e-6)
@@ -70,7 +73,7 @@ def test_forward_parity(task, gpu):
     assert (rel[ok] < 2e-2).mean() > 0.97, np.sort(rel)[-10:]
 
 
-@pytest.mark.parametrize("task", ["flat_terrain", "flat_terrain_backlash"])
+@pytest.mark.parametrize("task", TASKS)
 def test_substep_parity(task, gpu):
     n = 512
     m, g, r = _run(task, n, 1, seed=2, gpu=gpu)

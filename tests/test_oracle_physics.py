@@ -119,3 +119,41 @@ def test_batch_equals_single_env(m, om):
             o, p, r, done = e.step(a[env_id])
         np.testing.assert_array_equal(b.obs[env_id], o)
         np.testing.assert_array_equal(b.rew[env_id], r)
+
+
+def test_flat_height_field_equals_plane(m, om):
+    """An all-zero height field collides exactly like the z = 0 plane (same robot, same qpos)."""
+    import copy
+    mr = copy.deepcopy(Model.load(constants.task_to_xml("rough_terrain")))
+    mr.arrays["hfield_data"] = np.zeros_like(mr.arrays["hfield_data"])
+    omr = OracleModel(mr)
+    rng = np.random.default_rng(3)
+    q0, ctrl = _home(m)
+    for trial in range(5):
+        q = q0.copy()
+        q[2] = 0.14 + 0.02 * trial
+        q[7:] += rng.uniform(-0.2, 0.2, m.nu)
+        d1 = om.new_data(qpos=q, qvel=np.zeros(m.nv), ctrl=ctrl)
+        d2 = omr.new_data(qpos=q, qvel=np.zeros(m.nv), ctrl=ctrl)
+        om.forward(d1)
+        omr.forward(d2)
+        dist1, dist2 = d1.arr("con_dist", 12), d2.arr("con_dist", 12)
+        np.testing.assert_allclose(dist2, dist1, atol=1e-12)
+        np.testing.assert_allclose(np.ctypeslib.as_array(d2.con_pos), np.ctypeslib.as_array(d1.con_pos), atol=1e-12)
+
+
+def test_height_field_contacts_follow_terrain():
+    """On the rough scene, feet at rest report contacts whose normals match the terrain slope."""
+    mr = Model.load(constants.task_to_xml("rough_terrain"))
+    omr = OracleModel(mr)
+    q, ctrl = _home(mr)
+    d = omr.new_data(qpos=q, qvel=np.zeros(mr.nv), ctrl=ctrl)
+    omr.step(d, 300)
+    dist = d.arr("con_dist", 12)
+    frames = np.ctypeslib.as_array(d.con_frame)[:12]
+    active = dist[4:] < 0.002
+    assert active.sum() >= 2
+    normals = frames[4:][active][:, :3]
+    np.testing.assert_allclose(np.linalg.norm(normals, axis=1), 1.0, atol=1e-9)
+    assert (normals[:, 2] > 0.99).all()  # 1 cm relief over 7.8 cm cells: gentle slopes
+    assert np.isfinite(d.arr("qpos", mr.nq)).all()

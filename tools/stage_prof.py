@@ -25,12 +25,12 @@ def main():
     torch.cuda.synchronize()
     buf = (C.c_ulonglong * 16)()
     lib = native.lib()
-    lib.duck_debug_stage_cycles(buf, 1)
+    lib.duck_debug_stage_cycles(env._sim, buf, 1)
     steps = 5
     for _ in range(steps):
         env.step(st, a)
     torch.cuda.synchronize()
-    lib.duck_debug_stage_cycles(buf, 1)
+    lib.duck_debug_stage_cycles(env._sim, buf, 1)
     tot = sum(buf[k] for k in range(9))
     nwg = (n + 15) // 16
     for k, name in enumerate(NAMES):
