@@ -34,10 +34,18 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from open_duck_playground_amd.joystick import Joystick, wrap_for_brax_training  # noqa: E402
+from open_duck_playground_amd.joystick import Joystick, domain_randomize, wrap_for_brax_training  # noqa: E402
 from open_duck_playground_amd.sharding import shard_from_env  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# BASELINE.json configs[1..4] (configs[0] is the reference's 1-env CPU plumbing case)
+CONFIGS = {
+    "C2": dict(task="flat_terrain", imitation=False, dr=False, envs=4096),
+    "C3": dict(task="flat_terrain", imitation=True, dr=False, envs=4096),
+    "C4": dict(task="rough_terrain", imitation=False, dr=True, envs=8192),
+    "C5": dict(task="rough_terrain_backlash", imitation=False, dr=True, envs=4096),  # 32768 over 8 GPUs
+}
 
 
 def algorithmic_bytes(env: Joystick) -> int:
@@ -86,7 +94,8 @@ def cpu_baseline(task: str, use_imitation: bool, budget_s: float, threads: int):
         if el >= budget_s:
             break
     return {"value": n * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{task}, {n} envs x {steps} env-steps ({el:.1f} s), fp64 oracle, OpenMP {threads} threads"}
+            "sample": f"{task} (nominal model), {n} envs x {steps} env-steps ({el:.1f} s), fp64 oracle, "
+                      f"OpenMP {threads} threads"}
 
 
 def main():
@@ -94,9 +103,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
-    ap.add_argument("--task", default="flat_terrain")
-    ap.add_argument("--imitation", action="store_true")
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
+                    help="BASELINE.json workload: C2 flat (the metric), C3 +imitation, C4 rough+DR, C5 rough+DR+backlash")
+    ap.add_argument("--envs", type=int, default=0, help="envs per GPU (0 = the config's)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline sampling (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
     args = ap.parse_args()
@@ -113,10 +122,11 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
-    n = args.envs
+    cfg = CONFIGS[args.config]
+    n = args.envs or cfg["envs"]
     shard = shard_from_env(n)
-    env = Joystick(args.task, num_envs=n, device=dev, use_imitation=args.imitation, env_offset=shard.env_offset)
-    env = wrap_for_brax_training(env, episode_length=1000)
+    env = Joystick(cfg["task"], num_envs=n, device=dev, use_imitation=cfg["imitation"], env_offset=shard.env_offset)
+    env = wrap_for_brax_training(env, episode_length=1000, randomization_fn=domain_randomize if cfg["dr"] else None)
     state = env.reset(rng=0)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -150,7 +160,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         thr = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        cpu = cpu_baseline(args.task, args.imitation, args.cpu_budget, thr)
+        cpu = cpu_baseline(cfg["task"], cfg["imitation"], args.cpu_budget, thr)
 
     if rank == 0:
         B = algorithmic_bytes(env)
@@ -161,8 +171,9 @@ def main():
             "value": total / el, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
             "ms_per_step": el / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (keyframe home + reset randomisation, actions U(-1,1)^14)",
-            "config": {"workload": f"C2: {args.task}, {'imitation' if args.imitation else 'no imitation'}, "
-                                   f"{n} envs per GPU, episode_length 1000 + auto-reset",
+            "config": {"workload": f"{args.config}: {cfg['task']}, {'imitation' if cfg['imitation'] else 'no imitation'}"
+                                   f"{', domain randomization' if cfg['dr'] else ''}, {n} envs per GPU, "
+                                   "episode_length 1000 + auto-reset",
                        "envs_per_gpu": n, "total_envs": world * n, "substeps": env.n_substeps,
                        "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
