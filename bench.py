@@ -162,6 +162,12 @@ def main():
         thr = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         cpu = cpu_baseline(cfg["task"], cfg["imitation"], args.cpu_budget, thr)
 
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tpath):  # PMC bytes per launch from the committed rocprofv3 run of this config
+        t = json.load(open(tpath)).get(args.config)
+        if t and n == CONFIGS[args.config]["envs"]:
+            traffic = t["bytes_per_launch"]
     if rank == 0:
         B = algorithmic_bytes(env)
         achieved = B * n / (kern_ms * 1e-3) / 1e9
@@ -177,7 +183,7 @@ def main():
                        "envs_per_gpu": n, "total_envs": world * n, "substeps": env.n_substeps,
                        "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "step_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": B},
             "cpu_baseline": cpu,
             "finite": ok,
