@@ -116,6 +116,22 @@ def sparse_code(m: Model, adr) -> str:
     return "".join(o)
 
 
+def chain_of(m: Model, b: int):
+    """dof ancestors of body b (its weld body's dofs and above), increasing"""
+    wb = m.body_weldid[b]
+    c = []
+    if wb > 0:
+        j = m.body_dofadr[wb] + m.body_dofnum[wb] - 1
+        while j >= 0:
+            c.append(int(j))
+            j = m.dof_parentid[j]
+    return sorted(c)
+
+
+def maxchain_of(m: Model):
+    return max(len(chain_of(m, b)) for b in range(m.nbody))
+
+
 def team_tables(m: Model, rows, adr, pre: str, floor: int):
     """Index tables for the team (16 lanes per env) kernel: lanes pick their work items
     (bodies of a tree level, mass-matrix entries, LDL updates) from these."""
@@ -204,13 +220,85 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     br_arr = np.full((len(branches), brlen), -1)
     for i, b in enumerate(branches):
         br_arr[i, :len(b)] = b
+    # ---- model blob: lane-indexed tables and per-row constraint records, copied into LDS
+    # once per launch (int32 words; floats bit-cast) ----
+    dt = float(m.opt_timestep)
+
+    def kbi64(solref, solimp, pos):
+        tc = max(float(solref[0]), 2.0 * dt)
+        dr = float(solref[1])
+        dmin = min(max(float(solimp[0]), 1e-4), 0.9999)
+        dmax = min(max(float(solimp[1]), 1e-4), 0.9999)
+        width = max(1e-15, float(solimp[2]))
+        mid = min(max(float(solimp[3]), 1e-4), 0.9999)
+        power = max(1.0, float(solimp[4]))
+        k = 1.0 / (dmax * dmax * tc * tc * dr * dr)
+        b = 2.0 / (dmax * tc)
+        x = abs(pos) / width
+        if x < mid:
+            y = (1.0 / mid ** (power - 1)) * x ** power
+        else:
+            y = 1 - (1.0 / (1 - mid) ** (power - 1)) * (1 - x) ** power
+        imp = min(max(dmin + y * (dmax - dmin), dmin), dmax)
+        imp = dmax if x > 1.0 else imp
+        return k, b, imp
+
+    f2i = lambda x: int(np.float32(x).view(np.int32))
+    blob, boff = [], {}
+
+    def put(name, words):
+        boff[name] = len(blob)
+        blob.extend(int(w) for w in words)
+
+    put("madr", full.reshape(-1))
+    put("mi", mi)
+    put("mj", mj)
+    put("desc", desc.reshape(-1))
+    fric = [i for i in range(nv) if m.dof_frictionloss[i] > 0]
+    rec = []
+    for i in fric:
+        k_, b_, imp = kbi64(m.dof_solref[i], m.dof_solimp[i], 0.0)
+        R = max(float(m.dof_invweight0[i]) * (1 - imp) / imp, 1e-15)
+        rec += [i, f2i(1.0 / R), f2i(b_)]
+    put("fric", rec)  # stride 3: dof, D, b
+    lim = [j for j in range(m.njnt) if m.jnt_limited[j]]
+    rec = []
+    for j in lim:
+        k_, b_, _ = kbi64(m.jnt_solref[j], m.jnt_solimp[j], 0.0)
+        si = m.jnt_solimp[j]
+        rec += [m.jnt_dofadr[j], m.jnt_qposadr[j], f2i(m.jnt_range[j][0]), f2i(m.jnt_range[j][1]),
+                f2i(m.jnt_margin[j]), f2i(k_), f2i(b_), f2i(m.dof_invweight0[m.jnt_dofadr[j]])] + [f2i(x) for x in si]
+    put("lim", rec)  # stride 13: dof, qadr, lo, hi, margin, k, b, invweight, solimp[5]
+    slot_of = lambda g: 0 if g == floor else (1 if g == m.id("geom", "left_foot_bottom_tpu") else 2)
+    cbody = [m.geom_bodyid[g] for g in (floor, m.id("geom", "left_foot_bottom_tpu"), m.id("geom", "right_foot_bottom_tpu"))]
+    rec = []
+    for p in range(m.npair):
+        s1, s2 = slot_of(m.pair_geom1[p]), slot_of(m.pair_geom2[p])
+        tran = float(m.body_invweight0[cbody[s1]][0] + m.body_invweight0[cbody[s2]][0])
+        mu = float(m.pair_friction[p][0])
+        iw = (tran + mu * mu * tran) * 2.0 * mu * mu / float(m.opt_impratio)
+        k_, b_, _ = kbi64(m.pair_solref[p], m.pair_solimp[p], 0.0)
+        rec += [s1, s2, f2i(mu), f2i(iw), f2i(m.pair_margin[p]), f2i(k_), f2i(b_), 0] + \
+            [f2i(x) for x in m.pair_solimp[p]]
+    put("pair", rec)  # stride 13: s1, s2, mu, iw, margin, k, b, pad, solimp[5]
+    for name, g in (("chainl", "left_foot_bottom_tpu"), ("chainr", "right_foot_bottom_tpu")):
+        c = chain_of(m, m.geom_bodyid[m.id("geom", g)])
+        put(name, c + [-1] * (maxchain_of(m) - len(c)))
+    put("hull", [f2i(x) for x in np.asarray(m.hulls[0].vert, dtype=np.float64).reshape(-1)])
+    d2f, d2l = [-1] * nv, [-1] * nv
+    for r, i in enumerate(fric):
+        d2f[i] = r
+    for r, j in enumerate(lim):
+        d2l[m.jnt_dofadr[j]] = r
+    put("dof2fric", d2f)
+    put("dof2lim", d2l)
     T = lambda name, a, t: f"__device__ const {t} {pre}_{name}{''.join(f'[{d}]' for d in np.shape(a))} = " + \
         _arr("x", np.asarray(a), t).split("= ", 1)[1]
     tabs = {"lev": (lev, "int"), "child": (child, "int"), "madr": (full, "int"), "mi": (mi, "int"), "mj": (mj, "int"),
             "ldl": (np.array(ldl).reshape(-1, 3), "int"), "ldl_off": (ldl_off, "int"), "anc_dof": (anc_dof, "int"),
             "anc_adr": (anc_adr, "int"), "anc_off": (anc_off, "int"),
             "ldlp": (np.array(ldlp), "int"), "ancp": (np.array(ancp), "int"), "br": (br_arr, "int"),
-            "desc": (desc, "int")}
+            "desc": (desc, "int"), "blob": (np.array(blob, dtype=np.int64), "int")}
     dev = [T(k, a, t) for k, (a, t) in tabs.items()]
     acc = [f"  static constexpr int T_NLEV = {nlev}, T_LEVW = {levw}, T_MAXCH = {maxch};\n",
            f"  static constexpr int T_MAXLDL = {max(ldl_off[k + 1] - ldl_off[k] for k in range(nv))}, "
@@ -222,7 +310,9 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
            _arr("T_ANC_NR", anc_nr, "int"), _arr("T_ANC_RB", anc_rb, "int"),
            _arr("T_DIAG", [adr[i, i] for i in range(nv)], "int"),
            f"  static constexpr int T_NROOT = {len(root)}, T_NBR = {len(branches)}, T_BRLEN = {brlen};\n",
-           _arr("T_ROOT", root, "int")]
+           _arr("T_ROOT", root, "int"),
+           f"  static constexpr int NBLOB = {len(blob)};\n",
+           "".join(f"  static constexpr int B_{k.upper()} = {v};\n" for k, v in boff.items())]
     for k, (a, t) in tabs.items():
         shp = np.shape(a)
         if len(shp) == 1:

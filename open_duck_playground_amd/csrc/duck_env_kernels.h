@@ -272,6 +272,12 @@ DK void write_obs(const KArgs& A, int e, Slice<WG> L, const Rng& r, int slot_bas
 template <class Md, int WG>
 __global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
   using Ly = Lay<Md>;
+#if DUCK_TEAM
+  {
+    extern __shared__ float lds_t[];
+    load_model_tables<Md>(lds_t);
+  }
+#endif
   int lane;
   const int t = local_env(lane);
   if (t < 0) return;
@@ -337,6 +343,12 @@ __global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
 template <class Md, int WG>
 __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   using Ly = Lay<Md>;
+#if DUCK_TEAM
+  {
+    extern __shared__ float lds_t[];
+    load_model_tables<Md>(lds_t);
+  }
+#endif
   int lane;
   const int t = local_env(lane);
   if (t < 0) return;
@@ -528,6 +540,12 @@ template <class Md, int WG>
 __global__ void __launch_bounds__(TPB) physics_kernel(KArgs A, float* qpos_g, float* qvel_g, float* warm_g,
                                                      const float* ctrl_g, int nsub, float* aux) {
   using Ly = Lay<Md>;
+#if DUCK_TEAM
+  {
+    extern __shared__ float lds_t[];
+    load_model_tables<Md>(lds_t);
+  }
+#endif
   int lane;
   const int t = local_env(lane);
   if (t < 0) return;
@@ -613,7 +631,8 @@ static bool matches(const duck_model_desc* m) {
 template <class Md>
 static size_t lds_bytes() {
 #if DUCK_TEAM
-  return (size_t)TLay<Md>::STRIDE * WG * sizeof(float);
+  static_assert(WG == TEAM_WG, "team workgroup size");
+  return (size_t)TLay<Md>::LDS_FLOATS * sizeof(float);
 #else
   return (size_t)Lay<Md>::TOTAL * WG * sizeof(float);
 #endif

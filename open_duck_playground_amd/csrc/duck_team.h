@@ -17,6 +17,25 @@
 #include "duck_physics.h"
 
 constexpr int TEAM = 16;
+constexpr int TEAM_WG = 16;  // envs (teams) per workgroup: 256 threads = 4 waves
+typedef __attribute__((address_space(3))) int lds_int;
+
+// impedance of a constraint at violation pos (mjx constraint._kbi, imp part)
+DK float imp_of(const float* solimp, float pos) {
+  const float dmin = fminf(fmaxf(solimp[0], 0.0001f), 0.9999f), dmax = fminf(fmaxf(solimp[1], 0.0001f), 0.9999f);
+  const float width = fmaxf(1e-15f, solimp[2]), mid = fminf(fmaxf(solimp[3], 0.0001f), 0.9999f);
+  const float power = fmaxf(1.0f, solimp[4]);
+  const float x = fabsf(pos) / width;
+  float y;
+  if (power == 2.0f) {
+    y = x < mid ? (1.0f / mid) * x * x : 1.0f - (1.0f / (1.0f - mid)) * (1.0f - x) * (1.0f - x);
+  } else {
+    y = x < mid ? (1.0f / powf(mid, power - 1.0f)) * powf(x, power)
+                : 1.0f - (1.0f / powf(1.0f - mid, power - 1.0f)) * powf(1.0f - x, power);
+  }
+  const float im = fminf(fmaxf(dmin + y * (dmax - dmin), dmin), dmax);
+  return x > 1.0f ? dmax : im;
+}
 
 #define TSYNC()                           \
   do {                                    \
@@ -64,8 +83,23 @@ struct TLay {
   static constexpr int STRIDE = ((USED + 15) / 32) * 32 + 16;  // = 16 (mod 32), >= USED
   static_assert(STRIDE >= USED && STRIDE % 32 == 16, "stride");
   static constexpr int FTMP = Ly::JA;                  // crb: F_i = I_b cdof_i (dead row storage)
+  // the model blob (lane-indexed tables, constraint-row records) follows the env slices in
+  // LDS when it fits, else it is read from global memory
+  static constexpr int TAB = STRIDE * TEAM_WG;
+  static constexpr bool TAB_LDS = (size_t)(TAB + Md::NBLOB) * 4 <= 160 * 1024;
+  static constexpr int LDS_FLOATS = TAB + (TAB_LDS ? Md::NBLOB : 0);
   static_assert(6 * Md::NV <= 4 * Ly::NROW, "crb scratch must fit in the row storage");
 };
+
+// copy the model blob into the workgroup's LDS (before any thread of the block exits)
+template <class Md>
+DK void load_model_tables(float* lds) {
+  if constexpr (TLay<Md>::TAB_LDS) {
+    int* dst = (int*)(lds + TLay<Md>::TAB);
+    for (int i = threadIdx.x; i < Md::NBLOB; i += blockDim.x) dst[i] = Md::t_blob()[i];
+    __syncthreads();
+  }
+}
 
 template <class Md>
 struct TPhys {
@@ -77,6 +111,20 @@ struct TPhys {
   static constexpr int NV = Md::NV, NB = Md::NB, NQ = Md::NQ, NU = Md::NU, NJ = Md::NJ;
   static constexpr int NCON = Ly::NCON, NFRIC = Md::NFRIC, NLIM = Md::NLIM, NROW = Ly::NROW;
   static constexpr int R_LIM = Ly::R_LIM, R_CON = Ly::R_CON;
+  static DK int ti(int off) {
+    if constexpr (TL::TAB_LDS) {
+      extern __shared__ float lds_dyn[];
+      return ((lds_int*)(lds_dyn + TL::TAB))[off];
+    } else {
+      return Md::t_blob()[off];
+    }
+  }
+  static DK float tf(int off) { return __int_as_float(ti(off)); }
+  static constexpr int LIMW = 13, PAIRW = 13;
+  static DK int fric_dof(int r) { return ti(Md::B_FRIC + 3 * r); }
+  static DK int lim_dof(int r) { return ti(Md::B_LIM + LIMW * r); }
+  static DK int madr(int i, int j) { return ti(Md::B_MADR + NV * i + j); }
+
   static_assert(NFRIC <= TEAM, "one friction row per lane");
   static_assert(NCON <= TEAM, "one contact slot per lane");
   static_assert(NU <= TEAM, "one actuator per lane");
@@ -349,13 +397,12 @@ struct TPhys {
       for (int k = 0; k < 6; k++) L[TL::FTMP + 6 * i + k] = buf[k];
     }
     TSYNC();
-    const int* MI = Md::t_mi();
-    const int* MJ = Md::t_mj();
+
 #pragma unroll
     for (int a0 = 0; a0 < Md::NM; a0 += TEAM) {
       const int a = a0 + lane;
       if (a < Md::NM) {
-        const int i = MI[a], j = MJ[a];
+        const int i = ti(Md::B_MI + a), j = ti(Md::B_MJ + a);
         float s = 0.0f;
         for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * j + k] * L[TL::FTMP + 6 * i + k];
         if (i == j) s += L[Ly::DARM + i];
@@ -420,7 +467,7 @@ struct TPhys {
     }
   }
 
-  static DK int diag_adr(int i) { return Md::t_madr()[i][i]; }
+  static DK int diag_adr(int i) { return madr(i, i); }
 
   // DST = sign * H^-1 SRC with H factored in place (mj_solveLD)
   static DK void solve_H(LP L, int lane, int SRC, int DST, float sign) {
@@ -519,38 +566,180 @@ struct TPhys {
     (sol_fwd<J>(F, x, lane), ...);
   }
 
-  // DST = sign * A^-1 SRC for the tree-sparse SPD matrix A stored at HOFF (M_adr pattern)
-  static DK void solve_regs(LP L, int lane, int HOFF, int SRC, int DST, float sign) {
-    Fac F;
-    const int(*MA)[NV] = Md::t_madr();
+  // factor F.col in place and solve for x (lane l holds x[l], x[l+16]); F.desc must be set
+  static DK void factor_solve(Fac& F, float* x, int lane) {
 #pragma unroll
-    for (int s = 0; s < NC; s++) {
-      const int c = TEAM * s + lane;
-      F.desc[s] = c < NV ? (unsigned)Md::t_desc()[s][lane] : 0u;
-      F.dg[s] = 1.0f;
-#pragma unroll
-      for (int r = 0; r < NV; r++) {
-        const int a = (c < NV && r >= c) ? MA[r][c < NV ? c : 0] : -1;
-        F.col[s][r] = a >= 0 ? L[HOFF + a] : 0.0f;
-      }
-    }
+    for (int s = 0; s < NC; s++) F.dg[s] = 1.0f;
     fac_all(F, lane, std::make_integer_sequence<int, NV>{});
-    float x[NC];
-#pragma unroll
-    for (int s = 0; s < NC; s++) {
-      const int c = TEAM * s + lane;
-      x[s] = c < NV ? L[SRC + c] : 0.0f;
-    }
     back_all(F, x, std::make_integer_sequence<int, NV>{});
 #pragma unroll
     for (int s = 0; s < NC; s++) x[s] = x[s] / F.dg[s];
     fwd_all(F, x, lane, std::make_integer_sequence<int, NV>{});
+  }
+  static DK void set_desc(Fac& F, int lane) {
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane;
+      F.desc[s] = c < NV ? (unsigned)ti(Md::B_DESC + TEAM * s + lane) : 0u;
+    }
+  }
+  // columns of the symmetric tree-sparse matrix at HOFF: full (both triangles) or lower only
+  static DK void load_cols(LP L, int lane, int HOFF, float (*col)[NV], bool lower_only) {
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane, cc = c < NV ? c : 0;
+#pragma unroll
+      for (int r = 0; r < NV; r++) {
+        const int a = madr(r, cc);
+        const float v = L[HOFF + (a >= 0 ? a : 0)];  // unconditional load: no branch per entry
+        col[s][r] = (c < NV && a >= 0 && (!lower_only || r >= c)) ? v : 0.0f;
+      }
+    }
+  }
+
+  // DST = sign * A^-1 SRC for the tree-sparse SPD matrix A stored at HOFF (M_adr pattern)
+  static DK void solve_regs(LP L, int lane, int HOFF, int SRC, int DST, float sign) {
+    Fac F;
+    set_desc(F, lane);
+    load_cols(L, lane, HOFF, F.col, true);
+    float x[NC];
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane;
+      const float v = L[SRC + (c < NV ? c : 0)];
+      x[s] = c < NV ? v : 0.0f;
+    }
+    factor_solve(F, x, lane);
 #pragma unroll
     for (int s = 0; s < NC; s++) {
       const int c = TEAM * s + lane;
       if (c < NV) L[DST + c] = sign * x[s];
     }
     TSYNC();
+  }
+
+  // y = M x for the lane's columns (M held as full columns, x read by broadcast); Y[c] = y
+  static DK void mul_cols(LP L, int lane, const float (*Mc)[NV], int X, int Y) {
+    float y[NC];
+#pragma unroll
+    for (int s = 0; s < NC; s++) y[s] = 0.0f;
+#pragma unroll
+    for (int r = 0; r < NV; r++) {
+      const float xr = L[X + r];
+#pragma unroll
+      for (int s = 0; s < NC; s++) y[s] += Mc[s][r] * xr;
+    }
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane;
+      if (c < NV) L[Y + c] = y[s];
+    }
+  }
+
+  static constexpr unsigned chain_mask(int b) {
+    unsigned msk = 0;
+    for (int q = 0; q < Md::chain_len[b]; q++) msk |= 1u << Md::chain[b][q];
+    return msk;
+  }
+
+  // Newton direction at (QACC, JA, MA) with H = M + J'DJ assembled directly into register
+  // columns (mjx _update_gradient + the Cholesky solve): SRCH = -H^-1 grad. Returns false
+  // (nothing written) when foot/foot contact rows are active.
+  static DK bool newton_fused(LP L, int lane, const float (*Mc)[NV]) {
+    if (Md::FOOT_PAIR >= 0) {
+      const int row = R_CON + 16 * Md::FOOT_PAIR + lane;
+      const float act = (L[Ly::JA + row] < 0.0f && L[Ly::RD + row] != 0.0f) ? 1.0f : 0.0f;
+      if (tsum(act) > 0.0f) return false;
+    }
+    Fac F;
+    set_desc(F, lane);
+    float g[NC];
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane, cc = c < NV ? c : 0;
+      const bool valid = c < NV;
+      float gr = L[Ly::MA + cc] - L[Ly::FSM + cc], diag = 0.0f;
+      // friction row of dof c (Huber cost): force and quadratic-zone curvature
+      const int fr = ti(Md::B_DOF2FRIC + cc), frc = fr >= 0 ? fr : 0;
+      {
+        const float D = L[Ly::RD + frc], x = L[Ly::JA + frc], f = L[Ly::DFRIC + cc], rf = f / D;
+        const float force = x <= -rf ? f : (x >= rf ? -f : -D * x);
+        const bool quad = x > -rf && x < rf;
+        gr -= fr >= 0 ? force : 0.0f;
+        diag += (fr >= 0 && quad) ? D : 0.0f;
+      }
+      // joint-limit row of dof c (one-sided)
+      const int lr = ti(Md::B_DOF2LIM + cc), lrc = lr >= 0 ? lr : 0;
+      {
+        const float D = L[Ly::RD + R_LIM + lrc], x = L[Ly::JA + R_LIM + lrc], sg = L[Ly::LSGN + lrc];
+        const bool act = lr >= 0 && x < 0.0f;
+        gr -= act ? sg * (-D * x) : 0.0f;
+        diag += act ? D : 0.0f;
+      }
+      g[s] = valid ? gr : 0.0f;
+#pragma unroll
+      for (int r = 0; r < NV; r++) F.col[s][r] = (r >= c) ? Mc[s][r] + (r == c ? diag : 0.0f) : 0.0f;
+    }
+    // contact rows of each floor pair: per-foot 6x6 J'DJ block and J'force, by team sums
+#pragma unroll
+    for (int side = 0; side < 2; side++) {
+      const int p = Md::PLANE_PAIR[side];
+      const int foot = cgeom_slot<Md>(Md::pair_geom2[p]);  // 1 left, 2 right
+      const float mu = tf(Md::B_PAIR + PAIRW * p + 2);
+      const int slot = 4 * p + (lane >> 2), e = lane & 3, row = R_CON + 4 * slot + e;
+      const float D = L[Ly::RD + row], x = L[Ly::JA + row];
+      const float w = (x < 0.0f && D != 0.0f) ? D : 0.0f;
+      const float force = -w * x;
+      const int t = 1 + (e >> 1);
+      const float sg = (e & 1) ? -mu : mu;
+      float u[3], r3[3], a[6];
+      for (int q = 0; q < 3; q++) {
+        u[q] = L[Ly::CFR + 9 * slot + q] + sg * L[Ly::CFR + 9 * slot + 3 * t + q];
+        r3[q] = L[Ly::CR + 3 * slot + q];
+      }
+      cross3(a, r3, u);
+      a[3] = u[0]; a[4] = u[1]; a[5] = u[2];
+      float K[21], Fv[6];
+      {
+        int o = 0;
+        for (int q = 0; q < 6; q++)
+          for (int kk = q; kk < 6; kk++) { K[o] = tsum(w * a[q] * a[kk]); o++; }
+        for (int q = 0; q < 6; q++) Fv[q] = tsum(force * a[q]);
+      }
+      constexpr unsigned MASKL = chain_mask(Md::LFOOT_BODY), MASKR = chain_mask(Md::RFOOT_BODY);
+      const unsigned msk = foot == 1 ? MASKL : MASKR;
+#pragma unroll
+      for (int s = 0; s < NC; s++) {
+        const int c = TEAM * s + lane, cc = c < NV ? c : 0;
+        const bool in = c < NV && ((msk >> cc) & 1u);
+        float cdc[6], kc[6];
+        for (int k = 0; k < 6; k++) cdc[k] = L[Ly::CDOF + 6 * cc + k];
+        float gf = 0.0f;
+        for (int q = 0; q < 6; q++) {
+          float sacc = 0.0f;
+          for (int k = 0; k < 6; k++) sacc += K[kidx(q, k)] * cdc[k];
+          kc[q] = in ? sacc : 0.0f;
+          gf += cdc[q] * Fv[q];
+        }
+        g[s] -= in ? gf : 0.0f;
+        // H[r][c] += cdof_r . K cdof_c for chain rows r >= c (kc = 0 off the chain)
+#pragma unroll
+        for (int r = 0; r < NV; r++) {
+          if (!((msk >> r) & 1u)) continue;  // compile-time after unrolling: chain rows only
+          float h = 0.0f;
+          for (int k = 0; k < 6; k++) h += L[Ly::CDOF + 6 * r + k] * kc[k];
+          F.col[s][r] += r >= c ? h : 0.0f;
+        }
+      }
+    }
+    factor_solve(F, g, lane);
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane;
+      if (c < NV) L[Ly::SRCH + c] = -g[s];
+    }
+    TSYNC();
+    return true;
   }
 
   // ---------------- collision ----------------
@@ -604,7 +793,7 @@ struct TPhys {
     float pl[3], nl[3];
     mulmtv3(pl, CR, dif);
     mulmtv3(nl, CR, n);
-    const float(*HV)[3] = Md::hull_vert_d();
+    auto HVf = [&](int k, int q) { return tf(Md::B_HULL + 3 * k + q); };
     // this lane's vertices: k = sub + 8r
     constexpr int R = (NH + 7) / 8;
     float sup[R], vx[R], vy[R], vz[R];
@@ -612,7 +801,7 @@ struct TPhys {
     for (int r = 0; r < R; r++) {
       const int k = sub + 8 * r;
       const bool ok = k < NH;
-      vx[r] = ok ? HV[k][0] : 0.0f; vy[r] = ok ? HV[k][1] : 0.0f; vz[r] = ok ? HV[k][2] : 0.0f;
+      vx[r] = ok ? HVf(k, 0) : 0.0f; vy[r] = ok ? HVf(k, 1) : 0.0f; vz[r] = ok ? HVf(k, 2) : 0.0f;
       if constexpr (Md::FLOOR_TYPE == 0) {
         sup[r] = ok ? (pl[0] - vx[r]) * nl[0] + (pl[1] - vy[r]) * nl[1] + (pl[2] - vz[r]) * nl[2] : -1e30f;
       } else {
@@ -641,7 +830,7 @@ struct TPhys {
       best = hmin8i(best);
       return best < NH ? best : NH - 1;  // argmax_tol's default (also for NaN data)
     };
-    auto vert = [&](int k, float* o) { o[0] = HV[k][0]; o[1] = HV[k][1]; o[2] = HV[k][2]; };
+    auto vert = [&](int k, float* o) { o[0] = HVf(k, 0); o[1] = HVf(k, 1); o[2] = HVf(k, 2); };
     if constexpr (Md::FLOOR_TYPE == 1) {
       // manifold plane: the terrain normal under the deepest vertex, in the hull frame
       const int kd = argmax(sup, 0.0f);
@@ -757,44 +946,37 @@ struct TPhys {
 
   // ---------------- constraint rows ----------------
   static DK void make_rows(LP L, int lane) {
-    const float dt = Md::timestep;
-    S1 Ls{L};
     if (lane < NFRIC) {
-      const int r = lane, i = Md::fric_dof[r];
-      float k, b, imp;
-      kbi(Md::dof_solref[i], Md::dof_solimp[i], 0.0f, dt, k, b, imp);
-      const float R = fmaxf(Md::dof_invweight0[i] * (1.0f - imp) / imp, 1e-15f);
-      L[Ly::RD + r] = 1.0f / R;
-      L[Ly::AREF + r] = -b * L[Ly::QVEL + i];
+      const int r = lane, i = fric_dof(r);
+      L[Ly::RD + r] = tf(Md::B_FRIC + 3 * r + 1);
+      L[Ly::AREF + r] = -tf(Md::B_FRIC + 3 * r + 2) * L[Ly::QVEL + i];
     }
     for (int r = lane; r < NLIM; r += TEAM) {
-      const int j = Md::lim_jnt[r], i = Md::jnt_dofadr[j];
-      const float q = L[Ly::QPOS + Md::jnt_qposadr[j]];
-      const float dlo = q - Md::jnt_range[j][0], dhi = Md::jnt_range[j][1] - q;
-      const float pos = fminf(dlo, dhi) - Md::jnt_margin[j];
+      const int o = Md::B_LIM + LIMW * r;
+      const int i = ti(o), qa = ti(o + 1);
+      const float q = L[Ly::QPOS + qa];
+      const float dlo = q - tf(o + 2), dhi = tf(o + 3) - q;
+      const float pos = fminf(dlo, dhi) - tf(o + 4);
       const float sgn = dlo < dhi ? 1.0f : -1.0f;
-      float k, b, imp;
-      kbi(Md::jnt_solref[j], Md::jnt_solimp[j], pos, dt, k, b, imp);
-      const float R = fmaxf(Md::dof_invweight0[i] * (1.0f - imp) / imp, 1e-15f);
+      const float k = tf(o + 5), b = tf(o + 6);
+      const float si[5] = {tf(o + 8), tf(o + 9), tf(o + 10), tf(o + 11), tf(o + 12)};
+      const float imp = imp_of(si, pos);
+      const float R = fmaxf(tf(o + 7) * (1.0f - imp) / imp, 1e-15f);
       const bool active = pos < 0.0f;
       L[Ly::RD + R_LIM + r] = active ? 1.0f / R : 0.0f;
       L[Ly::AREF + R_LIM + r] = active ? (-b * sgn * L[Ly::QVEL + i] - k * imp * pos) : 0.0f;
       L[Ly::LSGN + r] = sgn;
     }
     if (lane < NCON) {
-      const int slot = lane, p = slot >> 2;
+      const int slot = lane, p = slot >> 2, o = Md::B_PAIR + PAIRW * p;
       float SL[6], SR[6];
       for (int k = 0; k < 6; k++) { SL[k] = L[Ly::CVEL + 6 * Md::LFOOT_BODY + k]; SR[k] = L[Ly::CVEL + 6 * Md::RFOOT_BODY + k]; }
-      const int s1 = cgeom_slot<Md>(Md::pair_geom1[p]), s2 = cgeom_slot<Md>(Md::pair_geom2[p]);
-      const int b1 = Md::cgeom_body[s1], b2 = Md::cgeom_body[s2];
-      const float tran = Md::body_invweight0[b1][0] + Md::body_invweight0[b2][0];
-      const float mu = Md::pair_friction[p][0];
-      const float iw = (tran + mu * mu * tran) * 2.0f * mu * mu / Md::impratio;
-      const float pos = L[Ly::CDIST + slot] - Md::pair_margin[p];
+      const float pos = L[Ly::CDIST + slot] - tf(o + 4);
       const bool active = pos < 0.0f;
-      float k, b, imp;
-      kbi(Md::pair_solref[p], Md::pair_solimp[p], pos, dt, k, b, imp);
-      const float R = fmaxf(iw * (1.0f - imp) / imp, 1e-15f);
+      const float k = tf(o + 5), b = tf(o + 6);
+      const float si[5] = {tf(o + 8), tf(o + 9), tf(o + 10), tf(o + 11), tf(o + 12)};
+      const float imp = imp_of(si, pos);
+      const float R = fmaxf(tf(o + 3) * (1.0f - imp) / imp, 1e-15f);
       float vel[4];
       contact_jx(L, p, slot, SL, SR, vel);
       for (int e = 0; e < 4; e++) {
@@ -808,8 +990,9 @@ struct TPhys {
 
   // J.x of one contact slot (4 pyramid edges) for body spatial motions SL/SR (runtime pair)
   static DK void contact_jx(LP L, int p, int slot, const float* SL, const float* SR, float* out4) {
-    const int s1 = cgeom_slot<Md>(Md::pair_geom1[p]), s2 = cgeom_slot<Md>(Md::pair_geom2[p]);
-    const float mu = Md::pair_friction[p][0];
+    const int o = Md::B_PAIR + PAIRW * p;
+    const int s1 = ti(o), s2 = ti(o + 1);
+    const float mu = tf(o + 2);
     const float r[3] = {L[Ly::CR + 3 * slot], L[Ly::CR + 3 * slot + 1], L[Ly::CR + 3 * slot + 2]};
     float v[3] = {0.0f, 0.0f, 0.0f}, t[3];
     if (s2 != 0) { P1::contact_vel(s2 == 1 ? SL : SR, r, t); v[0] += t[0]; v[1] += t[1]; v[2] += t[2]; }
@@ -830,20 +1013,22 @@ struct TPhys {
     // foot spatial motions: lanes 0-5 left, 6-11 right
     if (lane < 12) {
       const int b = lane < 6 ? Md::LFOOT_BODY : Md::RFOOT_BODY, k = lane < 6 ? lane : lane - 6;
-      const int(*CHN)[Md::MAXCHAIN] = Md::chain_d();
+      const int cb = lane < 6 ? Md::B_CHAINL : Md::B_CHAINR;
       float s = 0.0f;
       for (int c = 0; c < Md::MAXCHAIN; c++) {
-        const int i = CHN[b][c];
-        if (i >= 0) s += L[Ly::CDOF + 6 * i + k] * L[X + i];
+        const int i = ti(cb + c);
+        const int ic = i >= 0 ? i : 0;
+        const float t = L[Ly::CDOF + 6 * ic + k] * L[X + ic];
+        s += i >= 0 ? t : 0.0f;
       }
       L[TL::TSP + lane] = s;
     }
     if (lane < NFRIC) {
       const int r = lane;
-      L[DST + r] = L[X + Md::fric_dof[r]] - (sub_aref ? L[Ly::AREF + r] : 0.0f);
+      L[DST + r] = L[X + fric_dof(r)] - (sub_aref ? L[Ly::AREF + r] : 0.0f);
     }
     for (int r = lane; r < NLIM; r += TEAM)
-      L[DST + R_LIM + r] = L[Ly::LSGN + r] * L[X + Md::jnt_dofadr[Md::lim_jnt[r]]] -
+      L[DST + R_LIM + r] = L[Ly::LSGN + r] * L[X + lim_dof(r)] -
                            (sub_aref ? L[Ly::AREF + R_LIM + r] : 0.0f);
     TSYNC();
     if (lane < NCON) {
@@ -860,12 +1045,12 @@ struct TPhys {
 
   // Y = M X (sparse symmetric)
   static DK void mul_M(LP L, int lane, int X, int Y) {
-    const int(*MA)[NV] = Md::t_madr();
     for (int i = lane; i < NV; i += TEAM) {
       float acc = 0.0f;
       for (int j = 0; j < NV; j++) {
-        const int a = MA[i][j];
-        if (a >= 0) acc += L[Ly::M + a] * L[X + j];
+        const int a = madr(i, j);
+        const float t = L[Ly::M + (a >= 0 ? a : 0)] * L[X + j];
+        acc += a >= 0 ? t : 0.0f;
       }
       L[Y + i] = acc;
     }
@@ -883,7 +1068,7 @@ struct TPhys {
     float cost = 0.0f;
     if (lane < NFRIC) {
       const int r = lane;
-      const float D = L[Ly::RD + r], x = L[Ly::JA + r], f = L[Ly::DFRIC + Md::fric_dof[r]];
+      const float D = L[Ly::RD + r], x = L[Ly::JA + r], f = L[Ly::DFRIC + fric_dof(r)];
       const float rf = f / D;
       cost += x <= -rf ? (-f * x - 0.5f * rf * f) : (x >= rf ? (f * x - 0.5f * rf * f) : 0.5f * D * x * x);
     }
@@ -901,7 +1086,7 @@ struct TPhys {
     for (int k = lane; k < Md::NM; k += TEAM) L[Ly::H + k] = L[Ly::M + k];
     TSYNC();
     if (lane < NFRIC) {
-      const int r = lane, i = Md::fric_dof[r];
+      const int r = lane, i = fric_dof(r);
       const float D = L[Ly::RD + r], x = L[Ly::JA + r], f = L[Ly::DFRIC + i], rf = f / D;
       const float force = x <= -rf ? f : (x >= rf ? -f : -D * x);
       L[Ly::GRAD + i] -= force;
@@ -909,7 +1094,7 @@ struct TPhys {
     }
     TSYNC();
     for (int r = lane; r < NLIM; r += TEAM) {
-      const int i = Md::jnt_dofadr[Md::lim_jnt[r]];
+      const int i = lim_dof(r);
       const float D = L[Ly::RD + R_LIM + r], x = L[Ly::JA + R_LIM + r];
       if (x < 0.0f) {
         L[Ly::GRAD + i] -= L[Ly::LSGN + r] * (-D * x);
@@ -951,8 +1136,8 @@ struct TPhys {
         for (int q = 0; q < 6; q++) F[q] = tsum(force * a[q]);
       }
       // K.cdof_j and the gradient for the chain dofs (lane = chain position)
-      const int(*CHN)[Md::MAXCHAIN] = Md::chain_d();
-      const int jl = lane < Md::MAXCHAIN ? CHN[b][lane] : -1;
+      const int cb = foot == 1 ? Md::B_CHAINL : Md::B_CHAINR;
+      const int jl = lane < Md::MAXCHAIN ? ti(cb + lane) : -1;
       if (jl >= 0) {
         float cdj[6];
         for (int k = 0; k < 6; k++) cdj[k] = L[Ly::CDOF + 6 * jl + k];
@@ -971,10 +1156,10 @@ struct TPhys {
         float cdi[6];
         for (int k = 0; k < 6; k++) cdi[k] = L[Ly::CDOF + 6 * jl + k];
         for (int cj = 0; cj <= lane; cj++) {
-          const int j = CHN[b][cj];
+          const int j = ti(cb + cj);
           float s = 0.0f;
           for (int k = 0; k < 6; k++) s += cdi[k] * L[TL::KC + 6 * cj + k];
-          L[Ly::H + Md::t_madr()[jl][j]] += s;
+          L[Ly::H + madr(jl, j)] += s;
         }
       }
       TSYNC();
@@ -1001,7 +1186,7 @@ struct TPhys {
     R.fD = fr ? L[Ly::RD + lane] : 0.0f;
     R.fja = fr ? L[Ly::JA + lane] : 0.0f;
     R.fv = fr ? L[Ly::JV + lane] : 0.0f;
-    R.ff = fr ? L[Ly::DFRIC + Md::fric_dof[lane]] : 0.0f;
+    R.ff = fr ? L[Ly::DFRIC + fric_dof(lane)] : 0.0f;
     for (int m = 0; m < RQ; m++) {
       const int r = R_LIM + lane + TEAM * m;
       const bool ok = r < NROW;
@@ -1041,34 +1226,48 @@ struct TPhys {
 
   // ---- fused solver passes ----
   // foot spatial motions of X (and X2) into TSP[0..11] (and TSP[12..23]); Y = M X (and Y2 = M X2)
-  static DK void spatial_and_M(LP L, int lane, int X, int Y, int X2, int Y2) {
+  // foot spatial motions only (lanes 0-11): X into TSP[0..11], X2 (if >= 0) into TSP[12..23]
+  static DK void spatial2(LP L, int lane, int X, int X2) {
     if (lane < 12) {
-      const int b = lane < 6 ? Md::LFOOT_BODY : Md::RFOOT_BODY, k = lane < 6 ? lane : lane - 6;
-      const int(*CHN)[Md::MAXCHAIN] = Md::chain_d();
+      const int k = lane < 6 ? lane : lane - 6;
+      const int cb = lane < 6 ? Md::B_CHAINL : Md::B_CHAINR;
       float s = 0.0f, s2 = 0.0f;
 #pragma unroll
       for (int c = 0; c < Md::MAXCHAIN; c++) {
-        const int i = CHN[b][c];
-        if (i >= 0) {
-          const float cd = L[Ly::CDOF + 6 * i + k];
-          s += cd * L[X + i];
-          if (X2 >= 0) s2 += cd * L[X2 + i];
-        }
+        const int i = ti(cb + c), ic = i >= 0 ? i : 0;
+        const float cd = i >= 0 ? L[Ly::CDOF + 6 * ic + k] : 0.0f;
+        s += cd * L[X + ic];
+        if (X2 >= 0) s2 += cd * L[X2 + ic];
       }
       L[TL::TSP + lane] = s;
       if (X2 >= 0) L[TL::TSP + 12 + lane] = s2;
     }
-    const int(*MA)[NV] = Md::t_madr();
+  }
+
+  static DK void spatial_and_M(LP L, int lane, int X, int Y, int X2, int Y2) {
+    if (lane < 12) {
+      const int b = lane < 6 ? Md::LFOOT_BODY : Md::RFOOT_BODY, k = lane < 6 ? lane : lane - 6;
+      const int cb = lane < 6 ? Md::B_CHAINL : Md::B_CHAINR;
+      float s = 0.0f, s2 = 0.0f;
+#pragma unroll
+      for (int c = 0; c < Md::MAXCHAIN; c++) {
+        const int i = ti(cb + c), ic = i >= 0 ? i : 0;
+        const float cd = i >= 0 ? L[Ly::CDOF + 6 * ic + k] : 0.0f;
+        s += cd * L[X + ic];
+        if (X2 >= 0) s2 += cd * L[X2 + ic];
+      }
+      L[TL::TSP + lane] = s;
+      if (X2 >= 0) L[TL::TSP + 12 + lane] = s2;
+    }
     for (int i = lane; i < NV; i += TEAM) {
       float acc = 0.0f, acc2 = 0.0f;
 #pragma unroll
       for (int j = 0; j < NV; j++) {
-        const int a = MA[i][j];
-        if (a >= 0) {
-          const float m = L[Ly::M + a];
-          acc += m * L[X + j];
-          if (X2 >= 0) acc2 += m * L[X2 + j];
-        }
+        const int a = madr(i, j);
+        const float mv = L[Ly::M + (a >= 0 ? a : 0)];
+        const float m = a >= 0 ? mv : 0.0f;
+        acc += m * L[X + j];
+        if (X2 >= 0) acc2 += m * L[X2 + j];
       }
       L[Y + i] = acc;
       if (X2 >= 0) L[Y2 + i] = acc2;
@@ -1110,12 +1309,17 @@ struct TPhys {
   // mjx solver.solve, iterations = 1
   static DK void solve(LP L, int lane, float* scratch, int stride) {
     STAGE_T0();
+    // M as full symmetric columns in registers for every M.x of the solver
+    float Mc[NC][NV];
+    load_cols(L, lane, Ly::M, Mc, false);
     // warm start vs smooth acceleration: J and M products of both in one pass
-    spatial_and_M(L, lane, Ly::WARM, Ly::MA, Ly::QSM, Ly::GRAD);
+    spatial2(L, lane, Ly::WARM, Ly::QSM);
+    mul_cols(L, lane, Mc, Ly::WARM, Ly::MA);
+    mul_cols(L, lane, Mc, Ly::QSM, Ly::GRAD);
     TSYNC();
     float cwp = 0.0f, csp = 0.0f, gwp = 0.0f;
     if (lane < NFRIC) {
-      const int r = lane, i = Md::fric_dof[r];
+      const int r = lane, i = fric_dof(r);
       const float D = L[Ly::RD + r], f = L[Ly::DFRIC + i], ar = L[Ly::AREF + r];
       const float jw = L[Ly::WARM + i] - ar, js = L[Ly::QSM + i] - ar;
       cwp += fric_cost(D, jw, f);
@@ -1124,7 +1328,7 @@ struct TPhys {
       L[Ly::JV + r] = js;
     }
     for (int r = lane; r < NLIM; r += TEAM) {
-      const int i = Md::jnt_dofadr[Md::lim_jnt[r]], row = R_LIM + r;
+      const int i = lim_dof(r), row = R_LIM + r;
       const float D = L[Ly::RD + row], sg = L[Ly::LSGN + r], ar = L[Ly::AREF + row];
       const float jw = sg * L[Ly::WARM + i] - ar, js = sg * L[Ly::QSM + i] - ar;
       cwp += jw < 0.0f ? 0.5f * D * jw * jw : 0.0f;
@@ -1165,10 +1369,9 @@ struct TPhys {
     }
     TSYNC();
     STAGE_MARK(9);
-    const bool sparse_ok = newton_direction(L, lane);
+    const bool sparse_ok = newton_fused(L, lane, Mc);
     STAGE_MARK(10);
     if (sparse_ok) {
-      solve_regs(L, lane, Ly::H, Ly::GRAD, Ly::SRCH, -1.0f);
       STAGE_MARK(11);
     } else {
       TSYNC();
@@ -1178,22 +1381,22 @@ struct TPhys {
       TSYNC();
     }
     // J.search and M.search in one pass; rows go straight to registers
-    spatial_and_M(L, lane, Ly::SRCH, Ly::GRAD, -1, -1);
+    spatial2(L, lane, Ly::SRCH, -1);
+    mul_cols(L, lane, Mc, Ly::SRCH, Ly::GRAD);
     TSYNC();
     Rows2 R;
     R.fD = R.fja = R.fv = R.ff = 0.0f;
     if (lane < NFRIC) {
-      const int r = lane, i = Md::fric_dof[r];
+      const int r = lane, i = fric_dof(r);
       R.fD = L[Ly::RD + r]; R.fja = L[Ly::JA + r]; R.fv = L[Ly::SRCH + i]; R.ff = L[Ly::DFRIC + i];
     }
 #pragma unroll
     for (int m = 0; m < NLR; m++) {
       const int r = lane + TEAM * m;
-      R.lD[m] = R.lja[m] = R.lv[m] = 0.0f;
-      if (r < NLIM) {
-        const int i = Md::jnt_dofadr[Md::lim_jnt[r]], row = R_LIM + r;
-        R.lD[m] = L[Ly::RD + row]; R.lja[m] = L[Ly::JA + row]; R.lv[m] = L[Ly::LSGN + r] * L[Ly::SRCH + i];
-      }
+      const bool ok = r < NLIM;
+      const int rc = ok ? r : 0, i = lim_dof(rc), row = R_LIM + rc;
+      const float D = L[Ly::RD + row], ja = L[Ly::JA + row], v = L[Ly::LSGN + rc] * L[Ly::SRCH + i];
+      R.lD[m] = ok ? D : 0.0f; R.lja[m] = ok ? ja : 0.0f; R.lv[m] = ok ? v : 0.0f;
     }
     for (int e = 0; e < 4; e++) R.cD[e] = R.cja[e] = R.cv[e] = 0.0f;
     if (lane < NCON) {
