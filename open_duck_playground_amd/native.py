@@ -49,7 +49,10 @@ def build(verbose: bool = False, defines=(), out: str = None) -> str:
     if not defines and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
     import tempfile
-    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"] + [f"-D{d}" for d in defines]
+    # fp32 division and sqrt as v_rcp/v_sqrt (1-2 ulp) instead of the correctly rounded
+    # multi-instruction sequences: the physics tolerances are fp32-vs-fp64 anyway
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-hip-fp32-correctly-rounded-divide-sqrt"] + \
+        [f"-D{d}" for d in defines]
     with tempfile.TemporaryDirectory() as tmp:
         objs, procs = [], []
         for src in srcs:
