@@ -128,6 +128,15 @@ def chain_of(m: Model, b: int):
     return sorted(c)
 
 
+def _is_anc(m: Model, a: int, b: int) -> bool:
+    """body a is b or an ancestor of b"""
+    while b > 0:
+        if b == a:
+            return True
+        b = m.body_parentid[b]
+    return a == b
+
+
 def maxchain_of(m: Model):
     return max(len(chain_of(m, b)) for b in range(m.nbody))
 
@@ -292,6 +301,41 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         d2l[m.jnt_dofadr[j]] = r
     put("dof2fric", d2f)
     put("dof2lim", d2l)
+    # flattened tree recursions: per body its dof chain and its subtree, per body the local
+    # kinematics record, per dof its body / parent body / first dof of its body / free flag
+    mc = maxchain_of(m)
+    bchain = np.full((nb, mc), -1)
+    for b in range(nb):
+        c = chain_of(m, b)
+        bchain[b, :len(c)] = c
+    put("bchain", bchain.reshape(-1))
+    dyn = [b for b in range(1, nb) if m.body_weldid[b] != 0]
+    sub = [[d for d in dyn if _is_anc(m, b, d)] for b in range(nb)]
+    msub = max(len(x) for x in sub)
+    bsub = np.full((nb, msub), -1)
+    for b in range(nb):
+        bsub[b, :len(sub[b])] = sub[b]
+    put("bsub", bsub.reshape(-1))
+    rec = []
+    for b in range(nb):
+        q, pz = m.body_quat[b], m.body_pos[b]
+        nj = int(m.body_jntnum[b]) if b != 1 else 0
+        assert nj <= 2
+        jr = []
+        for jj in range(2):
+            if jj < nj:
+                j = m.body_jntadr[b] + jj
+                jr += [int(m.jnt_qposadr[j])] + [f2i(x) for x in m.jnt_axis[j]]
+            else:
+                jr += [0, 0, 0, 0]
+        rec += [f2i(x) for x in q] + [f2i(x) for x in pz] + [nj] + jr
+    put("bkin", rec)  # stride 16: quat4 pos3 njnt (qadr, axis3) x 2
+    rec = []
+    for i in range(nv):
+        b = int(m.dof_bodyid[i])
+        rec += [b, int(m.body_parentid[b]), int(m.body_dofadr[b]), int(m.jnt_type[m.dof_jntid[i]] == 0)]
+    put("dofrec", rec)  # stride 4: body, parent body, first dof of the body, free-joint flag
+    extra_const = [f"  static constexpr int T_MAXSUB = {msub};\n"]
     T = lambda name, a, t: f"__device__ const {t} {pre}_{name}{''.join(f'[{d}]' for d in np.shape(a))} = " + \
         _arr("x", np.asarray(a), t).split("= ", 1)[1]
     tabs = {"lev": (lev, "int"), "child": (child, "int"), "madr": (full, "int"), "mi": (mi, "int"), "mj": (mj, "int"),
@@ -311,7 +355,7 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
            _arr("T_DIAG", [adr[i, i] for i in range(nv)], "int"),
            f"  static constexpr int T_NROOT = {len(root)}, T_NBR = {len(branches)}, T_BRLEN = {brlen};\n",
            _arr("T_ROOT", root, "int"),
-           f"  static constexpr int NBLOB = {len(blob)};\n",
+           f"  static constexpr int NBLOB = {len(blob)};\n"] + extra_const + [
            "".join(f"  static constexpr int B_{k.upper()} = {v};\n" for k, v in boff.items())]
     for k, (a, t) in tabs.items():
         shp = np.shape(a)

@@ -83,6 +83,13 @@ struct TLay {
   static constexpr int STRIDE = ((USED + 15) / 32) * 32 + 16;  // = 16 (mod 32), >= USED
   static_assert(STRIDE >= USED && STRIDE % 32 == 16, "stride");
   static constexpr int FTMP = Ly::JA;                  // crb: F_i = I_b cdof_i (dead row storage)
+  // scratch of the flattened tree passes: the H + constraint-row storage is dead until the
+  // constraint stage (kinematics / rne / crb run before it)
+  static constexpr int TMP = Ly::H;
+  static constexpr int KLOC = TMP;                               // local body transforms (7 per body)
+  static constexpr int RCS = TMP, RCF = TMP + 6 * Md::NB, RCDD = TMP + 12 * Md::NB;  // rne
+  static constexpr int CRB = TMP, FT = TMP + 10 * Md::NB;        // crb
+  static_assert(12 * Md::NB + 6 * Md::NV <= Md::NM + 4 * Ly::NROW, "tree scratch must fit in H + rows");
   // the model blob (lane-indexed tables, constraint-row records) follows the env slices in
   // LDS when it fits, else it is read from global memory
   static constexpr int TAB = STRIDE * TEAM_WG;
@@ -160,19 +167,48 @@ struct TPhys {
   }
 
   static DK void kinematics(LP L, int lane) {
+    // K1: local transform (body quat x joint rotations, body pos) of every moving body, a
+    // body per lane, off the serial chain
+    for (int b = 2 + lane; b < NB; b += TEAM) {
+      if (Md::body_weldid[b] == 0) continue;
+      const int o = Md::B_BKIN + 16 * b;
+      float q[4] = {tf(o), tf(o + 1), tf(o + 2), tf(o + 3)};
+      const int nj = ti(o + 7);
+#pragma unroll
+      for (int jj = 0; jj < 2; jj++) {
+        if (jj < nj) {
+          const int oj = o + 8 + 4 * jj, a = ti(oj);
+          float sn, cs;
+          __sincosf(0.5f * (L[Ly::QPOS + a] - L[Ly::DQ0 + a]), &sn, &cs);
+          const float ql[4] = {cs, tf(oj + 1) * sn, tf(oj + 2) * sn, tf(oj + 3) * sn};
+          qmul(q, q, ql);
+        }
+      }
+      for (int k = 0; k < 4; k++) L[TL::KLOC + 7 * b + k] = q[k];
+      for (int k = 0; k < 3; k++) L[TL::KLOC + 7 * b + 4 + k] = tf(o + 4 + k);
+    }
+    TSYNC();
+    // K2: compose down the root path (every lane) and the limbs (a limb per lane)
     float p[3], q[4], R[9];
     for (int k = 0; k < 3; k++) p[k] = L[Ly::QPOS + k];
     for (int k = 0; k < 4; k++) q[k] = L[Ly::QPOS + 3 + k];
     qnormalize(q);
     q2m(R, q);
     if (lane == 0) store_pose(L, 1, p, q, R);
+    auto compose = [&](int b) {
+      float ql[4], pl[3], t[3], qn[4];
+      for (int k = 0; k < 4; k++) ql[k] = L[TL::KLOC + 7 * b + k];
+      for (int k = 0; k < 3; k++) pl[k] = L[TL::KLOC + 7 * b + 4 + k];
+      mulmv3(t, R, pl);
+      for (int k = 0; k < 3; k++) p[k] += t[k];
+      qmul(qn, q, ql);
+      qnormalize(qn);
+      for (int k = 0; k < 4; k++) q[k] = qn[k];
+      q2m(R, q);
+    };
 #pragma unroll
     for (int r = 1; r < Md::T_NROOT; r++) {
-      float p2[3], q2[4], R2[9];
-      body_pose(L, Md::T_ROOT[r], p, R, q, p2, q2, R2);
-      for (int k = 0; k < 3; k++) p[k] = p2[k];
-      for (int k = 0; k < 4; k++) q[k] = q2[k];
-      for (int k = 0; k < 9; k++) R[k] = R2[k];
+      compose(Md::T_ROOT[r]);
       if (lane == 0) store_pose(L, Md::T_ROOT[r], p, q, R);
     }
     if (lane < Md::T_NBR) {
@@ -182,11 +218,7 @@ struct TPhys {
 #pragma unroll
       for (int d = 0; d < Md::T_BRLEN; d++) {
         if (bb[d] < 0) break;
-        float p2[3], q2[4], R2[9];
-        body_pose(L, bb[d], p, R, q, p2, q2, R2);
-        for (int k = 0; k < 3; k++) p[k] = p2[k];
-        for (int k = 0; k < 4; k++) q[k] = q2[k];
-        for (int k = 0; k < 9; k++) R[k] = R2[k];
+        compose(bb[d]);
         store_pose(L, bb[d], p, q, R);
       }
     }
@@ -1551,7 +1583,7 @@ struct TPhys {
       float ax[3] = {1.0f, 0.0f, 0.0f};
       if (nvv > 1e-15f) { ax[0] = v[0] / nvv; ax[1] = v[1] / nvv; ax[2] = v[2] / nvv; }
       float s, c;
-      sincosf(0.5f * dt * nvv, &s, &c);
+      __sincosf(0.5f * dt * nvv, &s, &c);
       const float qr[4] = {c, ax[0] * s, ax[1] * s, ax[2] * s};
       float q[4] = {L[Ly::QPOS + 3], L[Ly::QPOS + 4], L[Ly::QPOS + 5], L[Ly::QPOS + 6]};
       qmul(q, q, qr);
