@@ -335,6 +335,12 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         b = int(m.dof_bodyid[i])
         rec += [b, int(m.body_parentid[b]), int(m.body_dofadr[b]), int(m.jnt_type[m.dof_jntid[i]] == 0)]
     put("dofrec", rec)  # stride 4: body, parent body, first dof of the body, free-joint flag
+    dch = np.full((nv, mc), -1)
+    for i in range(nv):
+        c = sorted(_ancestors(m, i, True))
+        dch[i, :len(c)] = c
+    put("dchain", dch.reshape(-1))  # ancestors of dof i incl. itself, ascending (= M row order)
+    put("mrow", [adr[i, min(_ancestors(m, i, True))] for i in range(nv)])  # adr of row i's first entry
     extra_const = [f"  static constexpr int T_MAXSUB = {msub};\n"]
     T = lambda name, a, t: f"__device__ const {t} {pre}_{name}{''.join(f'[{d}]' for d in np.shape(a))} = " + \
         _arr("x", np.asarray(a), t).split("= ", 1)[1]

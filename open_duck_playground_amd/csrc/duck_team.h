@@ -399,46 +399,71 @@ struct TPhys {
 
   // ---------------- mj_crb: composite inertias (limb sums, then the root path) and the sparse M ----
   static DK void crb(LP L, int lane) {
+    constexpr int BL = Md::T_BRLEN, MC = Md::MAXCHAIN;
+    // composite inertias: each limb lane loads its bodies' cinert first (no store in between,
+    // so the loads issue together), forms suffix sums, then stores; the trunk sums the limbs
     float S[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (lane < Md::T_NBR) {
-      int bb[Md::T_BRLEN];
+    {
+      int bb[BL];
+      float C[BL][10];
 #pragma unroll
-      for (int d = 0; d < Md::T_BRLEN; d++) bb[d] = Md::t_br()[lane][d];
+      for (int d = 0; d < BL; d++) bb[d] = lane < Md::T_NBR ? Md::t_br()[lane < Md::T_NBR ? lane : 0][d] : -1;
 #pragma unroll
-      for (int d = Md::T_BRLEN - 1; d >= 0; d--) {
-        if (bb[d] >= 0) {
-          for (int k = 0; k < 10; k++) { S[k] += L[Ly::CIN + 10 * bb[d] + k]; L[Ly::CIN + 10 * bb[d] + k] = S[k]; }
-        }
+      for (int d = 0; d < BL; d++) {
+        const int bc = bb[d] >= 0 ? bb[d] : 1;
+        for (int k = 0; k < 10; k++) C[d][k] = L[Ly::CIN + 10 * bc + k];
       }
+#pragma unroll
+      for (int d = BL - 1; d >= 0; d--)
+        for (int k = 0; k < 10; k++) {
+          S[k] += bb[d] >= 0 ? C[d][k] : 0.0f;
+          C[d][k] = S[k];
+        }
+#pragma unroll
+      for (int d = 0; d < BL; d++)
+        if (bb[d] >= 0)
+          for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * bb[d] + k] = C[d][k];
     }
     for (int k = 0; k < 10; k++) S[k] = tsum(S[k]);
+    {
+      float Rr[Md::T_NROOT][10];
 #pragma unroll
-    for (int r = Md::T_NROOT - 1; r >= 0; r--) {
-      const int b = Md::T_ROOT[r];
-      for (int k = 0; k < 10; k++) S[k] += L[Ly::CIN + 10 * b + k];
+      for (int r = 0; r < Md::T_NROOT; r++)
+        for (int k = 0; k < 10; k++) Rr[r][k] = L[Ly::CIN + 10 * Md::T_ROOT[r] + k];
+#pragma unroll
+      for (int r = Md::T_NROOT - 1; r >= 0; r--)
+        for (int k = 0; k < 10; k++) { S[k] += Rr[r][k]; Rr[r][k] = S[k]; }
       TSYNC();
       if (lane == 0)
-        for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * b + k] = S[k];
-    }
-    TSYNC();
-    for (int i = lane; i < NV; i += TEAM) {
-      float cd[6], buf[6], I[10];
-      for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
-      for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * Md::dof_bodyid[i] + k];
-      mul_inert_vec(buf, I, cd);
-      for (int k = 0; k < 6; k++) L[TL::FTMP + 6 * i + k] = buf[k];
-    }
-    TSYNC();
-
 #pragma unroll
-    for (int a0 = 0; a0 < Md::NM; a0 += TEAM) {
-      const int a = a0 + lane;
-      if (a < Md::NM) {
-        const int i = ti(Md::B_MI + a), j = ti(Md::B_MJ + a);
-        float s = 0.0f;
-        for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * j + k] * L[TL::FTMP + 6 * i + k];
-        if (i == j) s += L[Ly::DARM + i];
-        L[Ly::M + a] = s;
+        for (int r = 0; r < Md::T_NROOT; r++)
+          for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * Md::T_ROOT[r] + k] = Rr[r][k];
+    }
+    TSYNC();
+    // M row i (lane i, i + 16): F_i = crb_{body(i)} cdof_i stays in registers;
+    // M[i][j] = cdof_j . F_i over the ancestors j of i (the row is contiguous in M)
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int i = TEAM * s + lane, ic = i < NV ? i : 0;
+      float cd[6], F[6], I[10];
+      for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * ic + k];
+      for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * Md::dof_bodyid[ic] + k];
+      int jj[MC];
+      float cj[MC][6];
+#pragma unroll
+      for (int q = 0; q < MC; q++) {
+        jj[q] = ti(Md::B_DCHAIN + MC * ic + q);
+        const int jc = jj[q] >= 0 ? jj[q] : 0;
+        for (int k = 0; k < 6; k++) cj[q][k] = L[Ly::CDOF + 6 * jc + k];
+      }
+      const float arm = L[Ly::DARM + ic];
+      const int rs = ti(Md::B_MROW + ic);
+      mul_inert_vec(F, I, cd);
+#pragma unroll
+      for (int q = 0; q < MC; q++) {
+        float v = 0.0f;
+        for (int k = 0; k < 6; k++) v += cj[q][k] * F[k];
+        if (i < NV && jj[q] >= 0) L[Ly::M + rs + q] = v + (jj[q] == i ? arm : 0.0f);
       }
     }
     TSYNC();
