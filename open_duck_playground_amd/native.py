@@ -19,7 +19,7 @@ ROOT = os.path.dirname(HERE)
 
 EXPORTS = ["duck_version", "duck_last_error", "duck_layout_get", "duck_aux_size", "duck_create", "duck_destroy",
            "duck_debug_stage_cycles",
-           "duck_reset", "duck_step", "duck_randomize", "duck_physics_step"]
+           "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae"]
 
 
 class DuckError(RuntimeError):
@@ -93,6 +93,7 @@ def lib():
         L.duck_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.duck_randomize.argtypes = [vp, C.c_int, vp, C.c_uint64, C.c_int64, vp]
         L.duck_physics_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp, vp, vp]
+        L.duck_gae.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp]
         _lib = L
     return _lib
 

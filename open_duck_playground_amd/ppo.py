@@ -168,7 +168,7 @@ class ActorCritic(nn.Module):
 # losses (brax ppo/losses.py)
 # ---------------------------------------------------------------------------------------
 @torch.no_grad()
-def compute_gae(truncation: torch.Tensor, termination: torch.Tensor, rewards: torch.Tensor, values: torch.Tensor,
+def compute_gae_torch(truncation: torch.Tensor, termination: torch.Tensor, rewards: torch.Tensor, values: torch.Tensor,
                 bootstrap_value: torch.Tensor, lambda_: float, discount: float):
     """Time-major [T, B] GAE with truncation masking (brax losses.compute_gae)."""
     trunc_mask = 1.0 - truncation
@@ -183,6 +183,24 @@ def compute_gae(truncation: torch.Tensor, termination: torch.Tensor, rewards: to
     vs_t_plus_1 = torch.cat([vs[1:], bootstrap_value[None]], dim=0)
     advantages = (rewards + discount * (1.0 - termination) * vs_t_plus_1 - values) * trunc_mask
     return vs, advantages
+
+
+@torch.no_grad()
+def compute_gae(truncation: torch.Tensor, termination: torch.Tensor, rewards: torch.Tensor, values: torch.Tensor,
+                bootstrap_value: torch.Tensor, lambda_: float, discount: float):
+    """GAE: the ``duck_gae`` HIP kernel for fp32 GPU tensors (one launch instead of ~120 small
+    ones per minibatch), the torch recursion for host tensors (CPU-only toy runs, tests)."""
+    if not values.is_cuda:
+        return compute_gae_torch(truncation, termination, rewards, values, bootstrap_value, lambda_, discount)
+    from .native import check, lib
+    T, B = values.shape
+    args = [t.contiguous() for t in (truncation, termination, rewards, values, bootstrap_value)]
+    if any(a.dtype != torch.float32 for a in args):
+        raise TypeError("compute_gae on the GPU takes float32 tensors")
+    vs, adv = torch.empty_like(args[3]), torch.empty_like(args[3])
+    check(lib().duck_gae(T, B, *(a.data_ptr() for a in args), float(lambda_), float(discount), vs.data_ptr(),
+                         adv.data_ptr(), torch.cuda.current_stream(values.device).cuda_stream))
+    return vs, adv
 
 
 def ppo_loss(net: ActorCritic, batch: Dict[str, torch.Tensor], cfg: PPOConfig, gen: Optional[torch.Generator]):
@@ -232,6 +250,68 @@ def broadcast_params(module: nn.Module) -> None:
 # ---------------------------------------------------------------------------------------
 # training loop (brax ppo/train.py structure)
 # ---------------------------------------------------------------------------------------
+class _Learner:
+    """One SGD minibatch step: gather -> loss -> backward -> (grad all-reduce) -> clip -> Adam.
+
+    On the GPU the step is captured once into HIP graphs and replayed for every minibatch
+    (≈300 small kernels per step would otherwise be launch-bound): graph 1 = gather + loss +
+    backward into static grads, then the RCCL all-reduce runs eagerly (world > 1), graph 2 =
+    global-norm clip + Adam. The first ``WARMUP`` steps run eagerly on a side stream (they are
+    real updates, as torch's capture recipe requires), so the update sequence is unchanged.
+    """
+
+    WARMUP = 3
+
+    def __init__(self, net: ActorCritic, opt, cfg: PPOConfig, data: Dict[str, torch.Tensor], mb: int,
+                 device: torch.device, use_graph: bool):
+        self.net, self.opt, self.cfg, self.data = net, opt, cfg, data
+        self.params = list(net.parameters())
+        self.idx = torch.zeros(mb, dtype=torch.long, device=device)
+        self.use_graph = use_graph
+        self.calls = 0
+        self.g1 = self.g2 = None
+        self.out = None
+
+    def _fwd_bwd(self):
+        mbatch = {k: v[:, self.idx] for k, v in self.data.items()}
+        loss, m = ppo_loss(self.net, mbatch, self.cfg, None)
+        self.opt.zero_grad(set_to_none=False)
+        loss.backward()
+        return {"loss": loss.detach(), **m}
+
+    def _apply(self):
+        torch.nn.utils.clip_grad_norm_(self.params, self.cfg.max_grad_norm)
+        self.opt.step()
+
+    def step(self, idx: torch.Tensor) -> Dict[str, torch.Tensor]:
+        self.idx.copy_(idx)
+        self.calls += 1
+        if not self.use_graph:
+            out = self._fwd_bwd()
+            allreduce_grads(self.params)
+            self._apply()
+            return out
+        if self.calls <= self.WARMUP:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                out = self._fwd_bwd()
+                allreduce_grads(self.params)
+                self._apply()
+            torch.cuda.current_stream().wait_stream(s)
+            return out
+        if self.g1 is None:
+            self.g1, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g1):
+                self.out = self._fwd_bwd()
+            with torch.cuda.graph(self.g2, pool=self.g1.pool()):
+                self._apply()
+        self.g1.replay()
+        allreduce_grads(self.params)
+        self.g2.replay()
+        return self.out
+
+
 @dataclass
 class TrainResult:
     net: ActorCritic
@@ -244,15 +324,17 @@ class TrainResult:
 def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]] = None,
           eval_env=None, max_updates: Optional[int] = None, device=None,
           policy_params_fn: Optional[Callable[[int, "ActorCritic"], None]] = None,
-          restore_checkpoint_path: Optional[str] = None) -> TrainResult:
+          restore_checkpoint_path: Optional[str] = None, use_graph: Optional[bool] = None) -> TrainResult:
     """Train on a batched env with the Joystick surface (reset(rng) / step(state, action)).
 
     ``env`` is already wrapped for training (episode length + auto-reset, DR if wanted) and
-    holds ``cfg.num_envs`` envs (per rank). One update consumes ``batch_size * num_minibatches``
-    trajectories of ``unroll_length`` steps; with the default config that is one unroll of all
-    8192 envs per update, as brax PPO does.
+    holds this rank's ``num_envs / world`` envs. One update consumes ``batch_size *
+    num_minibatches`` trajectories of ``unroll_length`` steps over all ranks; with the default
+    config that is one unroll of all 8192 envs per update, as brax PPO does (train.py).
     """
     device = torch.device(device or env.device)
+    if use_graph is None:
+        use_graph = device.type == "cuda" and os.environ.get("DUCK_PPO_GRAPH", "1") != "0"
     rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
     world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
     torch.manual_seed(cfg.seed + rank)
@@ -260,12 +342,13 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
     gen.manual_seed(cfg.seed * 7919 + rank)
     obs_size = env.observation_size[cfg.policy_obs_key][0]
     priv_size = env.observation_size[cfg.value_obs_key][0]
-    net = ActorCritic(obs_size, priv_size, env.action_size, cfg).to(device)
+    A = env.action_size
+    net = ActorCritic(obs_size, priv_size, A, cfg).to(device)
     if restore_checkpoint_path is not None:  # brax: restores policy + normaliser (and value) params
         ck = torch.load(restore_checkpoint_path, map_location=device, weights_only=True)
         net.load_state_dict(ck["state_dict"])
     broadcast_params(net)
-    opt = torch.optim.Adam(net.parameters(), lr=cfg.learning_rate)
+    opt = torch.optim.Adam(net.parameters(), lr=cfg.learning_rate, capturable=device.type == "cuda")
     n = env.num_envs  # envs on this rank (brax: num_envs // devices)
     traj_per_update = cfg.batch_size * cfg.num_minibatches // world  # this rank's share
     if traj_per_update % n != 0 or traj_per_update % cfg.num_minibatches != 0:
@@ -276,6 +359,13 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
     n_updates = max(1, cfg.num_timesteps // steps_per_update)
     if max_updates is not None:
         n_updates = min(n_updates, max_updates)
+    T, B = cfg.unroll_length, traj_per_update
+    mb = B // cfg.num_minibatches
+    # rollout buffers, time-major [T, B, ...], written in place by the unroll (static for the graphs)
+    shapes = {"obs": (obs_size,), "priv": (priv_size,), "raw_action": (A,), "log_prob": (), "reward": (),
+              "done": (), "truncation": (), "next_priv": (priv_size,)}
+    data = {k: torch.zeros((T, B) + sh, dtype=torch.float32, device=device) for k, sh in shapes.items()}
+    learner = _Learner(net, opt, cfg, data, mb, device, use_graph)
     state = env.reset(rng=cfg.seed)  # streams are keyed by global env id: ranks draw disjoint envs
     result = TrainResult(net=net)
     # brax: num_evals evaluations spread evenly over training, the first before any update
@@ -285,7 +375,6 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
         if progress_fn is not None:
             progress_fn(0, m0)
     t0 = time.time()
-    T = cfg.unroll_length
 
     def _sync():
         if device.type == "cuda":
@@ -295,26 +384,22 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
         _sync()
         t_roll = time.time()
         # ---- rollouts: unroll_length env-steps of all envs, policy in inference mode ----
-        chunks = []
-        for _ in range(unrolls_per_update):
-            buf = {k: [] for k in ("obs", "priv", "raw_action", "log_prob", "reward", "done", "truncation", "next_priv")}
-            with torch.no_grad():
+        with torch.no_grad():
+            for u in range(unrolls_per_update):
+                cols = slice(u * n, (u + 1) * n)
                 for t in range(T):
-                    obs = state.obs[cfg.policy_obs_key].clone()
-                    priv = state.obs[cfg.value_obs_key].clone()
+                    obs, priv = state.obs[cfg.policy_obs_key], state.obs[cfg.value_obs_key]
+                    data["obs"][t, cols] = obs
+                    data["priv"][t, cols] = priv
                     d = NormalTanh(net.policy_logits(obs))
                     raw = d.sample_raw(gen)
-                    buf["obs"].append(obs)
-                    buf["priv"].append(priv)
-                    buf["raw_action"].append(raw)
-                    buf["log_prob"].append(d.log_prob(raw))
+                    data["raw_action"][t, cols] = raw
+                    data["log_prob"][t, cols] = d.log_prob(raw)
                     env.step(state, torch.tanh(raw))
-                    buf["reward"].append(state.reward.clone())
-                    buf["done"].append(state.done.clone())
-                    buf["truncation"].append(state.info["truncation"].clone())
-                    buf["next_priv"].append(state.obs[cfg.value_obs_key].clone())
-            chunks.append({k: torch.stack(v) for k, v in buf.items()})  # [T, n, ...]
-        data = {k: torch.cat([c[k] for c in chunks], dim=1) for k in chunks[0]}  # [T, B, ...]
+                    data["reward"][t, cols] = state.reward
+                    data["done"][t, cols] = state.done
+                    data["truncation"][t, cols] = state.info["truncation"]
+                    data["next_priv"][t, cols] = state.obs[cfg.value_obs_key]
         _sync()
         t_learn = time.time()
         result.timing["rollout_s"] += t_learn - t_roll
@@ -322,21 +407,10 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
             net.obs_norm.update(data["obs"])
             net.priv_norm.update(data["priv"])
         # ---- learning: epochs x shuffled minibatches of whole trajectories ----
-        B = data["obs"].shape[1]
-        mb = B // cfg.num_minibatches
-        last = {}
         for _ in range(cfg.num_updates_per_batch):
             perm = torch.randperm(B, device=device, generator=gen)
             for i in range(0, B - mb + 1, mb):
-                idx = perm[i:i + mb]
-                mbatch = {k: v[:, idx] for k, v in data.items()}
-                loss, m = ppo_loss(net, mbatch, cfg, gen)
-                opt.zero_grad(set_to_none=True)
-                loss.backward()
-                allreduce_grads(list(net.parameters()))
-                torch.nn.utils.clip_grad_norm_(net.parameters(), cfg.max_grad_norm)
-                opt.step()
-                last = m
+                last = learner.step(perm[i:i + mb])
         _sync()
         result.timing["learn_s"] += time.time() - t_learn
         result.env_steps += steps_per_update
@@ -344,7 +418,7 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
         if world > 1:
             dist.all_reduce(rew)
             rew /= world
-        metrics = {"train/reward_per_step": float(rew), "train/loss": float(loss.detach()),
+        metrics = {"train/reward_per_step": float(rew),
                    **{f"train/{k}": float(v) for k, v in last.items()},
                    "env_steps": result.env_steps, "sps": result.env_steps / (time.time() - t0)}
         if eval_env is not None and rank == 0 and eval_every is not None and (
@@ -382,14 +456,17 @@ def evaluate(net: ActorCritic, eval_env, cfg: PPOConfig, rng: int) -> Dict[str, 
 
 
 def save_checkpoint(net: ActorCritic, cfg: PPOConfig, path: str) -> None:
-    """torch state_dict + config (the reference saves orbax params)."""
+    """torch state_dict + config + sizes (the reference saves orbax params)."""
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
-    torch.save({"state_dict": net.state_dict(), "config": asdict(cfg)}, path)
+    sizes = {"obs": net.policy[0].in_features, "priv": net.value[0].in_features,
+             "action": net.policy[-1].out_features // 2}
+    torch.save({"state_dict": net.state_dict(), "config": asdict(cfg), "sizes": sizes}, path)
 
 
-def load_checkpoint(path: str, obs_size: int, priv_size: int, action_size: int, device="cpu") -> ActorCritic:
+def load_checkpoint(path: str, device="cpu") -> ActorCritic:
     ck = torch.load(path, map_location=device, weights_only=True)
     cfg = PPOConfig(**ck["config"])
-    net = ActorCritic(obs_size, priv_size, action_size, cfg).to(device)
+    z = ck["sizes"]
+    net = ActorCritic(z["obs"], z["priv"], z["action"], cfg).to(device)
     net.load_state_dict(ck["state_dict"])
     return net

@@ -181,7 +181,7 @@ def test_checkpoint_roundtrip(tmp_path):
     res = ppo.train(env, cfg, max_updates=2)
     p = str(tmp_path / "ck.pt")
     ppo.save_checkpoint(res.net, cfg, p)
-    net2 = ppo.load_checkpoint(p, 3, 4, 3)
+    net2 = ppo.load_checkpoint(p)
     x = torch.randn(5, 3)
     assert torch.equal(net2.policy_logits(x), res.net.policy_logits(x))
     # restore resumes from the same parameters (normaliser buffers included)
