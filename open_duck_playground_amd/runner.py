@@ -4,7 +4,8 @@ Same command line as the reference's ``python -m playground.open_duck_mini_v2.ru
 ``--output_dir``, ``--num_timesteps``, ``--env``, ``--task``, ``--restore_checkpoint_path``.
 Differences: the learner is ``ppo.train`` (PyTorch on the GPU, RCCL gradient all-reduce when
 launched one process per GPU under ``torch.distributed.run``); checkpoints are torch state
-dicts (``<output_dir>/<date>_<step>.pt``) instead of orbax trees; metrics go to a JSON-lines
+dicts (``<output_dir>/<date>_<step>.pt``) instead of orbax trees, each written next to its
+ONNX policy (``onnx_export``, same contract as common/export_onnx.py); metrics go to a JSON-lines
 file (``<output_dir>/metrics.jsonl``) instead of tensorboardX, which is not installed here.
 """
 
@@ -20,6 +21,7 @@ from pathlib import Path
 import torch
 import torch.distributed as dist
 
+from .onnx_export import export_onnx
 from .joystick import Joystick, domain_randomize, wrap_for_brax_training
 from .ppo import ActorCritic, PPOConfig, save_checkpoint, train
 from .sharding import shard_from_env
@@ -53,6 +55,7 @@ class BaseRunner:
         path = f"{self.output_dir}/{d}_{current_step}.pt"
         print(f"Saving checkpoint (step: {current_step}): {path}")
         save_checkpoint(net, self.ppo_params, path)
+        export_onnx(net, self.action_size, self.obs_size, output_path=f"{self.output_dir}/{d}_{current_step}.onnx")
 
     def make_ppo_params(self) -> PPOConfig:
         return replace(PPOConfig(), num_timesteps=self.num_timesteps)

@@ -41,6 +41,7 @@ def test_runner_cli_one_update(gpu, tmp_path, monkeypatch):
     assert lines[-1]["step"] == 2 * 20 * 256
     cks = sorted(p for p in os.listdir(tmp_path / "ck") if p.endswith(".pt"))
     assert cks, os.listdir(tmp_path / "ck")
+    assert os.path.exists(tmp_path / "ck" / cks[-1].replace(".pt", ".onnx"))
     net = ppo.load_checkpoint(str(tmp_path / "ck" / cks[-1]), device=gpu)
     assert net.policy_logits(torch.zeros(2, 101, device=gpu)).shape == (2, 28)
     # resume from it
