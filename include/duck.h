@@ -42,8 +42,8 @@ enum { DUCK_OK = 0, DUCK_EINVAL = -1, DUCK_EUNSUPPORTED = -2, DUCK_EHIP = -3 };
 int duck_version(void);
 /* message of the last failing call on this thread ("" if none) */
 const char* duck_last_error(void);
-/* per-env state layout for a model/config (same as duck_layout_make) */
-int duck_layout_get(int nq, int nv, int nu, int imitation, duck_layout* out);
+/* per-env state layout for a model/config/task (same as duck_layout_make) */
+int duck_layout_get(int nq, int nv, int nu, int imitation, int task, duck_layout* out);
 /* size in floats of the per-env debug record written by duck_physics_step(aux) */
 int duck_aux_size(const duck_sim* sim);
 /* debug: per-stage cycle counters of a -DDUCK_STAGE_PROF build (16 x uint64, optionally

@@ -1,7 +1,8 @@
-/* duck_env.h — Joystick env configuration and per-env state layout (C ABI).
+/* duck_env.h — Joystick / Standing env configuration and per-env state layout (C ABI).
  *
  * Mirrors the reference's env surface:
  *   default_config()            playground/open_duck_mini_v2/joystick.py:49-102
+ *                               (standing.py:44-100 for the Standing task)
  *   State.info / State.metrics  joystick.py:278-311 (reset) and :449-477 (step)
  *   obs["state"] (101)          joystick.py:570-589
  *   obs["privileged_state"]     joystick.py:596-615 (172, or 212 with imitation)
@@ -20,16 +21,27 @@
 extern "C" {
 #endif
 
+/* tasks: Joystick (joystick.py) and Standing (standing.py); same model, physics and info */
+enum { DUCK_TASK_JOYSTICK = 0, DUCK_TASK_STANDING = 1 };
+
+/* Joystick state: gyro, accel, command, q, qd, 3 last actions, motor targets, contact, phase */
 #define DUCK_OBS_SIZE(nu) (3 + 3 + 7 + 6 * (nu) + 2 + 2)
+/* Standing state (standing.py:532-548): no motor targets, no phase */
+#define DUCK_STANDING_OBS_SIZE(nu) (3 + 3 + 7 + 5 * (nu) + 2)
 #define DUCK_NMETRICS 8
 /* metric order = reward dict order of joystick.py:634-667, then swing_peak (:477) */
 enum {
   DUCK_M_TRACKING_LIN_VEL = 0, DUCK_M_TRACKING_ANG_VEL, DUCK_M_TORQUES, DUCK_M_ACTION_RATE,
   DUCK_M_ALIVE, DUCK_M_IMITATION, DUCK_M_STAND_STILL, DUCK_M_SWING_PEAK
 };
+/* Standing metric order = reward dict order of standing.py:584-606 (slot 6 unused) */
+enum {
+  DUCK_MS_ORIENTATION = 0, DUCK_MS_TORQUES, DUCK_MS_ACTION_RATE, DUCK_MS_ALIVE, DUCK_MS_STAND_STILL,
+  DUCK_MS_HEAD_POS
+};
 
 typedef struct duck_layout {
-  int nq, nv, nu, imitation, obs_size, priv_size;
+  int nq, nv, nu, imitation, task, obs_size, priv_size;
   /* float fields */
   int qpos, qvel, qacc_warmstart, ctrl;
   int command, last_act, last_last_act, last_last_last_act, motor_targets;
@@ -42,12 +54,18 @@ typedef struct duck_layout {
   int nint;
 } duck_layout;
 
-static inline duck_layout duck_layout_make(int nq, int nv, int nu, int imitation) {
+static inline duck_layout duck_layout_make(int nq, int nv, int nu, int imitation, int task) {
   duck_layout L;
   int o = 0;
-  L.nq = nq; L.nv = nv; L.nu = nu; L.imitation = imitation ? 1 : 0;
-  L.obs_size = DUCK_OBS_SIZE(nu);
-  L.priv_size = L.obs_size + 15 + 2 * nu + 1 + nu + 2 + 6 + 2 + (L.imitation ? 40 : 0) + 1 + 2;
+  L.nq = nq; L.nv = nv; L.nu = nu; L.task = task;
+  L.imitation = (imitation && task == DUCK_TASK_JOYSTICK) ? 1 : 0; /* standing.py:42 */
+  if (task == DUCK_TASK_STANDING) {
+    L.obs_size = DUCK_STANDING_OBS_SIZE(nu);
+    L.priv_size = L.obs_size + 15 + 2 * nu + 1 + nu + 2 + 6 + 2; /* standing.py:555-570 */
+  } else {
+    L.obs_size = DUCK_OBS_SIZE(nu);
+    L.priv_size = L.obs_size + 15 + 2 * nu + 1 + nu + 2 + 6 + 2 + (L.imitation ? 40 : 0) + 1 + 2;
+  }
   L.qpos = o; o += nq;
   L.qvel = o; o += nv;
   L.qacc_warmstart = o; o += nv;
@@ -115,6 +133,10 @@ typedef struct duck_env_config {
   int sens_gyro, sens_accelerometer, sens_upvector, sens_local_linvel, sens_global_angvel,
       sens_left_foot_linvel, sens_right_foot_linvel;
   int domain_randomize;
+  /* Standing task (standing.py): reset base velocity range U(+-0.5) and zero motor targets
+   * (:247-249, :279), reward terms orientation and head_pos (:584-606) */
+  int task;
+  float scale_orientation, scale_head_pos;
 } duck_env_config;
 
 /* reference-motion table (poly_reference_motion.py:74-146). get_reference_motion only

@@ -81,6 +81,7 @@ class DuckEnvConfig(C.Structure):
         ("sens_local_linvel", C.c_int), ("sens_global_angvel", C.c_int), ("sens_left_foot_linvel", C.c_int),
         ("sens_right_foot_linvel", C.c_int),
         ("domain_randomize", C.c_int),
+        ("task", C.c_int), ("scale_orientation", C.c_float), ("scale_head_pos", C.c_float),
     ]
 
 
@@ -178,6 +179,7 @@ class Layout:
     nv: int
     nu: int
     imitation: int
+    task: int
     off: Dict[str, int]
     ioff: Dict[str, int]
     nfloat: int
@@ -186,9 +188,17 @@ class Layout:
     priv_size: int
 
 
-def layout(nq: int, nv: int, nu: int, imitation: bool) -> Layout:
-    obs = 3 + 3 + 7 + 6 * nu + 2 + 2
-    priv = obs + 15 + 2 * nu + 1 + nu + 2 + 6 + 2 + (40 if imitation else 0) + 1 + 2
+TASK_JOYSTICK, TASK_STANDING = 0, 1
+
+
+def layout(nq: int, nv: int, nu: int, imitation: bool, task: int = TASK_JOYSTICK) -> Layout:
+    imitation = bool(imitation) and task == TASK_JOYSTICK
+    if task == TASK_STANDING:  # standing.py:532-570
+        obs = 3 + 3 + 7 + 5 * nu + 2
+        priv = obs + 15 + 2 * nu + 1 + nu + 2 + 6 + 2
+    else:
+        obs = 3 + 3 + 7 + 6 * nu + 2 + 2
+        priv = obs + 15 + 2 * nu + 1 + nu + 2 + 6 + 2 + (40 if imitation else 0) + 1 + 2
     fields = [("qpos", nq), ("qvel", nv), ("qacc_warmstart", nv), ("ctrl", nu), ("command", 7), ("last_act", nu),
               ("last_last_act", nu), ("last_last_last_act", nu), ("motor_targets", nu), ("feet_air_time", 2),
               ("last_contact", 2), ("swing_peak", 2), ("push", 2), ("action_history", 3 * nu), ("imu_history", 9),
@@ -205,7 +215,7 @@ def layout(nq: int, nv: int, nu: int, imitation: bool) -> Layout:
     for k, n in ifields:
         ioff[k] = io
         io += n
-    return Layout(nq, nv, nu, int(bool(imitation)), off, ioff, o, io, obs, priv)
+    return Layout(nq, nv, nu, int(imitation), int(task), off, ioff, o, io, obs, priv)
 
 
 def dr_layout(nbody: int, nu: int) -> Dict[str, int]:
@@ -220,3 +230,6 @@ def dr_layout(nbody: int, nu: int) -> Dict[str, int]:
 
 METRIC_NAMES = ["reward/tracking_lin_vel", "reward/tracking_ang_vel", "cost/torques", "cost/action_rate",
                 "reward/alive", "reward/imitation", "cost/stand_still", "swing_peak"]
+# standing.py:290-297 + :584-606 (slot 6 unused; swing_peak stays in slot 7)
+STANDING_METRIC_NAMES = ["cost/orientation", "cost/torques", "cost/action_rate", "reward/alive", "cost/stand_still",
+                         "cost/head_pos", None, "swing_peak"]

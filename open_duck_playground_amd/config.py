@@ -91,6 +91,40 @@ def default_config() -> ConfigDict:
     )
 
 
+def standing_default_config() -> ConfigDict:
+    """Same keys/defaults as standing.default_config (standing.py:44-100)."""
+    return create(
+        ctrl_dt=0.02,
+        sim_dt=0.002,
+        episode_length=1000,
+        action_repeat=1,
+        action_scale=0.25,
+        dof_vel_scale=0.05,
+        history_len=0,
+        soft_joint_pos_limit_factor=0.95,
+        noise_config=create(
+            level=1.0,
+            action_min_delay=0,
+            action_max_delay=3,
+            imu_min_delay=0,
+            imu_max_delay=3,
+            scales=create(hip_pos=0.03, knee_pos=0.05, ankle_pos=0.08, joint_vel=2.5, gravity=0.1, linvel=0.1,
+                          gyro=0.05, accelerometer=0.005),
+        ),
+        reward_config=create(
+            scales=create(orientation=-0.5, torques=-1.0e-3, action_rate=-0.375, stand_still=-0.3, alive=20.0,
+                          head_pos=-2.0),
+            tracking_sigma=0.01,
+        ),
+        push_config=create(enable=True, interval_range=[5.0, 10.0], magnitude_range=[0.1, 1.0]),
+        neck_pitch_range=[-0.34, 1.1],
+        head_pitch_range=[-0.78, 0.78],
+        head_yaw_range=[-2.7, 2.7],
+        head_roll_range=[-0.5, 0.5],
+        head_range_factor=1.0,
+    )
+
+
 def qpos_noise_scale(config: ConfigDict, nu: int) -> np.ndarray:
     """Bug-compatible joint-noise scales (joystick.py:184-200): indices come from the
     10-joint JOINTS_ORDER_NO_HEAD list but index the nu-long actuator vector."""
@@ -132,8 +166,12 @@ class AddressMaps:
 
 
 def env_config_struct(m: Model, config: ConfigDict, use_imitation: bool, auto_reset: bool = False,
-                      domain_randomize: bool = False) -> DuckEnvConfig:
+                      domain_randomize: bool = False, task: int = 0) -> DuckEnvConfig:
+    """task 0 = Joystick (joystick.py), 1 = Standing (standing.py: no imitation, no motor speed
+    limits, zero walking command, orientation + head_pos terms)."""
     c = DuckEnvConfig()
+    standing = task == 1
+    c.task = int(task)
     maps = AddressMaps(m)
     nu = m.nu
     c.ctrl_dt = config.ctrl_dt
@@ -143,9 +181,9 @@ def env_config_struct(m: Model, config: ConfigDict, use_imitation: bool, auto_re
     c.auto_reset = int(auto_reset)
     c.action_scale = config.action_scale
     c.dof_vel_scale = config.dof_vel_scale
-    c.max_motor_velocity = config.max_motor_velocity
-    c.use_imitation = int(use_imitation)
-    c.use_motor_speed_limits = int(USE_MOTOR_SPEED_LIMITS)
+    c.max_motor_velocity = config.get("max_motor_velocity", 0.0)
+    c.use_imitation = int(use_imitation and not standing)
+    c.use_motor_speed_limits = int(USE_MOTOR_SPEED_LIMITS and not standing)
     nc = config.noise_config
     c.noise_level = nc.level
     c.action_min_delay, c.action_max_delay = int(nc.action_min_delay), int(nc.action_max_delay)
@@ -156,20 +194,17 @@ def env_config_struct(m: Model, config: ConfigDict, use_imitation: bool, auto_re
     c.noise_joint_vel = nc.scales.joint_vel
     c.qpos_noise_scale[:nu] = [float(x) for x in qpos_noise_scale(config, nu)]
     sc = config.reward_config.scales
-    c.scale_tracking_lin_vel = sc.tracking_lin_vel
-    c.scale_tracking_ang_vel = sc.tracking_ang_vel
-    c.scale_torques = sc.torques
-    c.scale_action_rate = sc.action_rate
-    c.scale_alive = sc.alive
-    c.scale_imitation = sc.imitation
-    c.scale_stand_still = sc.stand_still
+    for k in ("tracking_lin_vel", "tracking_ang_vel", "torques", "action_rate", "alive", "imitation",
+              "stand_still", "orientation", "head_pos"):
+        setattr(c, "scale_" + k, float(sc.get(k, 0.0)))
     c.tracking_sigma = config.reward_config.tracking_sigma
     c.push_enable = int(bool(config.push_config.enable))
     c.push_interval_range[:] = list(config.push_config.interval_range)
     c.push_magnitude_range[:] = list(config.push_config.magnitude_range)
     for k in ("lin_vel_x", "lin_vel_y", "ang_vel_yaw", "neck_pitch_range", "head_pitch_range", "head_yaw_range",
               "head_roll_range"):
-        getattr(c, k)[:] = list(config[k])
+        # Standing samples no walking command (standing.py:614-655): U(0, 0) draws 0.0 exactly
+        getattr(c, k)[:] = list(config.get(k, [0.0, 0.0]))
     c.head_range_factor = config.head_range_factor
     key = m.names["key"].index("home")
     c.default_actuator[:nu] = [float(x) for x in m.key_ctrl[key]]

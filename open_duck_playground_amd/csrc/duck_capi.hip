@@ -23,9 +23,9 @@ extern "C" {
 int duck_version(void) { return DUCK_VERSION; }
 const char* duck_last_error(void) { return g_err.c_str(); }
 
-int duck_layout_get(int nq, int nv, int nu, int imitation, duck_layout* out) {
+int duck_layout_get(int nq, int nv, int nu, int imitation, int task, duck_layout* out) {
   if (!out) return duck_fail(DUCK_EINVAL, "null out");
-  *out = duck_layout_make(nq, nv, nu, imitation);
+  *out = duck_layout_make(nq, nv, nu, imitation, task);
   return DUCK_OK;
 }
 
@@ -62,7 +62,7 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
   s->variant = v;
   s->cfg = *cfg;
   s->nq = model->nq; s->nv = model->nv; s->nu = model->nu;
-  s->lay = duck_layout_make(model->nq, model->nv, model->nu, cfg->use_imitation);
+  s->lay = duck_layout_make(model->nq, model->nv, model->nu, cfg->use_imitation, cfg->task);
   s->drl = duck_dr_layout_make(model->nbody, model->nu);
   if (ref) {
     if (ref->n_dim != 40 || ref->n_dx > 16 || ref->n_dy > 16 || ref->n_dtheta > 16 || ref->nb_steps_in_period < 1 ||

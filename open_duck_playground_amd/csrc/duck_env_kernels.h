@@ -181,7 +181,8 @@ DK void load_dyn(const KArgs& A, int e, Slice<WG> L) {
   }
 }
 
-// Joystick._get_obs (joystick.py:487-620); reads the last forward's outputs from the slice
+// Joystick._get_obs (joystick.py:487-620) / Standing._get_obs (standing.py:462-575); reads the
+// last forward's outputs from the slice
 template <class Md, int WG>
 DK void write_obs(const KArgs& A, int e, Slice<WG> L, const Rng& r, int slot_base,
                                        int imitation_i) {
@@ -229,11 +230,15 @@ DK void write_obs(const KArgs& A, int e, Slice<WG> L, const Rng& r, int slot_bas
   for (int a = 0; a < NU; a++) put(F[Lo.last_act + a]);
   for (int a = 0; a < NU; a++) put(F[Lo.last_last_act + a]);
   for (int a = 0; a < NU; a++) put(F[Lo.last_last_last_act + a]);
-  for (int a = 0; a < NU; a++) put(F[Lo.motor_targets + a]);
+  const bool joystick = Lo.task == DUCK_TASK_JOYSTICK;
+  if (joystick)
+    for (int a = 0; a < NU; a++) put(F[Lo.motor_targets + a]);
   put(L[Ly::OCON]);
   put(L[Ly::OCON + 1]);
-  put(F[Lo.imitation_phase]);
-  put(F[Lo.imitation_phase + 1]);
+  if (joystick) {
+    put(F[Lo.imitation_phase]);
+    put(F[Lo.imitation_phase + 1]);
+  }
   int p = o;
   auto pp = [&](float v) { priv[p++] = v; };
 #pragma unroll
@@ -264,9 +269,11 @@ DK void write_obs(const KArgs& A, int e, Slice<WG> L, const Rng& r, int slot_bas
   pp(F[Lo.feet_air_time + 1]);
   if (Lo.imitation)
     for (int k = 0; k < 40; k++) pp(F[Lo.ref_motion + k]);
-  pp((float)imitation_i);
-  pp(F[Lo.imitation_phase]);
-  pp(F[Lo.imitation_phase + 1]);
+  if (joystick) {
+    pp((float)imitation_i);
+    pp(F[Lo.imitation_phase]);
+    pp(F[Lo.imitation_phase + 1]);
+  }
 }
 
 template <class Md, int WG>
@@ -312,7 +319,9 @@ __global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
     for (int k = 0; k < 4; k++) L[Ly::QPOS + 3 + k] = q[k];
   }
   for (int a = 0; a < NU; a++) L[Ly::QPOS + c.actuator_qposadr[a]] *= r.uniform(RSLOT_QSCALE + a, 0.5f, 1.5f);
-  for (int k = 0; k < 6; k++) L[Ly::QVEL + k] = r.uniform(RSLOT_QVEL + k, -0.05f, 0.05f);
+  // base velocity U(+-0.05) (joystick.py:247-249); U(+-0.5) for Standing (standing.py:247-249)
+  const float vr = Lo.task == DUCK_TASK_STANDING ? 0.5f : 0.05f;
+  for (int k = 0; k < 6; k++) L[Ly::QVEL + k] = r.uniform(RSLOT_QVEL + k, -vr, vr);
   for (int a = 0; a < NU; a++) L[Ly::CTRL + a] = L[Ly::QPOS + c.actuator_qposadr[a]];
   phys_step<Md>(L, lane, false, true, nullptr, 0, A.scratch ? A.scratch + e : nullptr, A.n, A.hfield);
   float cmd[7];
@@ -323,7 +332,8 @@ __global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
   iset(Lo.rng_key + 1, (int32_t)r.k1);
   iset(Lo.rng_ctr, 1);
   for (int k = 0; k < 7; k++) F[Lo.command + k] = cmd[k];
-  for (int a = 0; a < NU; a++) F[Lo.motor_targets + a] = c.default_actuator[a];
+  // info["motor_targets"]: home ctrl (joystick.py:285) / zeros (standing.py:279)
+  for (int a = 0; a < NU; a++) F[Lo.motor_targets + a] = Lo.task == DUCK_TASK_STANDING ? 0.0f : c.default_actuator[a];
   if (Lo.imitation) {
     float ref[40];
     reference_motion(A, cmd[0], cmd[1], cmd[2], 0, ref);
@@ -476,9 +486,38 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
     rr *= cn > 0.01f ? 1.0f : 0.0f;
     imit = nan_to_num(rr);
   }
-  const float terms[7] = {r_lin * c.scale_tracking_lin_vel, r_ang * c.scale_tracking_ang_vel,
-                          nan_to_num(torq) * c.scale_torques, nan_to_num(arate) * c.scale_action_rate,
-                          1.0f * c.scale_alive, imit * c.scale_imitation, r_still * c.scale_stand_still};
+  float terms[7];
+  if (Lo.task == DUCK_TASK_STANDING) {
+    // Standing._get_reward (standing.py:584-606): orientation, torques, action_rate, alive,
+    // stand_still(ignore_head=True), head_pos (common/rewards.py:45-46,93-117,131-147)
+    const float ux = L[Ly::SENS + c.sens_upvector], uy = L[Ly::SENS + c.sens_upvector + 1];
+    float lpc = 0.0f, lvc = 0.0f, hp = 0.0f;
+    for (int a = 0; a < NU; a++) {
+      const float q = L[Ly::QPOS + c.actuator_qposadr[a]];
+      if (a < 5 || a >= NU - 5) {  // legs: qpos[:5] and qpos[9:]
+        lpc += fabsf(q - c.default_actuator[a]);
+        lvc += fabsf(L[Ly::QVEL + c.actuator_qveladr[a]]);
+      } else {  // head joints qpos[5:9] vs cmd[3:]
+        const float d = q - cmd[3 + a - 5];
+        hp += d * d;
+      }
+    }
+    terms[0] = nan_to_num(ux * ux + uy * uy) * c.scale_orientation;
+    terms[1] = nan_to_num(torq) * c.scale_torques;
+    terms[2] = nan_to_num(arate) * c.scale_action_rate;
+    terms[3] = 1.0f * c.scale_alive;
+    terms[4] = nan_to_num(lpc + lvc) * (cn < 0.01f ? 1.0f : 0.0f) * c.scale_stand_still;
+    terms[5] = nan_to_num(hp) * (cn > 0.01f ? 1.0f : 0.0f) * c.scale_head_pos;
+    terms[6] = 0.0f;
+  } else {
+    terms[0] = r_lin * c.scale_tracking_lin_vel;
+    terms[1] = r_ang * c.scale_tracking_ang_vel;
+    terms[2] = nan_to_num(torq) * c.scale_torques;
+    terms[3] = nan_to_num(arate) * c.scale_action_rate;
+    terms[4] = 1.0f * c.scale_alive;
+    terms[5] = imit * c.scale_imitation;
+    terms[6] = r_still * c.scale_stand_still;
+  }
   float sum = 0.0f;
   for (int k = 0; k < 7; k++) sum += terms[k];
   const float reward = fminf(fmaxf(sum * dt, 0.0f), 10000.0f);
@@ -505,8 +544,15 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
     F[Lo.last_contact + k] = con[k];
     F[Lo.swing_peak + k] = F[Lo.swing_peak + k] * (con[k] != 0.0f ? 0.0f : 1.0f);
   }
-  const float scales[7] = {c.scale_tracking_lin_vel, c.scale_tracking_ang_vel, c.scale_torques, c.scale_action_rate,
-                           c.scale_alive, c.scale_imitation, c.scale_stand_still};
+  // metrics: reward/<k> = term, cost/<k> = -term (joystick.py:467-474, standing.py:424-431)
+  const bool standing = Lo.task == DUCK_TASK_STANDING;
+  const float scales[7] = {standing ? c.scale_orientation : c.scale_tracking_lin_vel,
+                           standing ? c.scale_torques : c.scale_tracking_ang_vel,
+                           standing ? c.scale_action_rate : c.scale_torques,
+                           standing ? c.scale_alive : c.scale_action_rate,
+                           standing ? c.scale_stand_still : c.scale_alive,
+                           standing ? c.scale_head_pos : c.scale_imitation,
+                           standing ? 0.0f : c.scale_stand_still};
   for (int k = 0; k < 7; k++) F[Lo.metrics + k] = scales[k] > 0.0f ? terms[k] : -terms[k];
   F[Lo.metrics + DUCK_M_SWING_PEAK] = 0.5f * (F[Lo.swing_peak] + F[Lo.swing_peak + 1]);
   iset(Lo.rng_ctr, (int32_t)(r.ctr + 1));

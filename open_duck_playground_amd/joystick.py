@@ -29,7 +29,7 @@ import torch
 
 from . import config as cfgmod
 from . import constants
-from .cabi import METRIC_NAMES, ModelDescHolder, dr_layout, layout, refmotion_struct
+from .cabi import METRIC_NAMES, TASK_JOYSTICK, ModelDescHolder, dr_layout, layout, refmotion_struct
 from .config import ConfigDict, default_config  # noqa: F401  (re-exported like the reference module)
 from .mjcf import JNT_FREE, Model
 from .native import DuckError, check, lib
@@ -144,6 +144,9 @@ class OpenDuckMiniV2Env:
 class Joystick(OpenDuckMiniV2Env):
     """Track a joystick command (joystick.py:105-725), batched on one MI355X."""
 
+    TASK = TASK_JOYSTICK
+    METRICS = METRIC_NAMES
+
     def __init__(self, task: str = "flat_terrain", config: ConfigDict = None,
                  config_overrides: Optional[Dict[str, Union[str, int, list]]] = None, num_envs: int = 1,
                  device: Union[str, torch.device] = "cuda:0", use_imitation: Optional[bool] = None,
@@ -182,14 +185,14 @@ class Joystick(OpenDuckMiniV2Env):
         self._floor_geom_id = m.id("geom", "floor")
         self._feet_geom_id = np.array([m.id("geom", g) for g in constants.FEET_GEOMS])
         self._qpos_noise_scale = cfgmod.qpos_noise_scale(self._config, m.nu)
-        self._layout = layout(m.nq, m.nv, m.nu, self.use_imitation)
+        self._layout = layout(m.nq, m.nv, m.nu, self.use_imitation, self.TASK)
         self._create_sim()
 
     def _create_sim(self) -> None:
         m = self._mj_model
         self._desc = ModelDescHolder(m)
         self._cfg_struct = cfgmod.env_config_struct(m, self._config, self.use_imitation, self.auto_reset,
-                                                    self.dr is not None)
+                                                    self.dr is not None, task=self.TASK)
         table = dict(np.load(constants.POLY_COEFFICIENTS, allow_pickle=False))
         self._ref_struct, self._ref_coeffs = refmotion_struct(table)
         handle = C.c_void_p()
@@ -249,7 +252,7 @@ class Joystick(OpenDuckMiniV2Env):
         if self.auto_reset:
             info["steps"] = iv("ep_steps")
             info["truncation"] = F[L.off["truncation"]]
-        metrics = {name: F[L.off["metrics"] + k] for k, name in enumerate(METRIC_NAMES)}
+        metrics = {name: F[L.off["metrics"] + k] for k, name in enumerate(self.METRICS) if name}
         return State(data=data, obs={"state": obs, "privileged_state": priv}, reward=reward, done=done,
                      metrics=metrics, info=info, fstate=fstate, istate=istate)
 

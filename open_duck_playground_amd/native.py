@@ -28,7 +28,7 @@ class DuckError(RuntimeError):
 
 class DuckLayout(C.Structure):
     _fields_ = [(k, C.c_int) for k in (
-        "nq", "nv", "nu", "imitation", "obs_size", "priv_size",
+        "nq", "nv", "nu", "imitation", "task", "obs_size", "priv_size",
         "qpos", "qvel", "qacc_warmstart", "ctrl", "command", "last_act", "last_last_act", "last_last_last_act",
         "motor_targets", "feet_air_time", "last_contact", "swing_peak", "push", "action_history", "imu_history",
         "ref_motion", "imitation_phase", "metrics", "reward", "done", "truncation", "first_qpos", "first_qvel",
@@ -83,7 +83,7 @@ def lib():
         vp = C.c_void_p
         L.duck_version.restype = C.c_int
         L.duck_last_error.restype = C.c_char_p
-        L.duck_layout_get.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(DuckLayout)]
+        L.duck_layout_get.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(DuckLayout)]
         L.duck_aux_size.argtypes = [vp]
         L.duck_create.argtypes = [C.POINTER(DuckModelDesc), C.POINTER(DuckEnvConfig), C.POINTER(DuckRefMotion), C.c_int,
                                   C.POINTER(vp)]

@@ -1441,6 +1441,35 @@ void oracle_rewards(const double cmd[7], const double lv[3], const double gyro[3
   out[4] = nan_to_num(pc + vc) * (cn < 0.01 ? 1.0 : 0.0);
 }
 
+/* Standing reward terms, unscaled (standing.py:584-606 via common/rewards.py):
+ * out = {orientation (:45-46), torques, action_rate, alive, stand_still(ignore_head=True) (:93-117),
+ *        head_pos (:131-147)} */
+void oracle_standing_rewards(const double cmd[7], const double up[3], const double* af, const double* action,
+                             const double* last_act, const double* jq, const double* jqd, const double* q0, int nu,
+                             double out[6]) {
+  double t = 0, a = 0, pc = 0, vc = 0, hp = 0;
+  for (int k = 0; k < nu; k++) {
+    t += af[k] * af[k];
+    a += (action[k] - last_act[k]) * (action[k] - last_act[k]);
+  }
+  for (int k = 0; k < 5; k++) { /* legs: qpos[:5] and qpos[9:] */
+    pc += fabs(jq[k] - q0[k]);
+    vc += fabs(jqd[k]);
+  }
+  for (int k = nu - 5; k < nu; k++) {
+    pc += fabs(jq[k] - q0[k]);
+    vc += fabs(jqd[k]);
+  }
+  for (int k = 0; k < 4; k++) hp += (jq[5 + k] - cmd[3 + k]) * (jq[5 + k] - cmd[3 + k]);
+  double cn = sqrt(cmd[0] * cmd[0] + cmd[1] * cmd[1] + cmd[2] * cmd[2]);
+  out[0] = nan_to_num(up[0] * up[0] + up[1] * up[1]);
+  out[1] = nan_to_num(t);
+  out[2] = nan_to_num(a);
+  out[3] = 1.0;
+  out[4] = nan_to_num(pc + vc) * (cn < 0.01 ? 1.0 : 0.0);
+  out[5] = nan_to_num(hp) * (cn > 0.01 ? 1.0 : 0.0);
+}
+
 /* Joystick.sample_command (joystick.py:671-725) */
 static void sample_command(const duck_env_config* cfg, const rng_t* r, int slot, double cmd[7]) {
   double f = cfg->head_range_factor;
@@ -1509,11 +1538,15 @@ static void get_obs(const oracle_model* m, const duck_env_config* cfg, const duc
   for (int a = 0; a < nu; a++) obs[o++] = fs[L->last_act + a];
   for (int a = 0; a < nu; a++) obs[o++] = fs[L->last_last_act + a];
   for (int a = 0; a < nu; a++) obs[o++] = fs[L->last_last_last_act + a];
-  for (int a = 0; a < nu; a++) obs[o++] = fs[L->motor_targets + a];
+  int joystick = L->task == DUCK_TASK_JOYSTICK; /* standing.py:532-548 has no targets, no phase */
+  if (joystick)
+    for (int a = 0; a < nu; a++) obs[o++] = fs[L->motor_targets + a];
   obs[o++] = contact[0];
   obs[o++] = contact[1];
-  obs[o++] = fs[L->imitation_phase];
-  obs[o++] = fs[L->imitation_phase + 1];
+  if (joystick) {
+    obs[o++] = fs[L->imitation_phase];
+    obs[o++] = fs[L->imitation_phase + 1];
+  }
   /* privileged */
   int p = 0;
   for (int k = 0; k < o; k++) priv[p++] = obs[k];
@@ -1534,9 +1567,11 @@ static void get_obs(const oracle_model* m, const duck_env_config* cfg, const duc
   priv[p++] = fs[L->feet_air_time + 1];
   if (L->imitation)
     for (int k = 0; k < 40; k++) priv[p++] = fs[L->ref_motion + k];
-  priv[p++] = 0; /* imitation_i, filled by caller */
-  priv[p++] = fs[L->imitation_phase];
-  priv[p++] = fs[L->imitation_phase + 1];
+  if (joystick) {
+    priv[p++] = 0; /* imitation_i, filled by caller */
+    priv[p++] = fs[L->imitation_phase];
+    priv[p++] = fs[L->imitation_phase + 1];
+  }
 }
 
 static void load_data(const duck_layout* L, const double* fs, oracle_data* d) {
@@ -1553,10 +1588,11 @@ static void store_data(const duck_layout* L, const oracle_data* d, double* fs) {
   memcpy(fs + L->ctrl, d->ctrl, sizeof(double) * L->nu);
 }
 
-/* Joystick.reset (joystick.py:206-321) */
+/* Joystick.reset (joystick.py:206-321); Standing.reset (standing.py:200-321) differs in the
+ * base velocity range and the initial motor targets */
 int oracle_env_reset(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref, uint64_t seed,
                      int64_t env_id, double* fs, int32_t* is, double* obs, double* priv) {
-  duck_layout L = duck_layout_make(m->nq, m->nv, m->nu, cfg->use_imitation);
+  duck_layout L = duck_layout_make(m->nq, m->nv, m->nu, cfg->use_imitation, cfg->task);
   int nu = m->nu;
   memset(fs, 0, sizeof(double) * L.nfloat);
   memset(is, 0, sizeof(int32_t) * L.nint);
@@ -1573,7 +1609,8 @@ int oracle_env_reset(const oracle_model* m, const duck_env_config* cfg, const du
   axis_angle_quat(qy, zax, yaw);
   quat_mul(d.qpos + 3, d.qpos + 3, qy);
   for (int a = 0; a < nu; a++) d.qpos[cfg->actuator_qposadr[a]] *= rng_uniform(&r, RSLOT_QSCALE + a, 0.5, 1.5);
-  for (int k = 0; k < 6; k++) d.qvel[k] = rng_uniform(&r, RSLOT_QVEL + k, -0.05, 0.05);
+  double vr = L.task == DUCK_TASK_STANDING ? 0.5 : 0.05;
+  for (int k = 0; k < 6; k++) d.qvel[k] = rng_uniform(&r, RSLOT_QVEL + k, -vr, vr);
   for (int a = 0; a < nu; a++) d.ctrl[a] = d.qpos[cfg->actuator_qposadr[a]];
   oracle_forward(m, &d); /* mjx_env.init -> mjx.forward */
   double cmd[7];
@@ -1584,13 +1621,13 @@ int oracle_env_reset(const oracle_model* m, const duck_env_config* cfg, const du
   is[L.rng_key + 1] = (int32_t)r.key[1];
   is[L.rng_ctr] = 1;
   for (int k = 0; k < 7; k++) fs[L.command + k] = cmd[k];
-  for (int a = 0; a < nu; a++) fs[L.motor_targets + a] = cfg->default_actuator[a];
+  for (int a = 0; a < nu; a++) fs[L.motor_targets + a] = L.task == DUCK_TASK_STANDING ? 0.0 : cfg->default_actuator[a];
   if (L.imitation) oracle_reference_motion(ref, cmd[0], cmd[1], cmd[2], 0, fs + L.ref_motion);
   store_data(&L, &d, fs);
   double contact[2] = {geoms_colliding(&d, cfg->left_foot_geom, cfg->floor_geom),
                        geoms_colliding(&d, cfg->right_foot_geom, cfg->floor_geom)};
   get_obs(m, cfg, &L, &d, fs, &r, RSLOT_OBS, contact, obs, priv);
-  priv[L.priv_size - 3] = is[L.imitation_i];
+  if (L.task == DUCK_TASK_JOYSTICK) priv[L.priv_size - 3] = is[L.imitation_i];
   /* AutoReset first-state snapshot */
   memcpy(fs + L.first_qpos, fs + L.qpos, sizeof(double) * m->nq);
   memcpy(fs + L.first_qvel, fs + L.qvel, sizeof(double) * m->nv);
@@ -1605,7 +1642,7 @@ int oracle_env_reset(const oracle_model* m, const duck_env_config* cfg, const du
 int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref, double* fs,
                     int32_t* is, const double* action, double* obs, double* priv, double* reward_out,
                     double* done_out, oracle_data* d_out) {
-  duck_layout L = duck_layout_make(m->nq, m->nv, m->nu, cfg->use_imitation);
+  duck_layout L = duck_layout_make(m->nq, m->nv, m->nu, cfg->use_imitation, cfg->task);
   int nu = m->nu;
   double dt = cfg->ctrl_dt;
   if (cfg->auto_reset) {
@@ -1668,7 +1705,7 @@ int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duc
   }
   store_data(&L, d, fs);
   get_obs(m, cfg, &L, d, fs, &r, 0, contact, obs, priv);
-  priv[L.priv_size - 3] = is[L.imitation_i];
+  if (L.task == DUCK_TASK_JOYSTICK) priv[L.priv_size - 3] = is[L.imitation_i];
   /* termination (:483-485) */
   int nan = 0;
   for (int i = 0; i < m->nq; i++) nan |= isnan(d->qpos[i]);
@@ -1695,6 +1732,19 @@ int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duc
   double terms[7] = {rr[0] * cfg->scale_tracking_lin_vel, rr[1] * cfg->scale_tracking_ang_vel,
                      rr[2] * cfg->scale_torques, rr[3] * cfg->scale_action_rate, 1.0 * cfg->scale_alive,
                      imit * cfg->scale_imitation, rr[4] * cfg->scale_stand_still};
+  double scales[7] = {cfg->scale_tracking_lin_vel, cfg->scale_tracking_ang_vel, cfg->scale_torques,
+                      cfg->scale_action_rate, cfg->scale_alive, cfg->scale_imitation, cfg->scale_stand_still};
+  if (L.task == DUCK_TASK_STANDING) {
+    /* Standing._get_reward (standing.py:584-606) */
+    double st[6];
+    oracle_standing_rewards(cmd, d->sensordata + cfg->sens_upvector, d->actuator_force, act, la, jq, jqd, q0, nu, st);
+    double ss[7] = {cfg->scale_orientation, cfg->scale_torques, cfg->scale_action_rate, cfg->scale_alive,
+                    cfg->scale_stand_still, cfg->scale_head_pos, 0.0};
+    for (int k = 0; k < 7; k++) {
+      scales[k] = ss[k];
+      terms[k] = k < 6 ? st[k] * ss[k] : 0.0;
+    }
+  }
   double sum = 0;
   for (int k = 0; k < 7; k++) sum += terms[k];
   double reward = fmin(fmax(sum * dt, 0.0), 10000.0);
@@ -1718,8 +1768,6 @@ int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duc
     fs[L.last_contact + k] = contact[k];
     fs[L.swing_peak + k] *= contact[k] ? 0.0 : 1.0;
   }
-  double scales[7] = {cfg->scale_tracking_lin_vel, cfg->scale_tracking_ang_vel, cfg->scale_torques,
-                      cfg->scale_action_rate, cfg->scale_alive, cfg->scale_imitation, cfg->scale_stand_still};
   for (int k = 0; k < 7; k++) fs[L.metrics + k] = scales[k] > 0 ? terms[k] : -terms[k];
   fs[L.metrics + DUCK_M_SWING_PEAK] = 0.5 * (fs[L.swing_peak] + fs[L.swing_peak + 1]);
   is[L.rng_ctr] = (int32_t)(r.ctr + 1);
@@ -1753,7 +1801,7 @@ int oracle_batch_reset(const oracle_model* const* models, int n_models, const du
                        const duck_refmotion* ref, int n, uint64_t seed, int64_t env_offset, double* fstate,
                        int32_t* istate, double* obs, double* priv, int n_threads) {
   const oracle_model* m0 = models[0];
-  duck_layout L = duck_layout_make(m0->nq, m0->nv, m0->nu, cfg->use_imitation);
+  duck_layout L = duck_layout_make(m0->nq, m0->nv, m0->nu, cfg->use_imitation, cfg->task);
 #ifdef _OPENMP
   if (n_threads > 0) omp_set_num_threads(n_threads);
 #pragma omp parallel for schedule(static)
@@ -1774,7 +1822,7 @@ int oracle_batch_step(const oracle_model* const* models, int n_models, const duc
                       const duck_refmotion* ref, int n, double* fstate, int32_t* istate, const double* actions,
                       double* obs, double* priv, double* reward, double* done, int n_threads) {
   const oracle_model* m0 = models[0];
-  duck_layout L = duck_layout_make(m0->nq, m0->nv, m0->nu, cfg->use_imitation);
+  duck_layout L = duck_layout_make(m0->nq, m0->nv, m0->nu, cfg->use_imitation, cfg->task);
 #ifdef _OPENMP
   if (n_threads > 0) omp_set_num_threads(n_threads);
 #pragma omp parallel for schedule(static)

@@ -81,6 +81,9 @@ void oracle_rewards(const double cmd[7], const double local_linvel[3], const dou
                     const double* actuator_force, const double* action, const double* last_act,
                     const double* joints_qpos, const double* joints_qvel, const double* default_act, int nu,
                     double tracking_sigma, double out[5]);
+void oracle_standing_rewards(const double cmd[7], const double upvector[3], const double* actuator_force,
+                             const double* action, const double* last_act, const double* joints_qpos,
+                             const double* joints_qvel, const double* default_act, int nu, double out[6]);
 
 /* batched CPU baseline: n_envs independent envs, OpenMP over envs.
  * fstate/istate are SoA with stride n_envs (duck_env.h); models[e] per env (or one shared). */

@@ -150,7 +150,7 @@ class OracleEnv:
     def __init__(self, model: OracleModel, cfg: DuckEnvConfig, table=None):
         self.model = model
         self.cfg = cfg
-        self.L = layout(model.m.nq, model.m.nv, model.m.nu, bool(cfg.use_imitation))
+        self.L = layout(model.m.nq, model.m.nv, model.m.nu, bool(cfg.use_imitation), int(cfg.task))
         if table is None:
             from open_duck_playground_amd import constants
             table = dict(np.load(constants.POLY_COEFFICIENTS, allow_pickle=False))
@@ -183,7 +183,7 @@ class OracleBatch:
         self.cfg = cfg
         self.n = n_envs
         m = self.models[0].m
-        self.L = layout(m.nq, m.nv, m.nu, bool(cfg.use_imitation))
+        self.L = layout(m.nq, m.nv, m.nu, bool(cfg.use_imitation), int(cfg.task))
         if table is None:
             from open_duck_playground_amd import constants
             table = dict(np.load(constants.POLY_COEFFICIENTS, allow_pickle=False))

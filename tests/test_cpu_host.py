@@ -135,12 +135,13 @@ def test_cabi_exports_every_declared_symbol():
     assert set(native.EXPORTS) >= syms
 
 
-@pytest.mark.parametrize("nq,nv,nu,imit", [(21, 20, 14, 0), (21, 20, 14, 1), (31, 30, 14, 1)])
-def test_layout_matches_c(nq, nv, nu, imit):
+@pytest.mark.parametrize("nq,nv,nu,imit,task", [(21, 20, 14, 0, 0), (21, 20, 14, 1, 0), (31, 30, 14, 1, 0),
+                                                (21, 20, 14, 0, 1), (31, 30, 14, 1, 1)])
+def test_layout_matches_c(nq, nv, nu, imit, task):
     lib = native.lib()
     cl = native.DuckLayout()
-    assert lib.duck_layout_get(nq, nv, nu, imit, C.byref(cl)) == 0
-    pl = layout(nq, nv, nu, bool(imit))
+    assert lib.duck_layout_get(nq, nv, nu, imit, task, C.byref(cl)) == 0
+    pl = layout(nq, nv, nu, bool(imit), task)
     for name, _ in native.DuckLayout._fields_:
         v = getattr(cl, name)
         if name in pl.off:
@@ -148,7 +149,10 @@ def test_layout_matches_c(nq, nv, nu, imit):
         elif name in pl.ioff:
             assert v == pl.ioff[name], name
     assert (cl.nfloat, cl.nint, cl.obs_size, cl.priv_size) == (pl.nfloat, pl.nint, pl.obs_size, pl.priv_size)
-    assert pl.obs_size == 101 and pl.priv_size == (212 if imit else 172)
+    if task == 0:
+        assert pl.obs_size == 101 and pl.priv_size == (212 if imit else 172)
+    else:  # standing.py: state 85 (3+3+7+14*5+2), privileged 153; no imitation
+        assert pl.obs_size == 85 and pl.priv_size == 153 and cl.imitation == 0
 
 
 def test_dr_layout():

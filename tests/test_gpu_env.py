@@ -54,6 +54,31 @@ def test_reset_step_parity(task, imit, gpu):
     assert good.mean() > 0.9
 
 
+@pytest.mark.parametrize("task", ["flat_terrain", "flat_terrain_backlash"])
+def test_standing_reset_step_parity(task, gpu):
+    """Standing (standing.py) through the same kernels, task switch on: obs 85 / priv 153."""
+    from open_duck_playground_amd.config import standing_default_config
+    from open_duck_playground_amd.standing import Standing
+    n = 100
+    env = Standing(task, num_envs=n, device=gpu)
+    assert env.observation_size == {"state": (85,), "privileged_state": (153,)}
+    st = env.reset(rng=11)
+    cfg = env_config_struct(env.mj_model, standing_default_config(), False, task=1)
+    ob = OracleBatch(OracleModel(env.mj_model), cfg, n)
+    ob.reset(seed=11)
+    L = env._layout
+    good = _compare(env, st, ob, L)
+    rng = np.random.default_rng(1)
+    for t in range(5):
+        a = rng.uniform(-1, 1, (n, env.action_size)).astype(np.float32)
+        env.step(st, torch.tensor(a, device=gpu))
+        ob.step(a.astype(np.float64))
+        good &= _compare(env, st, ob, L)
+    assert good.mean() > 0.9
+    assert set(st.metrics) == {"cost/orientation", "cost/torques", "cost/action_rate", "reward/alive",
+                               "cost/stand_still", "cost/head_pos", "swing_peak"}
+
+
 def test_autoreset_and_episode(gpu):
     n = 64
     env = wrap_for_brax_training(Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False),

@@ -78,3 +78,16 @@ def test_rewards_oracle():
                                            _dp(z["reference_frame"][i]), _dp(z["cmd"][i]), 14)
         np.testing.assert_allclose(im, z["expected"][i, 6], rtol=1e-12, atol=1e-12)
     assert np.all(z["expected"][:, 5] == 1.0)  # reward_alive
+
+
+def test_standing_rewards_oracle():
+    """Standing reward terms (standing.py:584-606) vs the reference's rewards_numpy.py twins."""
+    z = np.load(os.path.join(GOLD, "standing_rewards.npz"))
+    out = np.zeros(6)
+    for i in range(z["cmd"].shape[0]):
+        lib().oracle_standing_rewards(_dp(z["cmd"][i]), _dp(z["upvector"][i]), _dp(z["actuator_force"][i]),
+                                      _dp(z["action"][i]), _dp(z["last_act"][i]), _dp(z["joints_qpos"][i]),
+                                      _dp(z["joints_qvel"][i]), _dp(z["default_actuator"]), 14,
+                                      out.ctypes.data_as(C.POINTER(C.c_double)))
+        np.testing.assert_allclose(out, z["expected"][i], rtol=1e-12, atol=1e-12)
+    assert (z["expected"][:, 4] > 0).any() and (z["expected"][:, 5] > 0).any()  # both gates exercised

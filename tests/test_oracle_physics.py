@@ -157,3 +157,30 @@ def test_height_field_contacts_follow_terrain():
     np.testing.assert_allclose(np.linalg.norm(normals, axis=1), 1.0, atol=1e-9)
     assert (normals[:, 2] > 0.99).all()  # 1 cm relief over 7.8 cm cells: gentle slopes
     assert np.isfinite(d.arr("qpos", mr.nq)).all()
+
+
+def test_standing_task_surface(m, om):
+    """Standing (standing.py) on the oracle: obs 85 / privileged 153, zero initial motor targets,
+    no walking command, base velocity drawn from U(+-0.5), reward = clip(sum(terms) * dt)."""
+    from open_duck_playground_amd.config import standing_default_config
+    n = 8
+    cfg = env_config_struct(m, standing_default_config(), False, task=1)
+    assert cfg.use_imitation == 0 and cfg.use_motor_speed_limits == 0 and cfg.scale_head_pos == -2.0
+    b = OracleBatch(om, cfg, n)
+    L = b.L
+    assert (L.obs_size, L.priv_size) == (85, 153)
+    b.reset(seed=5)
+    F = b.fs.reshape(L.nfloat, n)
+    np.testing.assert_array_equal(F[L.off["motor_targets"]:L.off["motor_targets"] + m.nu], 0.0)
+    np.testing.assert_array_equal(F[L.off["command"]:L.off["command"] + 3], 0.0)
+    qv = F[L.off["qvel"]:L.off["qvel"] + 6]
+    assert np.abs(qv).max() <= 0.5 and np.abs(qv).max() > 0.05  # wider than the Joystick's +-0.05
+    np.testing.assert_array_equal(b.obs[:, 6:9], 0.0)  # command[:3] in the state
+    np.testing.assert_array_equal(b.priv[:, :85], b.obs)
+    b.step(np.zeros((n, m.nu)))
+    met = F[L.off["metrics"]:L.off["metrics"] + 8]
+    # reward = clip((orientation + torques + action_rate + alive + stand_still + head_pos) * dt, 0, 1e4)
+    terms = np.array([-met[0], -met[1], -met[2], met[3], -met[4], -met[5]])
+    np.testing.assert_allclose(b.rew, np.clip(terms.sum(0) * float(np.float32(0.02)), 0, 1e4), rtol=1e-12)
+    np.testing.assert_array_equal(met[3], 20.0)  # alive
+    np.testing.assert_array_equal(met[5], 0.0)   # head_pos gated off: no walking command

@@ -73,6 +73,22 @@ def main():
                         expected=out,
                         columns=np.array(["tracking_lin_vel", "tracking_ang_vel", "torques", "action_rate",
                                           "stand_still", "alive", "imitation"]))
+    # Standing reward terms (standing.py:584-606): orientation on the upvector, stand_still over
+    # the legs (ignore_head=True), head_pos; the same random inputs plus an upvector
+    up = np.random.default_rng(7).normal(0, 0.3, (n, 3))  # own stream: the cases below stay put
+    up[:, 2] += 1.0
+    st = np.zeros((n, 6))
+    for i in range(n):
+        st[i, 0] = rw.cost_orientation(up[i])
+        st[i, 1] = rw.cost_torques(af[i])
+        st[i, 2] = rw.cost_action_rate(act[i], last_act[i])
+        st[i, 3] = rw.reward_alive()
+        st[i, 4] = rw.cost_stand_still(cmd[i], jq[i], jqd[i], default, True)
+        st[i, 5] = rw.cost_head_pos(jq[i], jqd[i], cmd[i])
+    np.savez_compressed(os.path.join(OUT, "standing_rewards.npz"), cmd=cmd, upvector=up, actuator_force=af,
+                        action=act, last_act=last_act, joints_qpos=jq, joints_qvel=jqd, default_actuator=default,
+                        expected=st, columns=np.array(["orientation", "torques", "action_rate", "alive",
+                                                       "stand_still", "head_pos"]))
     # reference motion
     data = read_poly_pkl(f"{REF}/open_duck_mini_v2/data/polynomial_coefficients.pkl")
     prm = pm.PolyReferenceMotion.__new__(pm.PolyReferenceMotion)
