@@ -25,6 +25,7 @@ from .onnx_export import export_onnx
 from .joystick import Joystick, domain_randomize, wrap_for_brax_training
 from .ppo import ActorCritic, PPOConfig, save_checkpoint, train
 from .sharding import shard_from_env
+from .standing import Standing
 
 
 class BaseRunner:
@@ -74,8 +75,10 @@ class OpenDuckMiniV2Runner(BaseRunner):
 
     def __init__(self, args: argparse.Namespace) -> None:
         super().__init__(args)
-        if args.env != "joystick":
+        available_envs = {"joystick": Joystick, "standing": Standing}  # open_duck_mini_v2/runner.py:14-17
+        if args.env not in available_envs:
             raise ValueError(f"Unknown env {args.env}")
+        env_cls = available_envs[args.env]
         cfg = self.make_ppo_params()
         if dist.is_available() and dist.is_initialized():
             self.rank = dist.get_rank()
@@ -84,12 +87,12 @@ class OpenDuckMiniV2Runner(BaseRunner):
             raise ValueError(f"num_envs {cfg.num_envs} must divide over {world} ranks")
         shard = shard_from_env(cfg.num_envs // world)  # brax splits num_envs over devices
         dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count()))
-        self.env = Joystick(task=args.task, num_envs=shard.per_rank, device=dev, env_offset=shard.env_offset)
+        self.env = env_cls(task=args.task, num_envs=shard.per_rank, device=dev, env_offset=shard.env_offset)
         self.env = wrap_for_brax_training(self.env, episode_length=cfg.episode_length,
                                           randomization_fn=domain_randomize, rng=cfg.seed)
         self.eval_env = None
         if self.rank == 0:
-            self.eval_env = Joystick(task=args.task, num_envs=args.num_eval_envs, device=dev, env_offset=1 << 24)
+            self.eval_env = env_cls(task=args.task, num_envs=args.num_eval_envs, device=dev, env_offset=1 << 24)
             self.eval_env = wrap_for_brax_training(self.eval_env, episode_length=cfg.episode_length,
                                                    randomization_fn=domain_randomize, rng=cfg.seed + 1)
         self.action_size = self.env.action_size

@@ -79,3 +79,13 @@ def test_gae_kernel_matches_restatement(gpu, T, B):
     vs_n, adv_n = gae_numpy(*f32, 0.95, 0.97)
     np.testing.assert_allclose(vs.cpu().numpy(), vs_n, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(adv.cpu().numpy(), adv_n, rtol=1e-5, atol=1e-5)
+
+
+def test_runner_standing_env(gpu, tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setattr(runner.BaseRunner, "make_ppo_params",
+                        lambda self: ppo.PPOConfig(num_timesteps=self.num_timesteps, num_envs=256, batch_size=8,
+                                                   num_minibatches=32, episode_length=40, num_evals=0))
+    runner.main(["--output_dir", "ck", "--env", "standing", "--num_timesteps", str(20 * 256)])
+    line = json.loads(open(tmp_path / "ck" / "metrics.jsonl").readline())
+    assert line["step"] == 20 * 256 and np.isfinite(line["train/loss"])
