@@ -110,6 +110,10 @@ struct Col {  // SoA accessor for env e
   int n;
   DK float& operator[](int k) const { return p[(size_t)k * n]; }
 };
+struct LCol {  // the env's hot state staged in LDS (step_kernel, team mode)
+  lds_float* p;
+  DK lds_float& operator[](int k) const { return p[k]; }
+};
 
 // PolyReferenceMotion.get_reference_motion (poly_reference_motion.py:148-168)
 DK int nearest(const float* g, int n, float v) {
@@ -183,13 +187,31 @@ DK void load_dyn(const KArgs& A, int e, Slice<WG> L) {
 
 // Joystick._get_obs (joystick.py:487-620) / Standing._get_obs (standing.py:462-575); reads the
 // last forward's outputs from the slice
-template <class Md, int WG>
-DK void write_obs(const KArgs& A, int e, Slice<WG> L, const Rng& r, int slot_base,
-                                       int imitation_i) {
+// Observation sinks: GObs writes obs/priv rows in HBM directly; SObs stages the privileged row
+// (whose prefix is the state row) in the env slice's dead H/row storage, from where the team
+// stores both rows with coalesced 16-lane stores (step_kernel)
+struct GObs {
+  float* obs;
+  float* priv;
+  int obs_size;
+  DK void operator()(int k, float v) const {
+    if (k < obs_size) obs[k] = v;
+    priv[k] = v;
+  }
+};
+template <int WG>
+struct SObs {
+  Slice<WG> L;
+  int base;
+  DK void operator()(int k, float v) const { L[base + k] = v; }
+};
+
+template <class Md, int WG, class FA, class OS>
+DK void write_obs(const KArgs& A, int e, Slice<WG> L, const FA& F, const OS& out, const Rng& r, int slot_base,
+                  int imitation_i) {
   using Ly = Lay<Md>;
   const duck_env_config& c = A.cfg;
   const duck_layout& Lo = A.lay;
-  Col<0> F{A.fs + e, A.n};
   constexpr int NU = Md::NU;
   float gyro[3], acc[3], grav[3];
 #pragma unroll
@@ -207,10 +229,8 @@ DK void write_obs(const KArgs& A, int e, Slice<WG> L, const Rng& r, int slot_bas
   for (int k = 8; k >= 3; k--) F[Lo.imu_history + k] = F[Lo.imu_history + k - 3];
 #pragma unroll
   for (int k = 0; k < 3; k++) F[Lo.imu_history + k] = ngrav[k];
-  float* obs = A.obs + (size_t)e * Lo.obs_size;
-  float* priv = A.priv + (size_t)e * Lo.priv_size;
   int o = 0;
-  auto put = [&](float v) { obs[o] = v; priv[o] = v; o++; };
+  auto put = [&](float v) { out(o++, v); };
 #pragma unroll
   for (int k = 0; k < 3; k++) put(gyro[k] + (2.0f * r.u(slot_base + SLOT_GYRO + k) - 1.0f) * c.noise_level * c.noise_gyro);
 #pragma unroll
@@ -240,7 +260,7 @@ DK void write_obs(const KArgs& A, int e, Slice<WG> L, const Rng& r, int slot_bas
     put(F[Lo.imitation_phase + 1]);
   }
   int p = o;
-  auto pp = [&](float v) { priv[p++] = v; };
+  auto pp = [&](float v) { out(p++, v); };
 #pragma unroll
   for (int k = 0; k < 3; k++) pp(gyro[k]);
 #pragma unroll
@@ -345,35 +365,27 @@ __global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
     F[Lo.qacc_warmstart + i] = L[Ly::WARM + i]; F[Lo.first_qacc_warmstart + i] = L[Ly::WARM + i];
   }
   for (int a = 0; a < NU; a++) { F[Lo.ctrl + a] = L[Ly::CTRL + a]; F[Lo.first_ctrl + a] = L[Ly::CTRL + a]; }
-  write_obs<Md, SW>(A, e, L, r, RSLOT_OBS, 0);
+  write_obs<Md, SW>(A, e, L, F, GObs{A.obs + (size_t)e * Lo.obs_size, A.priv + (size_t)e * Lo.priv_size, Lo.obs_size},
+                    r, RSLOT_OBS, 0);
   for (int k = 0; k < Lo.obs_size; k++) F[Lo.first_obs + k] = A.obs[(size_t)e * Lo.obs_size + k];
   for (int k = 0; k < Lo.priv_size; k++) F[Lo.first_priv + k] = A.priv[(size_t)e * Lo.priv_size + k];
 }
 
-template <class Md, int WG>
-__global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
+// Joystick.step body for env e (joystick.py:323-481 + wrappers); F = the env's hot state
+// (LDS-staged or the global row), G = the global row (auto-reset snapshot)
+template <class Md, class FA, bool STAGE_OBS>
+DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, const Col<0>& G) {
   using Ly = Lay<Md>;
-#if DUCK_TEAM
-  {
-    extern __shared__ float lds_t[];
-    load_model_tables<Md>(lds_t);
-  }
-#endif
-  int lane;
-  const int t = local_env(lane);
-  if (t < 0) return;
-  const int e = blockIdx.x * WG + t;
-  if (e >= A.n) return;
-  extern __shared__ float lds[];
-  const Slice<SW> L = env_slice<Md>(lds, t);
   const duck_env_config& c = A.cfg;
   const duck_layout& Lo = A.lay;
   constexpr int NQ = Md::NQ, NV = Md::NV, NU = Md::NU;
   const int n = A.n;
-  Col<0> F{A.fs + e, n};
   auto iget = [&](int k) { return A.is[(size_t)k * n + e]; };
   auto iset = [&](int k, int32_t v) { A.is[(size_t)k * n + e] = v; };
   const float dt = c.ctrl_dt;
+  // every integer counter is read up front (a global load issued after the obs stores would
+  // wait for them: vmcnt counts stores too on CDNA)
+  const int step_prev = iget(Lo.step), push_step = iget(Lo.push_step), push_interval = iget(Lo.push_interval);
   int ep_steps = iget(Lo.ep_steps);
   if (c.auto_reset && F[Lo.done] != 0.0f) ep_steps = 0;
   Rng r;
@@ -415,7 +427,6 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   // push (joystick.py:381-400)
   const float theta = r.uniform(SLOT_PUSH_THETA, 0.0f, 2.0f * PI_F);
   const float mag = r.uniform(SLOT_PUSH_MAG, c.push_magnitude_range[0], c.push_magnitude_range[1]);
-  const int push_step = iget(Lo.push_step), push_interval = iget(Lo.push_interval);
   const float gate = ((push_step + 1) % push_interval == 0) ? 1.0f : 0.0f;
   const float push[2] = {cosf(theta) * gate * (float)c.push_enable, sinf(theta) * gate * (float)c.push_enable};
   for (int i = 0; i < NQ; i++) L[Ly::QPOS + i] = F[Lo.qpos + i];
@@ -434,7 +445,14 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
     F[Lo.feet_air_time + k] = F[Lo.feet_air_time + k] + dt;
     F[Lo.swing_peak + k] = fmaxf(F[Lo.swing_peak + k], L[Ly::FOOTZ + k]);
   }
-  write_obs<Md, SW>(A, e, L, r, 0, imitation_i);
+  if constexpr (STAGE_OBS) {
+    static_assert(DUCK_OBS_SIZE(NU) + 15 + 3 * NU + 1 + 2 + 6 + 2 + 40 + 1 + 2 <= Md::NM + 4 * Ly::NROW,
+                  "privileged row must fit in the H/row storage");
+    write_obs<Md, SW>(A, e, L, F, SObs<SW>{L, Ly::H}, r, 0, imitation_i);
+  } else {
+    write_obs<Md, SW>(A, e, L, F, GObs{A.obs + (size_t)e * Lo.obs_size, A.priv + (size_t)e * Lo.priv_size, Lo.obs_size},
+                      r, 0, imitation_i);
+  }
   // termination (joystick.py:483-485)
   bool nan = false;
   for (int i = 0; i < NQ; i++) nan = nan || isnan(L[Ly::QPOS + i]);
@@ -524,12 +542,12 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   // info bookkeeping (joystick.py:449-477)
   F[Lo.push] = push[0];
   F[Lo.push + 1] = push[1];
-  int step = iget(Lo.step) + 1;
+  int step = step_prev + 1;
   iset(Lo.push_step, push_step + 1);
   for (int a = 0; a < NU; a++) {
     F[Lo.last_last_last_act + a] = F[Lo.last_last_act + a];
     F[Lo.last_last_act + a] = F[Lo.last_act + a];
-    F[Lo.last_act + a] = A.action[(size_t)e * NU + a];
+    F[Lo.last_act + a] = F[Lo.action_history + a];  // this step's action
   }
   if (step > 500) {
     float nc[7];
@@ -566,11 +584,16 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
     iset(Lo.ep_steps, ep_steps);
   }
   if (restore) {
-    for (int i = 0; i < NQ; i++) F[Lo.qpos + i] = F[Lo.first_qpos + i];
-    for (int i = 0; i < NV; i++) { F[Lo.qvel + i] = F[Lo.first_qvel + i]; F[Lo.qacc_warmstart + i] = F[Lo.first_qacc_warmstart + i]; }
-    for (int a = 0; a < NU; a++) F[Lo.ctrl + a] = F[Lo.first_ctrl + a];
-    for (int k = 0; k < Lo.obs_size; k++) A.obs[(size_t)e * Lo.obs_size + k] = F[Lo.first_obs + k];
-    for (int k = 0; k < Lo.priv_size; k++) A.priv[(size_t)e * Lo.priv_size + k] = F[Lo.first_priv + k];
+    for (int i = 0; i < NQ; i++) F[Lo.qpos + i] = G[Lo.first_qpos + i];
+    for (int i = 0; i < NV; i++) { F[Lo.qvel + i] = G[Lo.first_qvel + i]; F[Lo.qacc_warmstart + i] = G[Lo.first_qacc_warmstart + i]; }
+    for (int a = 0; a < NU; a++) F[Lo.ctrl + a] = G[Lo.first_ctrl + a];
+    if constexpr (STAGE_OBS) {
+      TSYNC();
+      for (int k = lane; k < Lo.priv_size; k += TEAM) L[Ly::H + k] = G[Lo.first_priv + k];  // state = its prefix
+    } else {
+      for (int k = 0; k < Lo.obs_size; k++) A.obs[(size_t)e * Lo.obs_size + k] = G[Lo.first_obs + k];
+      for (int k = 0; k < Lo.priv_size; k++) A.priv[(size_t)e * Lo.priv_size + k] = G[Lo.first_priv + k];
+    }
   } else {
     for (int i = 0; i < NQ; i++) F[Lo.qpos + i] = L[Ly::QPOS + i];
     for (int i = 0; i < NV; i++) { F[Lo.qvel + i] = L[Ly::QVEL + i]; F[Lo.qacc_warmstart + i] = L[Ly::WARM + i]; }
@@ -580,6 +603,53 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   F[Lo.truncation] = trunc;
   A.reward[e] = reward;
   A.done[e] = done;
+  if constexpr (STAGE_OBS) {  // coalesced rows: lane k of the team stores elements k, k + 16, ...
+    TSYNC();
+    float* priv = A.priv + (size_t)e * Lo.priv_size;
+    float* obs = A.obs + (size_t)e * Lo.obs_size;
+    for (int k = lane; k < Lo.priv_size; k += TEAM) priv[k] = L[Ly::H + k];
+    for (int k = lane; k < Lo.obs_size; k += TEAM) obs[k] = L[Ly::H + k];
+  }
+}
+
+
+template <class Md, int WG>
+__global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
+  STAGE_T0();
+#if DUCK_TEAM
+  {
+    extern __shared__ float lds_t[];
+    load_model_tables<Md>(lds_t);
+  }
+#endif
+  STAGE_MARK(14);
+  int lane;
+  const int t = local_env(lane);
+  if (t < 0) return;
+  const int e = blockIdx.x * WG + t;
+  const int n = A.n;
+  if (e >= n) return;
+  extern __shared__ float lds[];
+  const Slice<SW> L = env_slice<Md>(lds, t);
+  const Col<0> G{A.fs + e, n};  // global row: the auto-reset snapshot (first_*) stays in HBM
+#if DUCK_TEAM
+  using TL = TLay<Md>;
+  if constexpr (TL::ES_LDS) {
+    // hot state -> LDS: the team's 16 lanes issue the env's loads together (one latency),
+    // and write it back together at the end
+    lds_float* esp = (lds_float*)(lds + TL::ES + t * TL::ESTRIDE);
+    for (int k = lane; k < TL::HOT; k += TEAM) esp[k] = A.fs[(size_t)k * n + e];
+    TSYNC();
+    step_env<Md, LCol, true>(A, e, lane, L, LCol{esp}, G);
+    TSYNC();
+    for (int k = lane; k < TL::HOT; k += TEAM) A.fs[(size_t)k * n + e] = esp[k];
+  } else {
+    step_env<Md, Col<0>, true>(A, e, lane, L, G, G);
+  }
+#else
+  step_env<Md, Col<0>, false>(A, e, lane, L, G, G);
+#endif
+  STAGE_MARK(15);
 }
 
 template <class Md, int WG>
@@ -720,6 +790,9 @@ static int launch_step(duck_sim* s, int n, float* fs, int32_t* is, const float* 
   KArgs A = make_args(s, n);
   A.fs = fs; A.is = is; A.dr = dr; A.action = action; A.obs = obs; A.priv = priv;
   A.reward = reward; A.done = done; A.scratch = scratch;
+#if DUCK_TEAM
+  if (s->lay.first_qpos != TLay<Md>::HOT) return duck_fail(DUCK_EINVAL, "state layout does not match the kernel's hot-state size");
+#endif
   const dim3 grid((A.n + WG - 1) / WG), block(TPB);
   hipLaunchKernelGGL((step_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A);
   HIPCHECK(hipGetLastError());

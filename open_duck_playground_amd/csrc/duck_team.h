@@ -93,8 +93,18 @@ struct TLay {
   // the model blob (lane-indexed tables, constraint-row records) follows the env slices in
   // LDS when it fits, else it is read from global memory
   static constexpr int TAB = STRIDE * TEAM_WG;
-  static constexpr bool TAB_LDS = (size_t)(TAB + Md::NBLOB) * 4 <= 160 * 1024;
-  static constexpr int LDS_FLOATS = TAB + (TAB_LDS ? Md::NBLOB : 0);
+  // step_kernel stages each env's hot state (the duck_layout fields before first_qpos) in LDS:
+  // one batch of independent global loads in, one batch of stores out
+  static constexpr int HOT = Md::NQ + 2 * Md::NV + 8 * Md::NU + 77;
+  static constexpr int ESTRIDE = HOT | 1;  // odd: the 16 envs' copies of a field hit distinct banks
+  static constexpr int ES_FLOATS = ESTRIDE * TEAM_WG;
+  static constexpr size_t LDS_MAX = 160 * 1024 / 4;
+  // LDS priority: model blob (read every substep), then the hot state (read once per env-step)
+  static constexpr bool TAB_LDS = (size_t)(TAB + Md::NBLOB) <= LDS_MAX;
+  static constexpr int ES = TAB + (TAB_LDS ? Md::NBLOB : 0);
+  static constexpr bool ES_LDS = (size_t)(ES + ES_FLOATS) <= LDS_MAX;
+  static constexpr int LDS_FLOATS = ES + (ES_LDS ? ES_FLOATS : 0);
+  static_assert((size_t)LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
   static_assert(6 * Md::NV <= 4 * Ly::NROW, "crb scratch must fit in the row storage");
 };
 
