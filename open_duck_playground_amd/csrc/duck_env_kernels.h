@@ -150,7 +150,8 @@ DK float nan_to_num(float x) {
   return x;
 }
 
-DK void sample_command(const duck_env_config& c, const Rng& r, int slot, float* cmd) {
+template <class RT>
+DK void sample_command(const duck_env_config& c, const RT& r, int slot, float* cmd) {
   const float f = c.head_range_factor;
   cmd[0] = r.uniform(slot + 0, c.lin_vel_x[0], c.lin_vel_x[1]);
   cmd[1] = r.uniform(slot + 1, c.lin_vel_y[0], c.lin_vel_y[1]);
@@ -206,8 +207,8 @@ struct SObs {
   DK void operator()(int k, float v) const { L[base + k] = v; }
 };
 
-template <class Md, int WG, class FA, class OS>
-DK void write_obs(const KArgs& A, int e, Slice<WG> L, const FA& F, const OS& out, const Rng& r, int slot_base,
+template <class Md, int WG, class FA, class OS, class RT>
+DK void write_obs(const KArgs& A, int e, Slice<WG> L, const FA& F, const OS& out, const RT& r, int slot_base,
                   int imitation_i) {
   using Ly = Lay<Md>;
   const duck_env_config& c = A.cfg;
@@ -373,8 +374,8 @@ __global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
 
 // Joystick.step body for env e (joystick.py:323-481 + wrappers); F = the env's hot state
 // (LDS-staged or the global row), G = the global row (auto-reset snapshot)
-template <class Md, class FA, bool STAGE_OBS>
-DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, const Col<0>& G) {
+template <class Md, class FA, bool STAGE_OBS, class RT>
+DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, const Col<0>& G, const RT& r) {
   using Ly = Lay<Md>;
   const duck_env_config& c = A.cfg;
   const duck_layout& Lo = A.lay;
@@ -388,10 +389,6 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   const int step_prev = iget(Lo.step), push_step = iget(Lo.push_step), push_interval = iget(Lo.push_interval);
   int ep_steps = iget(Lo.ep_steps);
   if (c.auto_reset && F[Lo.done] != 0.0f) ep_steps = 0;
-  Rng r;
-  r.k0 = (uint32_t)iget(Lo.rng_key);
-  r.k1 = (uint32_t)iget(Lo.rng_key + 1);
-  r.ctr = (uint32_t)iget(Lo.rng_ctr);
   int imitation_i = iget(Lo.imitation_i);
   if (Lo.imitation) {  // joystick.py:325-355
     const int nb = A.ref.nb;
@@ -632,22 +629,32 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   extern __shared__ float lds[];
   const Slice<SW> L = env_slice<Md>(lds, t);
   const Col<0> G{A.fs + e, n};  // global row: the auto-reset snapshot (first_*) stays in HBM
+  const duck_layout& Lo = A.lay;
+  Rng r;
+  r.k0 = (uint32_t)A.is[(size_t)Lo.rng_key * n + e];
+  r.k1 = (uint32_t)A.is[(size_t)(Lo.rng_key + 1) * n + e];
+  r.ctr = (uint32_t)A.is[(size_t)Lo.rng_ctr * n + e];
 #if DUCK_TEAM
   using TL = TLay<Md>;
   if constexpr (TL::ES_LDS) {
     // hot state -> LDS: the team's 16 lanes issue the env's loads together (one latency),
-    // and write it back together at the end
+    // and write it back together at the end; the step's 64 random draws are made by the
+    // team in parallel into the same region
     lds_float* esp = (lds_float*)(lds + TL::ES + t * TL::ESTRIDE);
     for (int k = lane; k < TL::HOT; k += TEAM) esp[k] = A.fs[(size_t)k * n + e];
+    RngTab rt;
+    rt.k0 = r.k0; rt.k1 = r.k1; rt.ctr = r.ctr;
+    rt.tab = esp + TL::HOT;
+    rt.fill(esp + TL::HOT, lane);
     TSYNC();
-    step_env<Md, LCol, true>(A, e, lane, L, LCol{esp}, G);
+    step_env<Md, LCol, true>(A, e, lane, L, LCol{esp}, G, rt);
     TSYNC();
     for (int k = lane; k < TL::HOT; k += TEAM) A.fs[(size_t)k * n + e] = esp[k];
   } else {
-    step_env<Md, Col<0>, true>(A, e, lane, L, G, G);
+    step_env<Md, Col<0>, true>(A, e, lane, L, G, G, r);
   }
 #else
-  step_env<Md, Col<0>, false>(A, e, lane, L, G, G);
+  step_env<Md, Col<0>, false>(A, e, lane, L, G, G, r);
 #endif
   STAGE_MARK(15);
 }

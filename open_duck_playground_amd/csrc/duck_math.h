@@ -115,6 +115,30 @@ struct Rng {
   }
 };
 
+// The first 64 slots of a step's stream drawn by the team in parallel (lane l runs the threefry
+// blocks l and l + 16) and read back from LDS; later slots fall back to direct evaluation.
+struct RngTab : Rng {
+  static constexpr int N = 64;
+  const __attribute__((address_space(3))) float* tab;
+  DK float u(int slot) const { return slot < N ? tab[slot] : Rng::u(slot); }
+  DK float uniform(int slot, float lo, float hi) const { return lo + (hi - lo) * u(slot); }
+  DK int randint(int slot, int lo, int hi) const {
+    int k = (int)floorf(u(slot) * (float)(hi - lo));
+    return lo + (k > hi - lo - 1 ? hi - lo - 1 : k);
+  }
+  // fill tab[0..N) (team lane `lane` of 16 writes 4 entries)
+  DK void fill(__attribute__((address_space(3))) float* t, int lane) const {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int j = lane + 16 * h;
+      uint32_t a, b;
+      threefry2x32(k0, k1, ctr, (uint32_t)j, a, b);
+      t[2 * j] = (float)(a >> 9) * (1.0f / 8388608.0f);
+      t[2 * j + 1] = (float)(b >> 9) * (1.0f / 8388608.0f);
+    }
+  }
+};
+
 DK void derive_key(uint64_t seed, int64_t env_id, uint32_t tag, uint32_t& k0, uint32_t& k1) {
   threefry2x32((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)env_id, tag ^ (uint32_t)((uint64_t)env_id >> 32), k0,
                k1);

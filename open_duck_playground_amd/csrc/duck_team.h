@@ -96,7 +96,7 @@ struct TLay {
   // step_kernel stages each env's hot state (the duck_layout fields before first_qpos) in LDS:
   // one batch of independent global loads in, one batch of stores out
   static constexpr int HOT = Md::NQ + 2 * Md::NV + 8 * Md::NU + 77;
-  static constexpr int ESTRIDE = HOT | 1;  // odd: the 16 envs' copies of a field hit distinct banks
+  static constexpr int ESTRIDE = (HOT + 64) | 1;  // + the step's 64 random draws; odd: distinct banks
   static constexpr int ES_FLOATS = ESTRIDE * TEAM_WG;
   static constexpr size_t LDS_MAX = 160 * 1024 / 4;
   // LDS priority: model blob (read every substep), then the hot state (read once per env-step)
