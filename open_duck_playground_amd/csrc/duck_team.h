@@ -1349,28 +1349,41 @@ struct TPhys {
   // the lane's constraint rows for the line search: its friction row, limit rows, and the
   // 4 edges of its contact slot (the same rows the lane computes J.x for)
   static constexpr int NLR = (NLIM + TEAM - 1) / TEAM;
+  // Along the search line every row's cost is a fixed quadratic in alpha inside each zone,
+  // so its coefficients are formed once: a one-sided row contributes (Q0, Q1, Q2) where
+  // ja + alpha v < 0; the friction row (Huber) its quadratic zone or a linear piece.
   struct Rows2 {
-    float fD, fja, fv, ff;
-    float lD[NLR], lja[NLR], lv[NLR];
-    float cD[4], cja[4], cv[4];
+    float fja, fv, frf, flin0, ffja, ffv, fQ0, fQ1, fQ2;  // friction row (zeros off the friction lanes)
+    float ja[NLR + 4], v[NLR + 4], Q0[NLR + 4], Q1[NLR + 4], Q2[NLR + 4];  // limit rows, then contact edges
   };
+  static DK void set_fric(Rows2& R, float D, float ja, float v, float f) {
+    const float rf = f / D;
+    R.fja = ja; R.fv = v; R.frf = rf;
+    R.flin0 = -0.5f * rf * f; R.ffja = f * ja; R.ffv = f * v;
+    R.fQ0 = 0.5f * D * ja * ja; R.fQ1 = D * v * ja; R.fQ2 = 0.5f * D * v * v;
+  }
+  static DK void set_row(Rows2& R, int k, float D, float ja, float v) {
+    R.ja[k] = ja; R.v[k] = v;
+    R.Q0[k] = 0.5f * D * ja * ja; R.Q1[k] = D * v * ja; R.Q2[k] = 0.5f * D * v * v;
+  }
 
-  static DK void quad2(const Rows2& R, int lane, float alpha, float& q0, float& q1, float& q2) {
-    if (lane < NFRIC) {
-      const float D = R.fD, ja = R.fja, v = R.fv, f = R.ff;
-      const float rf = f / D, x = ja + alpha * v;
-      if (x <= -rf) { q0 += -0.5f * rf * f - f * ja; q1 += -f * v; }
-      else if (x >= rf) { q0 += -0.5f * rf * f + f * ja; q1 += f * v; }
-      else { q0 += 0.5f * D * ja * ja; q1 += D * v * ja; q2 += 0.5f * D * v * v; }
+  // partial quadratic coefficients of this lane's rows at alpha (branchless)
+  static DK void quad2(const Rows2& R, float alpha, float& q0, float& q1, float& q2) {
+    {
+      const float x = R.fja + alpha * R.fv;
+      const bool lo = x <= -R.frf, hi = x >= R.frf, quad = !(lo || hi);
+      const float sg = lo ? -1.0f : 1.0f;
+      q0 += quad ? R.fQ0 : R.flin0 + sg * R.ffja;
+      q1 += quad ? R.fQ1 : sg * R.ffv;
+      q2 += quad ? R.fQ2 : 0.0f;
     }
-    auto one = [&](float D, float ja, float v) {
-      const float x = ja + alpha * v;
-      if (x < 0.0f) { q0 += 0.5f * D * ja * ja; q1 += D * v * ja; q2 += 0.5f * D * v * v; }
-    };
 #pragma unroll
-    for (int m = 0; m < NLR; m++) one(R.lD[m], R.lja[m], R.lv[m]);
-#pragma unroll
-    for (int e = 0; e < 4; e++) one(R.cD[e], R.cja[e], R.cv[e]);
+    for (int k = 0; k < NLR + 4; k++) {
+      const float on = (R.ja[k] + alpha * R.v[k] < 0.0f) ? 1.0f : 0.0f;
+      q0 = fmaf(on, R.Q0[k], q0);
+      q1 = fmaf(on, R.Q1[k], q1);
+      q2 = fmaf(on, R.Q2[k], q2);
+    }
   }
 
   // mjx solver.solve, iterations = 1
@@ -1452,10 +1465,11 @@ struct TPhys {
     mul_cols(L, lane, Mc, Ly::SRCH, Ly::GRAD);
     TSYNC();
     Rows2 R;
-    R.fD = R.fja = R.fv = R.ff = 0.0f;
-    if (lane < NFRIC) {
-      const int r = lane, i = fric_dof(r);
-      R.fD = L[Ly::RD + r]; R.fja = L[Ly::JA + r]; R.fv = L[Ly::SRCH + i]; R.ff = L[Ly::DFRIC + i];
+    {
+      const bool fr = lane < NFRIC;
+      const int r = fr ? lane : 0, i = fric_dof(r);
+      const float D = L[Ly::RD + r], ja = L[Ly::JA + r], v = L[Ly::SRCH + i], f = L[Ly::DFRIC + i];
+      set_fric(R, fr ? D : 1.0f, fr ? ja : 0.0f, fr ? v : 0.0f, fr ? f : 0.0f);
     }
 #pragma unroll
     for (int m = 0; m < NLR; m++) {
@@ -1463,16 +1477,17 @@ struct TPhys {
       const bool ok = r < NLIM;
       const int rc = ok ? r : 0, i = lim_dof(rc), row = R_LIM + rc;
       const float D = L[Ly::RD + row], ja = L[Ly::JA + row], v = L[Ly::LSGN + rc] * L[Ly::SRCH + i];
-      R.lD[m] = ok ? D : 0.0f; R.lja[m] = ok ? ja : 0.0f; R.lv[m] = ok ? v : 0.0f;
+      set_row(R, m, ok ? D : 0.0f, ok ? ja : 0.0f, ok ? v : 0.0f);
     }
-    for (int e = 0; e < 4; e++) R.cD[e] = R.cja[e] = R.cv[e] = 0.0f;
-    if (lane < NCON) {
+    {
       float SL[6], SR[6], v[4];
+      const int slot = lane < NCON ? lane : 0;
       for (int k = 0; k < 6; k++) { SL[k] = L[TL::TSP + k]; SR[k] = L[TL::TSP + 6 + k]; }
-      contact_jx(L, lane >> 2, lane, SL, SR, v);
+      contact_jx(L, slot >> 2, slot, SL, SR, v);
       for (int e = 0; e < 4; e++) {
-        const int row = R_CON + 4 * lane + e;
-        R.cD[e] = L[Ly::RD + row]; R.cja[e] = L[Ly::JA + row]; R.cv[e] = v[e];
+        const int row = R_CON + 4 * slot + e;
+        const bool ok = lane < NCON;
+        set_row(R, NLR + e, ok ? L[Ly::RD + row] : 0.0f, ok ? L[Ly::JA + row] : 0.0f, ok ? v[e] : 0.0f);
       }
     }
     float sn = 0.0f, sMa = 0.0f, sf = 0.0f, sMv = 0.0f;
@@ -1499,14 +1514,14 @@ struct TPhys {
     Pt p0;
     {
       float q0 = 0, q1 = 0, q2 = 0;
-      quad2(R, lane, 0.0f, q0, q1, q2);
+      quad2(R, 0.0f, q0, q1, q2);
       p0 = mk(0.0f, q0, q1, q2);
     }
     Pt lo;
     {
       const float a1 = p0.alpha - p0.d0 / p0.d1;
       float q0 = 0, q1 = 0, q2 = 0;
-      quad2(R, lane, a1, q0, q1, q2);
+      quad2(R, a1, q0, q1, q2);
       lo = mk(a1, q0, q1, q2);
     }
     Pt hi;
@@ -1519,9 +1534,9 @@ struct TPhys {
       if (done) break;
       const float al = lo.alpha - lo.d0 / lo.d1, ah = hi.alpha - hi.d0 / hi.d1, am = 0.5f * (lo.alpha + hi.alpha);
       float a0 = 0, a1 = 0, a2 = 0, b0 = 0, b1 = 0, b2 = 0, c0 = 0, c1 = 0, c2 = 0;
-      quad2(R, lane, al, a0, a1, a2);
-      quad2(R, lane, ah, b0, b1, b2);
-      quad2(R, lane, am, c0, c1, c2);
+      quad2(R, al, a0, a1, a2);
+      quad2(R, ah, b0, b1, b2);
+      quad2(R, am, c0, c1, c2);
       const Pt lo_next = mk(al, a0, a1, a2), hi_next = mk(ah, b0, b1, b2), mid = mk(am, c0, c1, c2);
       const bool s1 = (lo.d0 > 0.0f) || (lo.d0 < lo_next.d0);
       if (s1) lo = lo_next;
