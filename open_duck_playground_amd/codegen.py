@@ -229,6 +229,13 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     br_arr = np.full((len(branches), brlen), -1)
     for i, b in enumerate(branches):
         br_arr[i, :len(b)] = b
+    # dofs of each limb body (<= 2: a hinge and its backlash hinge), -1 where absent
+    brdof = np.full((len(branches), brlen * 2), -1)
+    for i, b in enumerate(branches):
+        for d, body in enumerate(b):
+            assert m.body_dofnum[body] <= 2
+            for jj in range(m.body_dofnum[body]):
+                brdof[i, 2 * d + jj] = m.body_dofadr[body] + jj
     # ---- model blob: lane-indexed tables and per-row constraint records, copied into LDS
     # once per launch (int32 words; floats bit-cast) ----
     dt = float(m.opt_timestep)
@@ -347,7 +354,7 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     tabs = {"lev": (lev, "int"), "child": (child, "int"), "madr": (full, "int"), "mi": (mi, "int"), "mj": (mj, "int"),
             "ldl": (np.array(ldl).reshape(-1, 3), "int"), "ldl_off": (ldl_off, "int"), "anc_dof": (anc_dof, "int"),
             "anc_adr": (anc_adr, "int"), "anc_off": (anc_off, "int"),
-            "ldlp": (np.array(ldlp), "int"), "ancp": (np.array(ancp), "int"), "br": (br_arr, "int"),
+            "ldlp": (np.array(ldlp), "int"), "ancp": (np.array(ancp), "int"), "br": (br_arr, "int"), "brdof": (brdof, "int"),
             "desc": (desc, "int"), "blob": (np.array(blob, dtype=np.int64), "int")}
     dev = [T(k, a, t) for k, (a, t) in tabs.items()]
     acc = [f"  static constexpr int T_NLEV = {nlev}, T_LEVW = {levw}, T_MAXCH = {maxch};\n",
@@ -359,7 +366,8 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
            _arr("T_LDL_NR", ldl_nr, "int"), _arr("T_LDL_RB", ldl_rb, "int"),
            _arr("T_ANC_NR", anc_nr, "int"), _arr("T_ANC_RB", anc_rb, "int"),
            _arr("T_DIAG", [adr[i, i] for i in range(nv)], "int"),
-           f"  static constexpr int T_NROOT = {len(root)}, T_NBR = {len(branches)}, T_BRLEN = {brlen};\n",
+           f"  static constexpr int T_NROOT = {len(root)}, T_NBR = {len(branches)}, T_BRLEN = {brlen}, "
+           f"T_BRMD = {int(max(m.body_dofnum[b] for br in branches for b in br))};\n",
            _arr("T_ROOT", root, "int"),
            f"  static constexpr int NBLOB = {len(blob)};\n"] + extra_const + [
            "".join(f"  static constexpr int B_{k.upper()} = {v};\n" for k, v in boff.items())]

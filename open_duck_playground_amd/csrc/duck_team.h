@@ -307,95 +307,128 @@ struct TPhys {
     TSYNC();
   }
 
-  // ---------------- mj_comVel + mj_rne (flg_acc = 0): root path on every lane, a limb per lane ----
-  // cvel/cacc of body b from its parent's (registers); returns cfrc_b (before subtree sums)
-  static DK void body_motion(LP L, int b, float* cv, float* ca, float* f) {
+  // ---------------- mj_comVel + mj_rne (flg_acc = 0) ----------------
+  // Three passes: (A) cvel/cacc down the tree — root path on every lane, a limb per lane, the
+  // limb's cdof/qvel loaded into registers before the chain; (B) body forces
+  // cinert cacc + cvel x* (cinert cvel), a body per lane; (C) subtree sums of the forces — limb
+  // suffix sums per lane, a team sum at the trunk, the root path on every lane.
+  static constexpr int RCA = TL::RCS, RFB = TL::RCDD;  // body accelerations / body forces (scratch)
+
+  // cvel/cacc of the free-joint root body (every lane); its cdof_dot rows go to CDD1 (sensors)
+  static DK void root_motion(LP L, int lane, int b, float* cv, float* ca) {
     const int da = Md::body_dofadr[b], nd = Md::body_dofnum[b];
-    if (b == 1) {
+    if (nd == 6) {
       for (int i = 0; i < 3; i++) {
-        const float v = L[Ly::QVEL + i];
-        for (int k = 0; k < 6; k++) cv[k] += L[Ly::CDOF + 6 * i + k] * v;
+        const float v = L[Ly::QVEL + da + i];
+        for (int k = 0; k < 6; k++) cv[k] += L[Ly::CDOF + 6 * (da + i) + k] * v;
       }
       float cvt[6];
       for (int k = 0; k < 6; k++) cvt[k] = cv[k];
       for (int i = 3; i < 6; i++) {
         float cd[6], cdd[6];
-        for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
+        for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * (da + i) + k];
         cross_motion(cdd, cvt, cd);
-        const float v = L[Ly::QVEL + i];
+        if (lane == i - 3)
+          for (int k = 0; k < 6; k++) L[Ly::CDD1 + 6 * (i - 3) + k] = cdd[k];
+        const float v = L[Ly::QVEL + da + i];
         for (int k = 0; k < 6; k++) { ca[k] += cdd[k] * v; cv[k] += cd[k] * v; }
       }
     } else {
-#pragma unroll
-      for (int jj = 0; jj < 2; jj++) {
-        if (jj < nd) {
-          const int i = da + jj;
-          float cd[6], cdd[6];
-          for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
-          cross_motion(cdd, cv, cd);
-          const float v = L[Ly::QVEL + i];
-          for (int k = 0; k < 6; k++) { ca[k] += cdd[k] * v; cv[k] += cd[k] * v; }
-        }
+      for (int jj = 0; jj < nd; jj++) {
+        float cd[6], cdd[6];
+        for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * (da + jj) + k];
+        cross_motion(cdd, cv, cd);
+        const float v = L[Ly::QVEL + da + jj];
+        for (int k = 0; k < 6; k++) { ca[k] += cdd[k] * v; cv[k] += cd[k] * v; }
       }
     }
-    float I[10], t1[6], t2[6];
-    for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * b + k];
-    mul_inert_vec(f, I, ca);
-    mul_inert_vec(t1, I, cv);
-    cross_force(t2, cv, t1);
-    for (int k = 0; k < 6; k++) f[k] += t2[k];
   }
 
   static DK void rne(LP L, int lane) {
-    constexpr int NR = Md::T_NROOT;
-    float cv[6], ca[6], fr[NR][6];
+    constexpr int NR = Md::T_NROOT, BL = Md::T_BRLEN, MD = Md::T_BRMD;  // dofs per limb body (2: backlash)
+    static_assert(Md::T_NBR <= TEAM, "a limb per lane");
+    // (A) velocities and accelerations
+    float cv[6], ca[6];
     for (int k = 0; k < 6; k++) { cv[k] = 0.0f; ca[k] = (k >= 3) ? -Md::gravity[k - 3] : 0.0f; }
 #pragma unroll
     for (int r = 0; r < NR; r++) {
       const int b = Md::T_ROOT[r];
-      body_motion(L, b, cv, ca, fr[r]);
+      root_motion(L, lane, b, cv, ca);
       if (lane == 0)
-        for (int k = 0; k < 6; k++) L[Ly::CVEL + 6 * b + k] = cv[k];
+        for (int k = 0; k < 6; k++) { L[Ly::CVEL + 6 * b + k] = cv[k]; L[RCA + 6 * b + k] = ca[k]; }
     }
-    if (lane == 0) {  // free-joint cdof_dot for the accelerometer (sensors)
-      float cv1[6] = {0, 0, 0, 0, 0, 0};
-      for (int i = 0; i < 3; i++) {
-        const float v = L[Ly::QVEL + i];
-        for (int k = 0; k < 6; k++) cv1[k] += L[Ly::CDOF + 6 * i + k] * v;
-      }
-      for (int i = 3; i < 6; i++) {
-        float cd[6], cdd[6];
-        for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * i + k];
-        cross_motion(cdd, cv1, cd);
-        for (int k = 0; k < 6; k++) L[Ly::CDD1 + 6 * (i - 3) + k] = cdd[k];
+    const bool limb = lane < Md::T_NBR;
+    int bb[BL];
+#pragma unroll
+    for (int d = 0; d < BL; d++) bb[d] = Md::t_br()[limb ? lane : 0][d];
+    {
+      float cd[BL][MD][6], qv[BL][MD];
+      int dof[BL][MD];
+#pragma unroll
+      for (int d = 0; d < BL; d++)
+#pragma unroll
+        for (int jj = 0; jj < MD; jj++) dof[d][jj] = Md::t_brdof()[limb ? lane : 0][2 * d + jj];
+#pragma unroll
+      for (int d = 0; d < BL; d++)
+#pragma unroll
+        for (int jj = 0; jj < MD; jj++) {
+          const int i = dof[d][jj] >= 0 ? dof[d][jj] : 0;
+          for (int k = 0; k < 6; k++) cd[d][jj][k] = L[Ly::CDOF + 6 * i + k];
+          qv[d][jj] = dof[d][jj] >= 0 ? L[Ly::QVEL + i] : 0.0f;
+        }
+#pragma unroll
+      for (int d = 0; d < BL; d++) {
+#pragma unroll
+        for (int jj = 0; jj < MD; jj++) {
+          float cdd[6];
+          cross_motion(cdd, cv, cd[d][jj]);
+          const float v = qv[d][jj];
+          for (int k = 0; k < 6; k++) { ca[k] += cdd[k] * v; cv[k] += cd[d][jj][k] * v; }
+        }
+        if (limb && bb[d] >= 0)
+          for (int k = 0; k < 6; k++) { L[Ly::CVEL + 6 * bb[d] + k] = cv[k]; L[RCA + 6 * bb[d] + k] = ca[k]; }
       }
     }
+    TSYNC();
+    // (B) body forces, a body per lane
+    for (int b = 1 + lane; b < NB; b += TEAM) {
+      if (Md::body_weldid[b] == 0) continue;
+      float I[10], v6[6], a6[6], f[6], t1[6], t2[6];
+      for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * b + k];
+      for (int k = 0; k < 6; k++) { v6[k] = L[Ly::CVEL + 6 * b + k]; a6[k] = L[RCA + 6 * b + k]; }
+      mul_inert_vec(f, I, a6);
+      mul_inert_vec(t1, I, v6);
+      cross_force(t2, v6, t1);
+      for (int k = 0; k < 6; k++) L[RFB + 6 * b + k] = f[k] + t2[k];
+    }
+    TSYNC();
+    // (C) subtree sums
     float S[6] = {0, 0, 0, 0, 0, 0};
-    if (lane < Md::T_NBR) {
-      int bb[Md::T_BRLEN];
-      float fb[Md::T_BRLEN][6];
+    {
+      float fb[BL][6];
 #pragma unroll
-      for (int d = 0; d < Md::T_BRLEN; d++) bb[d] = Md::t_br()[lane][d];
-#pragma unroll
-      for (int d = 0; d < Md::T_BRLEN; d++) {
-        if (bb[d] >= 0) {
-          body_motion(L, bb[d], cv, ca, fb[d]);
-          for (int k = 0; k < 6; k++) L[Ly::CVEL + 6 * bb[d] + k] = cv[k];
-        }
+      for (int d = 0; d < BL; d++) {
+        const int bc = bb[d] >= 0 ? bb[d] : 1;
+        for (int k = 0; k < 6; k++) fb[d][k] = L[RFB + 6 * bc + k];
       }
 #pragma unroll
-      for (int d = Md::T_BRLEN - 1; d >= 0; d--) {
-        if (bb[d] >= 0) {
+      for (int d = BL - 1; d >= 0; d--) {
+        if (limb && bb[d] >= 0)
           for (int k = 0; k < 6; k++) { S[k] += fb[d][k]; L[Ly::CFRC + 6 * bb[d] + k] = S[k]; }
-        }
       }
     }
     for (int k = 0; k < 6; k++) S[k] = tsum(S[k]);
+    {
+      float fr[NR][6];
 #pragma unroll
-    for (int r = NR - 1; r >= 0; r--) {
-      for (int k = 0; k < 6; k++) S[k] += fr[r][k];
-      if (lane == 0)
-        for (int k = 0; k < 6; k++) L[Ly::CFRC + 6 * Md::T_ROOT[r] + k] = S[k];
+      for (int r = 0; r < NR; r++)
+        for (int k = 0; k < 6; k++) fr[r][k] = L[RFB + 6 * Md::T_ROOT[r] + k];
+#pragma unroll
+      for (int r = NR - 1; r >= 0; r--) {
+        for (int k = 0; k < 6; k++) S[k] += fr[r][k];
+        if (lane == 0)
+          for (int k = 0; k < 6; k++) L[Ly::CFRC + 6 * Md::T_ROOT[r] + k] = S[k];
+      }
     }
     TSYNC();
     for (int i = lane; i < NV; i += TEAM) {
