@@ -222,13 +222,26 @@ struct TPhys {
       if (lane == 0) store_pose(L, Md::T_ROOT[r], p, q, R);
     }
     if (lane < Md::T_NBR) {
-      int bb[Md::T_BRLEN];
+      constexpr int BL = Md::T_BRLEN;
+      int bb[BL];
+      float kl[BL][7];  // the limb's local transforms, loaded before the chain (no LDS round trip per body)
 #pragma unroll
-      for (int d = 0; d < Md::T_BRLEN; d++) bb[d] = Md::t_br()[lane][d];
+      for (int d = 0; d < BL; d++) bb[d] = Md::t_br()[lane][d];
 #pragma unroll
-      for (int d = 0; d < Md::T_BRLEN; d++) {
+      for (int d = 0; d < BL; d++) {
+        const int bc = bb[d] >= 0 ? bb[d] : 1;
+        for (int k = 0; k < 7; k++) kl[d][k] = L[TL::KLOC + 7 * bc + k];
+      }
+#pragma unroll
+      for (int d = 0; d < BL; d++) {
         if (bb[d] < 0) break;
-        compose(bb[d]);
+        float t[3], qn[4];
+        mulmv3(t, R, &kl[d][4]);
+        for (int k = 0; k < 3; k++) p[k] += t[k];
+        qmul(qn, q, kl[d]);
+        qnormalize(qn);
+        for (int k = 0; k < 4; k++) q[k] = qn[k];
+        q2m(R, q);
         store_pose(L, bb[d], p, q, R);
       }
     }
@@ -620,12 +633,18 @@ struct TPhys {
   template <int SRC>
   static DK float bc(float v) { return dppf<0x150 + SRC>(v); }
 
+  // Pivot K: every lane c updates its column at each ancestor row I of K,
+  // H[I][c] -= (H[K][I] / H[K][K]) H[K][c], with H[K][I] read from lane I's register by the DPP
+  // operand of one v_mul (row_newbcast), then scales its entry H[K][c]. Column sets s whose
+  // columns all lie right of row I (TEAM s > I) hold only above-diagonal entries there and are
+  // skipped at compile time. The pivot reciprocal is v_rcp_f32 (1 ulp; pivots are never denormal).
   template <int K, int I>
   static DK void fac_anc(Fac& F, float inv) {
     if constexpr (I >= 0) {
-      const float hki = bc<I % TEAM>(F.col[I / TEAM][K]);  // H[K][I], unscaled
+      const float t = bc<I % TEAM>(F.col[I / TEAM][K]) * inv;
 #pragma unroll
-      for (int s = 0; s < NC; s++) F.col[s][I] -= hki * inv * F.col[s][K];
+      for (int s = 0; s < NC; s++)
+        if (TEAM * s <= I) F.col[s][I] -= t * F.col[s][K];
       fac_anc<K, Md::dof_parentid[I]>(F, inv);
     }
   }
@@ -634,22 +653,25 @@ struct TPhys {
     constexpr int ks = K / TEAM, kl = K % TEAM;
     const float dk = bc<kl>(F.col[ks][K]);
     F.dg[ks] = lane == kl ? F.col[ks][K] : F.dg[ks];
-    const float inv = 1.0f / dk;
+    const float inv = __builtin_amdgcn_rcpf(dk);
     fac_anc<K, Md::dof_parentid[K]>(F, inv);
 #pragma unroll
-    for (int s = 0; s < NC; s++) F.col[s][K] = (s == ks && lane == kl) ? F.col[s][K] : F.col[s][K] * inv;
+    for (int s = 0; s < NC; s++)
+      if (TEAM * s <= K) F.col[s][K] = (s == ks && lane == kl) ? F.col[s][K] : F.col[s][K] * inv;
   }
   template <int K>
   static DK void sol_back(const Fac& F, float* x) {
     const float xk = bc<K % TEAM>(x[K / TEAM]);
 #pragma unroll
-    for (int s = 0; s < NC; s++) x[s] -= ((F.desc[s] >> K) & 1u) ? F.col[s][K] * xk : 0.0f;
+    for (int s = 0; s < NC; s++)
+      if (TEAM * s < K) x[s] -= ((F.desc[s] >> K) & 1u) ? F.col[s][K] * xk : 0.0f;
   }
   template <int K>
   static DK void sol_fwd(const Fac& F, float* x, int lane) {
     float p = 0.0f;
 #pragma unroll
-    for (int s = 0; s < NC; s++) p += ((F.desc[s] >> K) & 1u) ? F.col[s][K] * x[s] : 0.0f;
+    for (int s = 0; s < NC; s++)
+      if (TEAM * s < K) p += ((F.desc[s] >> K) & 1u) ? F.col[s][K] * x[s] : 0.0f;
     p = tsum(p);
     if (lane == K % TEAM) x[K / TEAM] -= p;
   }
@@ -673,7 +695,7 @@ struct TPhys {
     fac_all(F, lane, std::make_integer_sequence<int, NV>{});
     back_all(F, x, std::make_integer_sequence<int, NV>{});
 #pragma unroll
-    for (int s = 0; s < NC; s++) x[s] = x[s] / F.dg[s];
+    for (int s = 0; s < NC; s++) x[s] = x[s] * __builtin_amdgcn_rcpf(F.dg[s]);
     fwd_all(F, x, lane, std::make_integer_sequence<int, NV>{});
   }
   static DK void set_desc(Fac& F, int lane) {
@@ -691,6 +713,7 @@ struct TPhys {
 #pragma unroll
       for (int r = 0; r < NV; r++) {
         const int a = madr(r, cc);
+        if (lower_only && r < TEAM * s) { col[s][r] = 0.0f; continue; }  // above the diagonal
         const float v = L[HOFF + (a >= 0 ? a : 0)];  // unconditional load: no branch per entry
         col[s][r] = (c < NV && a >= 0 && (!lower_only || r >= c)) ? v : 0.0f;
       }
@@ -778,7 +801,7 @@ struct TPhys {
       }
       g[s] = valid ? gr : 0.0f;
 #pragma unroll
-      for (int r = 0; r < NV; r++) F.col[s][r] = (r >= c) ? Mc[s][r] + (r == c ? diag : 0.0f) : 0.0f;
+      for (int r = 0; r < NV; r++) F.col[s][r] = (r >= TEAM * s && r >= c) ? Mc[s][r] + (r == c ? diag : 0.0f) : 0.0f;
     }
     // contact rows of each floor pair: per-foot 6x6 J'DJ block and J'force, by team sums
 #pragma unroll
@@ -825,7 +848,7 @@ struct TPhys {
         // H[r][c] += cdof_r . K cdof_c for chain rows r >= c (kc = 0 off the chain)
 #pragma unroll
         for (int r = 0; r < NV; r++) {
-          if (!((msk >> r) & 1u)) continue;  // compile-time after unrolling: chain rows only
+          if (!((msk >> r) & 1u) || r < TEAM * s) continue;  // compile-time: chain rows on or below the diagonal
           float h = 0.0f;
           for (int k = 0; k < 6; k++) h += L[Ly::CDOF + 6 * r + k] * kc[k];
           F.col[s][r] += r >= c ? h : 0.0f;
@@ -1426,9 +1449,9 @@ struct TPhys {
     float Mc[NC][NV];
     load_cols(L, lane, Ly::M, Mc, false);
     // warm start vs smooth acceleration: J and M products of both in one pass
+    // (M qacc_smooth = qfrc_smooth by definition: no product needed for the smooth start)
     spatial2(L, lane, Ly::WARM, Ly::QSM);
     mul_cols(L, lane, Mc, Ly::WARM, Ly::MA);
-    mul_cols(L, lane, Mc, Ly::QSM, Ly::GRAD);
     TSYNC();
     float cwp = 0.0f, csp = 0.0f, gwp = 0.0f;
     if (lane < NFRIC) {
@@ -1476,7 +1499,7 @@ struct TPhys {
       for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] = L[Ly::WARM + i];
       g0 = gw;
     } else {
-      for (int i = lane; i < NV; i += TEAM) { L[Ly::QACC + i] = L[Ly::QSM + i]; L[Ly::MA + i] = L[Ly::GRAD + i]; }
+      for (int i = lane; i < NV; i += TEAM) { L[Ly::QACC + i] = L[Ly::QSM + i]; L[Ly::MA + i] = L[Ly::FSM + i]; }
       for (int r = lane; r < NROW; r += TEAM) L[Ly::JA + r] = L[Ly::JV + r];
       g0 = 0.0f;  // gauss(qacc_smooth) = 0.5 (M qs - f).(qs - qs) = 0
     }
