@@ -267,8 +267,6 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         blob.extend(int(w) for w in words)
 
     put("madr", full.reshape(-1))
-    put("mi", mi)
-    put("mj", mj)
     put("desc", desc.reshape(-1))
     fric = [i for i in range(nv) if m.dof_frictionloss[i] > 0]
     rec = []
@@ -315,14 +313,12 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     for b in range(nb):
         c = chain_of(m, b)
         bchain[b, :len(c)] = c
-    put("bchain", bchain.reshape(-1))
     dyn = [b for b in range(1, nb) if m.body_weldid[b] != 0]
     sub = [[d for d in dyn if _is_anc(m, b, d)] for b in range(nb)]
     msub = max(len(x) for x in sub)
     bsub = np.full((nb, msub), -1)
     for b in range(nb):
         bsub[b, :len(sub[b])] = sub[b]
-    put("bsub", bsub.reshape(-1))
     rec = []
     for b in range(nb):
         q, pz = m.body_quat[b], m.body_pos[b]
@@ -342,6 +338,41 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         b = int(m.dof_bodyid[i])
         rec += [b, int(m.body_parentid[b]), int(m.body_dofadr[b]), int(m.jnt_type[m.dof_jntid[i]] == 0)]
     put("dofrec", rec)  # stride 4: body, parent body, first dof of the body, free-joint flag
+    # per-body / joint / actuator / collision-geom / sensor records and the limb tables: every
+    # lane-indexed model constant of the substep is read from LDS (no vector-memory loads)
+    rec = []
+    for b in range(nb):
+        rec += [f2i(x) for x in m.body_ipos[b]] + [f2i(x) for x in quat2mat(m.body_iquat[b]).reshape(-1)] + \
+            [f2i(x) for x in m.body_inertia[b]] + [int(m.body_weldid[b] != 0)]
+    put("binert", rec)  # stride 16: ipos3, imat9, inertia3, moving flag
+    rec = []
+    for j in range(m.njnt):
+        rec += [int(m.jnt_bodyid[j]), int(m.jnt_dofadr[j]), int(m.jnt_qposadr[j]), int(m.jnt_type[j])] + \
+            [f2i(x) for x in m.jnt_axis[j]] + [0]
+    put("jrec", rec)  # stride 8: body, dofadr, qposadr, type, axis3, pad
+    put("damp", [f2i(x) for x in m.dof_damping])
+    rec = []
+    for a in range(m.nu):
+        j = int(m.actuator_trnid[a])
+        rec += [int(m.actuator_ctrllimited[a]), f2i(m.actuator_ctrlrange[a][0]), f2i(m.actuator_ctrlrange[a][1]),
+                f2i(m.actuator_gear[a]), int(m.jnt_qposadr[j]), int(m.jnt_dofadr[j]), f2i(m.actuator_kv[a]),
+                int(m.actuator_forcelimited[a]), f2i(m.actuator_forcerange[a][0]), f2i(m.actuator_forcerange[a][1]),
+                0, 0]
+    put("act", rec)  # stride 12: ctrllimited, ctrlrange2, gear, qadr, dof, kv, forcelimited, forcerange2, pad2
+    rec = []
+    for g in (floor, m.id("geom", "left_foot_bottom_tpu"), m.id("geom", "right_foot_bottom_tpu")):
+        rec += [int(m.geom_bodyid[g])] + [f2i(x) for x in m.geom_pos[g]] + \
+            [f2i(x) for x in quat2mat(m.geom_quat[g]).reshape(-1)] + [0, 0, 0]
+    put("cgeom", rec)  # stride 16: body, pos3, mat9, pad3 (slots: floor, left foot, right foot)
+    rec = []
+    for i in range(m.nsensor):
+        st = int(m.sensor_objid[i])
+        rec += [int(m.sensor_type[i]), st, int(m.sensor_adr[i]), int(m.site_bodyid[st])] + \
+            [f2i(x) for x in m.site_pos[st]] + [f2i(x) for x in quat2mat(m.site_quat[st]).reshape(-1)] + \
+            [f2i(x) for x in m.site_quat[st]]
+    put("sens", rec)  # stride 20: type, site, adr, body, spos3, smat9, squat4
+    put("br", br_arr.reshape(-1))  # [T_NBR][T_BRLEN] limb bodies
+    put("brdof", brdof.reshape(-1))  # [T_NBR][2 T_BRLEN] their dofs
     dch = np.full((nv, mc), -1)
     for i in range(nv):
         c = sorted(_ancestors(m, i, True))

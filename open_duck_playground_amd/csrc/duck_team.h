@@ -141,6 +141,17 @@ struct TPhys {
   static DK int fric_dof(int r) { return ti(Md::B_FRIC + 3 * r); }
   static DK int lim_dof(int r) { return ti(Md::B_LIM + LIMW * r); }
   static DK int madr(int i, int j) { return ti(Md::B_MADR + NV * i + j); }
+  // lane-indexed model constants live in the LDS blob (codegen.team_tables records)
+  static constexpr unsigned long long moving_mask() {
+    unsigned long long msk = 0;
+    for (int b = 0; b < Md::NB; b++)
+      if (Md::body_weldid[b] != 0) msk |= 1ull << b;
+    return msk;
+  }
+  static DK bool moving(int b) { return (moving_mask() >> b) & 1ull; }
+  static DK int limb_body(int lane, int d) { return ti(Md::B_BR + Md::T_BRLEN * (lane < Md::T_NBR ? lane : 0) + d); }
+  static DK int limb_dof(int lane, int k) { return ti(Md::B_BRDOF + 2 * Md::T_BRLEN * (lane < Md::T_NBR ? lane : 0) + k); }
+  static DK int dof_body(int i) { return ti(Md::B_DOFREC + 4 * i); }
 
   static_assert(NFRIC <= TEAM, "one friction row per lane");
   static_assert(NCON <= TEAM, "one contact slot per lane");
@@ -180,7 +191,7 @@ struct TPhys {
     // K1: local transform (body quat x joint rotations, body pos) of every moving body, a
     // body per lane, off the serial chain
     for (int b = 2 + lane; b < NB; b += TEAM) {
-      if (Md::body_weldid[b] == 0) continue;
+      if (!moving(b)) continue;
       const int o = Md::B_BKIN + 16 * b;
       float q[4] = {tf(o), tf(o + 1), tf(o + 2), tf(o + 3)};
       const int nj = ti(o + 7);
@@ -226,7 +237,7 @@ struct TPhys {
       int bb[BL];
       float kl[BL][7];  // the limb's local transforms, loaded before the chain (no LDS round trip per body)
 #pragma unroll
-      for (int d = 0; d < BL; d++) bb[d] = Md::t_br()[lane][d];
+      for (int d = 0; d < BL; d++) bb[d] = limb_body(lane, d);
 #pragma unroll
       for (int d = 0; d < BL; d++) {
         const int bc = bb[d] >= 0 ? bb[d] : 1;
@@ -252,10 +263,10 @@ struct TPhys {
   static DK void com_pos(LP L, int lane) {
     float ms = 0.0f, cx = 0.0f, cy = 0.0f, cz = 0.0f;
     for (int b = 1 + lane; b < NB; b += TEAM) {
-      if (Md::body_weldid[b] == 0) continue;
+      if (!moving(b)) continue;
       float R[9], t[3], ip[3];
       for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
-      for (int k = 0; k < 3; k++) ip[k] = (b == 1) ? L[Ly::DIPOS + k] : Md::body_ipos[b][k];
+      for (int k = 0; k < 3; k++) ip[k] = (b == 1) ? L[Ly::DIPOS + k] : tf(Md::B_BINERT + 16 * b + k);
       mulmv3(t, R, ip);
       const float m = L[Ly::DMASS + b];
       ms += m;
@@ -269,14 +280,15 @@ struct TPhys {
     if (lane == 0)
       for (int k = 0; k < 3; k++) L[Ly::COM + k] = com[k];
     for (int b = 1 + lane; b < NB; b += TEAM) {
-      if (Md::body_weldid[b] == 0) continue;
+      if (!moving(b)) continue;
+      const int ob = Md::B_BINERT + 16 * b;
       float R[9], t[3], ip[3], Ri[9], Bi[9];
       for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
-      for (int k = 0; k < 3; k++) ip[k] = (b == 1) ? L[Ly::DIPOS + k] : Md::body_ipos[b][k];
-      for (int k = 0; k < 9; k++) Bi[k] = Md::body_imat[b][k];
+      for (int k = 0; k < 3; k++) ip[k] = (b == 1) ? L[Ly::DIPOS + k] : tf(ob + k);
+      for (int k = 0; k < 9; k++) Bi[k] = tf(ob + 3 + k);
       mulmv3(t, R, ip);
       mulmm3(Ri, R, Bi);
-      const float I[3] = {Md::body_inertia[b][0], Md::body_inertia[b][1], Md::body_inertia[b][2]};
+      const float I[3] = {tf(ob + 12), tf(ob + 13), tf(ob + 14)};
       float rot[9];
       for (int a = 0; a < 3; a++)
         for (int c = 0; c < 3; c++)
@@ -295,9 +307,9 @@ struct TPhys {
       L[o + 9] = m;
     }
     for (int j = lane; j < NJ; j += TEAM) {
-      const int b = Md::jnt_bodyid[j], da = Md::jnt_dofadr[j];
+      const int oj = Md::B_JREC + 8 * j, b = ti(oj), da = ti(oj + 1);
       const float off[3] = {com[0] - L[Ly::XPOS + 3 * b], com[1] - L[Ly::XPOS + 3 * b + 1], com[2] - L[Ly::XPOS + 3 * b + 2]};
-      if (Md::jnt_type[j] == 0) {
+      if (ti(oj + 3) == 0) {
         for (int k = 0; k < 3; k++)
           for (int q = 0; q < 6; q++) L[Ly::CDOF + 6 * (da + k) + q] = (q == 3 + k) ? 1.0f : 0.0f;
         for (int k = 0; k < 3; k++) {
@@ -309,7 +321,7 @@ struct TPhys {
         }
       } else {
         float R[9], ax[3], t[3];
-        const float ja[3] = {Md::jnt_axis[j][0], Md::jnt_axis[j][1], Md::jnt_axis[j][2]};
+        const float ja[3] = {tf(oj + 4), tf(oj + 5), tf(oj + 6)};
         for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
         mulmv3(ax, R, ja);
         cross3(t, ax, off);
@@ -373,14 +385,14 @@ struct TPhys {
     const bool limb = lane < Md::T_NBR;
     int bb[BL];
 #pragma unroll
-    for (int d = 0; d < BL; d++) bb[d] = Md::t_br()[limb ? lane : 0][d];
+    for (int d = 0; d < BL; d++) bb[d] = limb_body(lane, d);
     {
       float cd[BL][MD][6], qv[BL][MD];
       int dof[BL][MD];
 #pragma unroll
       for (int d = 0; d < BL; d++)
 #pragma unroll
-        for (int jj = 0; jj < MD; jj++) dof[d][jj] = Md::t_brdof()[limb ? lane : 0][2 * d + jj];
+        for (int jj = 0; jj < MD; jj++) dof[d][jj] = limb_dof(lane, 2 * d + jj);
 #pragma unroll
       for (int d = 0; d < BL; d++)
 #pragma unroll
@@ -405,7 +417,7 @@ struct TPhys {
     TSYNC();
     // (B) body forces, a body per lane
     for (int b = 1 + lane; b < NB; b += TEAM) {
-      if (Md::body_weldid[b] == 0) continue;
+      if (!moving(b)) continue;
       float I[10], v6[6], a6[6], f[6], t1[6], t2[6];
       for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * b + k];
       for (int k = 0; k < 6; k++) { v6[k] = L[Ly::CVEL + 6 * b + k]; a6[k] = L[RCA + 6 * b + k]; }
@@ -445,7 +457,7 @@ struct TPhys {
     }
     TSYNC();
     for (int i = lane; i < NV; i += TEAM) {
-      const int b = Md::dof_bodyid[i];
+      const int b = dof_body(i);
       float s = 0.0f;
       for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * i + k] * L[Ly::CFRC + 6 * b + k];
       L[Ly::FSM + i] = -s;
@@ -463,7 +475,7 @@ struct TPhys {
       int bb[BL];
       float C[BL][10];
 #pragma unroll
-      for (int d = 0; d < BL; d++) bb[d] = lane < Md::T_NBR ? Md::t_br()[lane < Md::T_NBR ? lane : 0][d] : -1;
+      for (int d = 0; d < BL; d++) bb[d] = lane < Md::T_NBR ? limb_body(lane, d) : -1;
 #pragma unroll
       for (int d = 0; d < BL; d++) {
         const int bc = bb[d] >= 0 ? bb[d] : 1;
@@ -503,7 +515,8 @@ struct TPhys {
       const int i = TEAM * s + lane, ic = i < NV ? i : 0;
       float cd[6], F[6], I[10];
       for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * ic + k];
-      for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * Md::dof_bodyid[ic] + k];
+      const int bi = dof_body(ic);
+      for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * bi + k];
       int jj[MC];
       float cj[MC][6];
 #pragma unroll
@@ -527,18 +540,19 @@ struct TPhys {
 
   // ---------------- actuation + passive; H = M ----------------
   static DK void smooth(LP L, int lane) {
-    for (int i = lane; i < NV; i += TEAM) L[Ly::FSM + i] += -Md::dof_damping[i] * L[Ly::QVEL + i];
+    for (int i = lane; i < NV; i += TEAM) L[Ly::FSM + i] += -tf(Md::B_DAMP + i) * L[Ly::QVEL + i];
     TSYNC();
     if (lane < NU) {
-      const int a = lane;
+      const int a = lane, o = Md::B_ACT + 12 * a;
+      const int dof = ti(o + 5);
       float c = L[Ly::CTRL + a];
-      if (Md::actuator_ctrllimited[a]) c = fminf(fmaxf(c, Md::actuator_ctrlrange[a][0]), Md::actuator_ctrlrange[a][1]);
-      const float g = Md::actuator_gear[a], kp = L[Ly::DKP + a];
-      const float len = g * L[Ly::QPOS + Md::actuator_qadr[a]], vel = g * L[Ly::QVEL + Md::actuator_dof[a]];
-      float f = kp * c + (-kp * len - Md::actuator_kv[a] * vel);
-      if (Md::actuator_forcelimited[a]) f = fminf(fmaxf(f, Md::actuator_forcerange[a][0]), Md::actuator_forcerange[a][1]);
+      if (ti(o)) c = fminf(fmaxf(c, tf(o + 1)), tf(o + 2));
+      const float g = tf(o + 3), kp = L[Ly::DKP + a];
+      const float len = g * L[Ly::QPOS + ti(o + 4)], vel = g * L[Ly::QVEL + dof];
+      float f = kp * c + (-kp * len - tf(o + 6) * vel);
+      if (ti(o + 7)) f = fminf(fmaxf(f, tf(o + 8)), tf(o + 9));
       L[Ly::AF + a] = f;
-      L[Ly::FSM + Md::actuator_dof[a]] += g * f;
+      L[Ly::FSM + dof] += g * f;
     }
     TSYNC();
   }
@@ -900,6 +914,17 @@ struct TPhys {
     return (pl[2] - z) * nl[2];
   }
 
+  // world frame of collision geom slot gs (1 left foot, 2 right foot: moving bodies)
+  static DK void cgeom_frame(LP L, int gs, float* gp, float* gR) {
+    const int o = Md::B_CGEOM + 16 * gs, b = ti(o);
+    float R[9], t[3], gpos[3], gm[9];
+    for (int k = 0; k < 9; k++) { R[k] = L[Ly::XMAT + 9 * b + k]; gm[k] = tf(o + 4 + k); }
+    for (int k = 0; k < 3; k++) gpos[k] = tf(o + 1 + k);
+    mulmv3(t, R, gpos);
+    for (int k = 0; k < 3; k++) gp[k] = L[Ly::XPOS + 3 * b + k] + t[k];
+    mulmm3(gR, R, gm);
+  }
+
   // floor (plane or height field) vs hull for both feet at once: lanes 0-7 take the first
   // floor pair, 8-15 the second
   static DK void collide_planes(LP L, int lane, const float* hf) {
@@ -910,7 +935,7 @@ struct TPhys {
     float pp[3], PR[9], cp[3], CR[9];
     S1 Ls{L};
     P1::geom_frame(Ls, 0, pp, PR);
-    P1::geom_frame(Ls, gs, cp, CR);
+    cgeom_frame(L, gs, cp, CR);
     const float n[3] = {PR[2], PR[5], PR[8]};
     const float dif[3] = {pp[0] - cp[0], pp[1] - cp[1], pp[2] - cp[2]};
     float pl[3], nl[3];
@@ -1625,11 +1650,11 @@ struct TPhys {
       }
     }
     for (int s = lane; s < Md::NSENSOR; s += TEAM) {
-      const int typ = Md::sensor_type[s], site = Md::sensor_objid[s], adr = Md::sensor_adr[s];
-      const int b = Md::site_bodyid[site];
+      const int os = Md::B_SENS + 20 * s;
+      const int typ = ti(os), site = ti(os + 1), adr = ti(os + 2), b = ti(os + 3);
       float R[9], sp[3], sR[9], t[3], SM[9];
-      const float spos[3] = {Md::site_pos[site][0], Md::site_pos[site][1], Md::site_pos[site][2]};
-      for (int k = 0; k < 9; k++) { R[k] = L[Ly::XMAT + 9 * b + k]; SM[k] = Md::site_mat[site][k]; }
+      const float spos[3] = {tf(os + 4), tf(os + 5), tf(os + 6)};
+      for (int k = 0; k < 9; k++) { R[k] = L[Ly::XMAT + 9 * b + k]; SM[k] = tf(os + 7 + k); }
       mulmv3(t, R, spos);
       for (int k = 0; k < 3; k++) sp[k] = L[Ly::XPOS + 3 * b + k] + t[k];
       mulmm3(sR, R, SM);
@@ -1654,7 +1679,7 @@ struct TPhys {
       else if (typ == 7) { o[0] = sp[0]; o[1] = sp[1]; o[2] = sp[2]; }
       else if (typ == 8) {
         const float bq[4] = {L[Ly::XQ + 4 * b], L[Ly::XQ + 4 * b + 1], L[Ly::XQ + 4 * b + 2], L[Ly::XQ + 4 * b + 3]};
-        const float sq[4] = {Md::site_quat[site][0], Md::site_quat[site][1], Md::site_quat[site][2], Md::site_quat[site][3]};
+        const float sq[4] = {tf(os + 16), tf(os + 17), tf(os + 18), tf(os + 19)};
         qmul(o, bq, sq);
         qnormalize(o);
       }
@@ -1696,7 +1721,10 @@ struct TPhys {
       qnormalize(q);
       for (int k = 0; k < 4; k++) L[Ly::QPOS + 3 + k] = q[k];
     }
-    for (int j = 1 + lane; j < NJ; j += TEAM) L[Ly::QPOS + Md::jnt_qposadr[j]] += dt * L[Ly::QVEL + Md::jnt_dofadr[j]];
+    for (int j = 1 + lane; j < NJ; j += TEAM) {
+      const int oj = Md::B_JREC + 8 * j;
+      L[Ly::QPOS + ti(oj + 2)] += dt * L[Ly::QVEL + ti(oj + 1)];
+    }
     TSYNC();
   }
 
