@@ -141,6 +141,20 @@ def maxchain_of(m: Model):
     return max(len(chain_of(m, b)) for b in range(m.nbody))
 
 
+def pivot_order(m: Model):
+    """Leaves-first elimination order of the dof tree for the register LDL': dofs sorted by
+    height (longest path down to a leaf of their subtree), so the limbs' pivots interleave
+    (independent dependency chains side by side) while every dof still follows all of its
+    descendants. The forward substitution runs it in reverse."""
+    nv = m.nv
+    h = [0] * nv
+    for i in range(nv - 1, -1, -1):
+        p = m.dof_parentid[i]
+        if p >= 0:
+            h[p] = max(h[p], h[i] + 1)
+    return sorted(range(nv), key=lambda i: (h[i], -i))
+
+
 def team_tables(m: Model, rows, adr, pre: str, floor: int):
     """Index tables for the team (16 lanes per env) kernel: lanes pick their work items
     (bodies of a tree level, mass-matrix entries, LDL updates) from these."""
@@ -397,6 +411,7 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
            _arr("T_LDL_NR", ldl_nr, "int"), _arr("T_LDL_RB", ldl_rb, "int"),
            _arr("T_ANC_NR", anc_nr, "int"), _arr("T_ANC_RB", anc_rb, "int"),
            _arr("T_DIAG", [adr[i, i] for i in range(nv)], "int"),
+           _arr("T_PORD", pivot_order(m), "int"),
            f"  static constexpr int T_NROOT = {len(root)}, T_NBR = {len(branches)}, T_BRLEN = {brlen}, "
            f"T_BRMD = {int(max(m.body_dofnum[b] for br in branches for b in br))};\n",
            _arr("T_ROOT", root, "int"),

@@ -828,9 +828,9 @@ static int launch_physics(duck_sim* s, int n, float* qpos, float* qvel, float* w
 
 static int stage_cycles_of(unsigned long long* out, int reset) {
 #ifdef DUCK_STAGE_PROF
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), sizeof(unsigned long long) * 16);
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), sizeof(unsigned long long) * 32);
   if (e == hipSuccess && reset) {
-    unsigned long long z[16] = {0};
+    unsigned long long z[32] = {0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, sizeof(z));
   }
   return e == hipSuccess ? 0 : DUCK_EHIP;

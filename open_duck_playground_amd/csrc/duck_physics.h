@@ -33,7 +33,7 @@ typedef __attribute__((address_space(3))) float lds_float;
 
 // optional per-stage cycle counters (build with -DDUCK_STAGE_PROF; read by duck_debug_stage_cycles)
 #ifdef DUCK_STAGE_PROF
-static __device__ unsigned long long g_stage_cycles[16];
+static __device__ unsigned long long g_stage_cycles[32];
 #define STAGE_T0() unsigned long long _t0 = wall_clock64(), _c0 = clock64()
 #define STAGE_MARK(k)                                                             \
   do {                                                                            \

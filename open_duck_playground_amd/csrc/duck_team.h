@@ -44,13 +44,16 @@ DK float imp_of(const float* solimp, float pos) {
     asm volatile("" ::: "memory");        \
   } while (0)
 
+// DPP reads with every lane of the row valid (full masks): no "old" value is needed, so the
+// mov has an undefined old operand and folds into its consumer (v_add_f32_dpp, v_mul_f32_dpp)
+// without a zeroing v_mov per read
 template <int CTRL>
 DK float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 template <int CTRL>
 DK int dppi(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
 // reductions over the 16 lanes of a DPP row (= one team); every lane gets the result
 DK float tsum(float v) {
@@ -188,6 +191,7 @@ struct TPhys {
   }
 
   static DK void kinematics(LP L, int lane) {
+    STAGE_T0();
     // K1: local transform (body quat x joint rotations, body pos) of every moving body, a
     // body per lane, off the serial chain
     for (int b = 2 + lane; b < NB; b += TEAM) {
@@ -209,6 +213,7 @@ struct TPhys {
       for (int k = 0; k < 3; k++) L[TL::KLOC + 7 * b + 4 + k] = tf(o + 4 + k);
     }
     TSYNC();
+    STAGE_MARK(24);
     // K2: compose down the root path (every lane) and the limbs (a limb per lane)
     float p[3], q[4], R[9];
     for (int k = 0; k < 3; k++) p[k] = L[Ly::QPOS + k];
@@ -370,6 +375,7 @@ struct TPhys {
   }
 
   static DK void rne(LP L, int lane) {
+    STAGE_T0();
     constexpr int NR = Md::T_NROOT, BL = Md::T_BRLEN, MD = Md::T_BRMD;  // dofs per limb body (2: backlash)
     static_assert(Md::T_NBR <= TEAM, "a limb per lane");
     // (A) velocities and accelerations
@@ -415,6 +421,7 @@ struct TPhys {
       }
     }
     TSYNC();
+    STAGE_MARK(21);
     // (B) body forces, a body per lane
     for (int b = 1 + lane; b < NB; b += TEAM) {
       if (!moving(b)) continue;
@@ -427,6 +434,7 @@ struct TPhys {
       for (int k = 0; k < 6; k++) L[RFB + 6 * b + k] = f[k] + t2[k];
     }
     TSYNC();
+    STAGE_MARK(22);
     // (C) subtree sums
     float S[6] = {0, 0, 0, 0, 0, 0};
     {
@@ -467,6 +475,7 @@ struct TPhys {
 
   // ---------------- mj_crb: composite inertias (limb sums, then the root path) and the sparse M ----
   static DK void crb(LP L, int lane) {
+    STAGE_T0();
     constexpr int BL = Md::T_BRLEN, MC = Md::MAXCHAIN;
     // composite inertias: each limb lane loads its bodies' cinert first (no store in between,
     // so the loads issue together), forms suffix sums, then stores; the trunk sums the limbs
@@ -508,6 +517,7 @@ struct TPhys {
           for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * Md::T_ROOT[r] + k] = Rr[r][k];
     }
     TSYNC();
+    STAGE_MARK(19);
     // M row i (lane i, i + 16): F_i = crb_{body(i)} cdof_i stays in registers;
     // M[i][j] = cdof_j . F_i over the ancestors j of i (the row is contiguous in M)
 #pragma unroll
@@ -669,9 +679,11 @@ struct TPhys {
     F.dg[ks] = lane == kl ? F.col[ks][K] : F.dg[ks];
     const float inv = __builtin_amdgcn_rcpf(dk);
     fac_anc<K, Md::dof_parentid[K]>(F, inv);
+    // scale row K of every column; the diagonal entry (lane kl) becomes 1, never read again
+    // (D is kept in dg; the solves read strictly-below-diagonal entries via descendant masks)
 #pragma unroll
     for (int s = 0; s < NC; s++)
-      if (TEAM * s <= K) F.col[s][K] = (s == ks && lane == kl) ? F.col[s][K] : F.col[s][K] * inv;
+      if (TEAM * s <= K) F.col[s][K] *= inv;
   }
   template <int K>
   static DK void sol_back(const Fac& F, float* x) {
@@ -691,15 +703,15 @@ struct TPhys {
   }
   template <int... J>
   static DK void fac_all(Fac& F, int lane, std::integer_sequence<int, J...>) {
-    (fac_pass<NV - 1 - J>(F, lane), ...);
+    (fac_pass<Md::T_PORD[J]>(F, lane), ...);  // leaves first, limbs interleaved (codegen.pivot_order)
   }
   template <int... J>
   static DK void back_all(const Fac& F, float* x, std::integer_sequence<int, J...>) {
-    (sol_back<NV - 1 - J>(F, x), ...);
+    (sol_back<Md::T_PORD[J]>(F, x), ...);
   }
   template <int... J>
   static DK void fwd_all(const Fac& F, float* x, int lane, std::integer_sequence<int, J...>) {
-    (sol_fwd<J>(F, x, lane), ...);
+    (sol_fwd<Md::T_PORD[NV - 1 - J]>(F, x, lane), ...);
   }
 
   // factor F.col in place and solve for x (lane l holds x[l], x[l+16]); F.desc must be set
@@ -783,6 +795,7 @@ struct TPhys {
   // columns (mjx _update_gradient + the Cholesky solve): SRCH = -H^-1 grad. Returns false
   // (nothing written) when foot/foot contact rows are active.
   static DK bool newton_fused(LP L, int lane, const float (*Mc)[NV]) {
+    STAGE_T0();
     if (Md::FOOT_PAIR >= 0) {
       const int row = R_CON + 16 * Md::FOOT_PAIR + lane;
       const float act = (L[Ly::JA + row] < 0.0f && L[Ly::RD + row] != 0.0f) ? 1.0f : 0.0f;
@@ -817,6 +830,7 @@ struct TPhys {
 #pragma unroll
       for (int r = 0; r < NV; r++) F.col[s][r] = (r >= TEAM * s && r >= c) ? Mc[s][r] + (r == c ? diag : 0.0f) : 0.0f;
     }
+    STAGE_MARK(16);
     // contact rows of each floor pair: per-foot 6x6 J'DJ block and J'force, by team sums
 #pragma unroll
     for (int side = 0; side < 2; side++) {
@@ -869,7 +883,9 @@ struct TPhys {
         }
       }
     }
+    STAGE_MARK(17);
     factor_solve(F, g, lane);
+    STAGE_MARK(18);
 #pragma unroll
     for (int s = 0; s < NC; s++) {
       const int c = TEAM * s + lane;
@@ -1062,7 +1078,9 @@ struct TPhys {
   }
 
   static DK void collision(LP L, int lane, const float* hf) {
+    STAGE_T0();
     collide_planes(L, lane, hf);
+    STAGE_MARK(26);
     if (Md::FOOT_PAIR >= 0) {
       constexpr int p = Md::FOOT_PAIR;
       const int s1 = cgeom_slot<Md>(Md::pair_geom1[p]), s2 = cgeom_slot<Md>(Md::pair_geom2[p]);
@@ -1740,6 +1758,7 @@ struct TPhys {
     crb(L, lane);
     STAGE_MARK(3);
     smooth(L, lane);
+    STAGE_MARK(28);
     solve_regs(L, lane, Ly::M, Ly::FSM, Ly::QSM, 1.0f);
     STAGE_MARK(4);
     collision(L, lane, hf);

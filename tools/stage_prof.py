@@ -1,5 +1,11 @@
 #!/usr/bin/env python3
-"""Per-stage cycle breakdown of step_kernel (needs a -DDUCK_STAGE_PROF build in DUCK_LIB)."""
+"""Per-stage cycle breakdown of step_kernel (needs a -DDUCK_STAGE_PROF build in DUCK_LIB).
+
+Counters are wave-0 clock64 deltas summed over workgroups; printed per substep per wave.
+Top-level stages (they partition a substep): 0-8 and 28. Sub-stage counters measure from
+the start of their parent stage: 9-13 solve, 16-18 newton direction, 19 crb limb/root
+sums, 21/22 rne passes A/B, 24 kinematics local transforms, 26 floor collision.
+"""
 import ctypes as C
 import os
 import sys
@@ -10,9 +16,12 @@ import torch  # noqa: E402
 from open_duck_playground_amd import native  # noqa: E402
 from open_duck_playground_amd.joystick import Joystick, wrap_for_brax_training  # noqa: E402
 
-NAMES = ["kinematics", "com_pos", "rne", "crb", "smooth+factor+solve_H", "collision", "make_rows", "solve",
-         "sensors+euler", "solve:warmstart", "solve:newton_dir", "solve:factor+solve", "solve:jmul+mulM",
-         "solve:linesearch"]
+TOP = {0: "kinematics", 1: "com_pos", 2: "rne", 3: "crb", 28: "smooth (actuation, damping)",
+       4: "qacc_smooth solve", 5: "collision", 6: "make_rows", 7: "solve", 8: "sensors+euler"}
+SUB = {24: "kinematics:local", 21: "rne:A vel/acc", 22: "rne:A+B forces", 19: "crb:inertia sums",
+       26: "collision:floor", 9: "solve:warmstart", 10: "solve:newton_dir", 16: "  newton:grad+diag",
+       17: "  newton:+J'DJ", 18: "  newton:+factor_solve", 11: "solve:(dense fallback)", 12: "solve:jmul+mulM",
+       13: "solve:linesearch"}
 
 
 def main():
@@ -25,11 +34,10 @@ def main():
     g.manual_seed(1234)
     pool = [torch.rand(n, env.action_size, device="cuda:0", generator=g) * 2 - 1 for _ in range(8)] if rand else \
         [torch.zeros(n, env.action_size, device="cuda:0")]
-    a = pool[0]
     for i in range(20):
         env.step(st, pool[i % len(pool)])
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 32)()
     lib = native.lib()
     lib.duck_debug_stage_cycles(env._sim, buf, 1)
     steps = 5
@@ -37,16 +45,19 @@ def main():
         env.step(st, pool[i % len(pool)])
     torch.cuda.synchronize()
     lib.duck_debug_stage_cycles(env._sim, buf, 1)
-    tot = sum(buf[k] for k in range(9))
     nwg = (n + 15) // 16
-    for k, name in enumerate(NAMES):
-        print(f"{name:24s} {buf[k] / (nwg * steps * 10):12.0f} cycles/substep/wave  {100 * buf[k] / tot:5.1f}%")
+    per_sub = lambda k: buf[k] / (nwg * steps * 10)
+    tot = sum(buf[k] for k in TOP)
+    for k, name in TOP.items():
+        print(f"{name:28s} {per_sub(k):10.0f} cycles/substep/wave  {100 * buf[k] / tot:5.1f}%")
+    for k, name in SUB.items():
+        print(f"{name:28s} {per_sub(k):10.0f}")
     per = lambda k: buf[k] / (nwg * steps)
     kern = per(14) + per(15)
-    print(f"{'kernel (per env-step)':24s} {kern:12.0f} cycles/env-step/wave")
-    print(f"{'  model-table copy':24s} {per(14):12.0f}  {100 * per(14) / kern:5.1f}%")
-    print(f"{'  10 substeps':24s} {tot / (nwg * steps):12.0f}  {100 * tot / (nwg * steps) / kern:5.1f}%")
-    print(f"{'  env code outside':24s} {per(15) - tot / (nwg * steps):12.0f}  "
+    print(f"{'kernel (per env-step)':28s} {kern:10.0f} cycles/env-step/wave")
+    print(f"{'  model-table copy':28s} {per(14):10.0f}  {100 * per(14) / kern:5.1f}%")
+    print(f"{'  10 substeps':28s} {tot / (nwg * steps):10.0f}  {100 * tot / (nwg * steps) / kern:5.1f}%")
+    print(f"{'  env code outside':28s} {per(15) - tot / (nwg * steps):10.0f}  "
           f"{100 * (per(15) - tot / (nwg * steps)) / kern:5.1f}%")
 
 
