@@ -20,15 +20,18 @@ constexpr int TEAM = 16;
 constexpr int TEAM_WG = 16;  // envs (teams) per workgroup: 256 threads = 4 waves
 typedef __attribute__((address_space(3))) int lds_int;
 
+// fp32 reciprocal as one v_rcp_f32 (1 ulp; operands here are never denormal or zero)
+DK float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
 // impedance of a constraint at violation pos (mjx constraint._kbi, imp part)
 DK float imp_of(const float* solimp, float pos) {
   const float dmin = fminf(fmaxf(solimp[0], 0.0001f), 0.9999f), dmax = fminf(fmaxf(solimp[1], 0.0001f), 0.9999f);
   const float width = fmaxf(1e-15f, solimp[2]), mid = fminf(fmaxf(solimp[3], 0.0001f), 0.9999f);
   const float power = fmaxf(1.0f, solimp[4]);
-  const float x = fabsf(pos) / width;
+  const float x = fabsf(pos) * frcp(width);
   float y;
   if (power == 2.0f) {
-    y = x < mid ? (1.0f / mid) * x * x : 1.0f - (1.0f / (1.0f - mid)) * (1.0f - x) * (1.0f - x);
+    y = x < mid ? frcp(mid) * x * x : 1.0f - frcp(1.0f - mid) * (1.0f - x) * (1.0f - x);
   } else {
     y = x < mid ? (1.0f / powf(mid, power - 1.0f)) * powf(x, power)
                 : 1.0f - (1.0f / powf(1.0f - mid, power - 1.0f)) * powf(1.0f - x, power);
@@ -280,7 +283,7 @@ struct TPhys {
       cz += m * (L[Ly::XPOS + 3 * b + 2] + t[2]);
     }
     ms = tsum(ms);
-    const float inv = 1.0f / ms;
+    const float inv = frcp(ms);
     const float com[3] = {tsum(cx) * inv, tsum(cy) * inv, tsum(cz) * inv};
     if (lane == 0)
       for (int k = 0; k < 3; k++) L[Ly::COM + k] = com[k];
@@ -690,14 +693,14 @@ struct TPhys {
     const float xk = bc<K % TEAM>(x[K / TEAM]);
 #pragma unroll
     for (int s = 0; s < NC; s++)
-      if (TEAM * s < K) x[s] -= ((F.desc[s] >> K) & 1u) ? F.col[s][K] * xk : 0.0f;
+      if (TEAM * s < K) x[s] -= F.col[s][K] * xk;
   }
   template <int K>
   static DK void sol_fwd(const Fac& F, float* x, int lane) {
     float p = 0.0f;
 #pragma unroll
     for (int s = 0; s < NC; s++)
-      if (TEAM * s < K) p += ((F.desc[s] >> K) & 1u) ? F.col[s][K] * x[s] : 0.0f;
+      if (TEAM * s < K) p += F.col[s][K] * x[s];
     p = tsum(p);
     if (lane == K % TEAM) x[K / TEAM] -= p;
   }
@@ -714,11 +717,18 @@ struct TPhys {
     (sol_fwd<Md::T_PORD[NV - 1 - J]>(F, x, lane), ...);
   }
 
-  // factor F.col in place and solve for x (lane l holds x[l], x[l+16]); F.desc must be set
+  // factor F.col (lower triangle of a tree-sparse SPD matrix, zeros elsewhere) in place and
+  // solve for x (lane l holds x[l], x[l+16])
   static DK void factor_solve(Fac& F, float* x, int lane) {
 #pragma unroll
     for (int s = 0; s < NC; s++) F.dg[s] = 1.0f;
     fac_all(F, lane, std::make_integer_sequence<int, NV>{});
+    // keep the strictly lower triangle (the unit diagonal and the upper garbage become 0): the
+    // tree-sparse factor has no fill-in outside ancestor pairs, so the solves need no masks
+#pragma unroll
+    for (int s = 0; s < NC; s++)
+#pragma unroll
+      for (int r = TEAM * s + 1; r < NV; r++) F.col[s][r] = lane < r - TEAM * s ? F.col[s][r] : 0.0f;
     back_all(F, x, std::make_integer_sequence<int, NV>{});
 #pragma unroll
     for (int s = 0; s < NC; s++) x[s] = x[s] * __builtin_amdgcn_rcpf(F.dg[s]);
@@ -749,7 +759,6 @@ struct TPhys {
   // DST = sign * A^-1 SRC for the tree-sparse SPD matrix A stored at HOFF (M_adr pattern)
   static DK void solve_regs(LP L, int lane, int HOFF, int SRC, int DST, float sign) {
     Fac F;
-    set_desc(F, lane);
     load_cols(L, lane, HOFF, F.col, true);
     float x[NC];
 #pragma unroll
@@ -802,7 +811,6 @@ struct TPhys {
       if (tsum(act) > 0.0f) return false;
     }
     Fac F;
-    set_desc(F, lane);
     float g[NC];
 #pragma unroll
     for (int s = 0; s < NC; s++) {
@@ -812,7 +820,7 @@ struct TPhys {
       // friction row of dof c (Huber cost): force and quadratic-zone curvature
       const int fr = ti(Md::B_DOF2FRIC + cc), frc = fr >= 0 ? fr : 0;
       {
-        const float D = L[Ly::RD + frc], x = L[Ly::JA + frc], f = L[Ly::DFRIC + cc], rf = f / D;
+        const float D = L[Ly::RD + frc], x = L[Ly::JA + frc], f = L[Ly::DFRIC + cc], rf = f * frcp(D);
         const float force = x <= -rf ? f : (x >= rf ? -f : -D * x);
         const bool quad = x > -rf && x < rf;
         gr -= fr >= 0 ? force : 0.0f;
@@ -1127,9 +1135,9 @@ struct TPhys {
       const float k = tf(o + 5), b = tf(o + 6);
       const float si[5] = {tf(o + 8), tf(o + 9), tf(o + 10), tf(o + 11), tf(o + 12)};
       const float imp = imp_of(si, pos);
-      const float R = fmaxf(tf(o + 7) * (1.0f - imp) / imp, 1e-15f);
+      const float R = fmaxf(tf(o + 7) * (1.0f - imp) * frcp(imp), 1e-15f);
       const bool active = pos < 0.0f;
-      L[Ly::RD + R_LIM + r] = active ? 1.0f / R : 0.0f;
+      L[Ly::RD + R_LIM + r] = active ? frcp(R) : 0.0f;
       L[Ly::AREF + R_LIM + r] = active ? (-b * sgn * L[Ly::QVEL + i] - k * imp * pos) : 0.0f;
       L[Ly::LSGN + r] = sgn;
     }
@@ -1142,12 +1150,12 @@ struct TPhys {
       const float k = tf(o + 5), b = tf(o + 6);
       const float si[5] = {tf(o + 8), tf(o + 9), tf(o + 10), tf(o + 11), tf(o + 12)};
       const float imp = imp_of(si, pos);
-      const float R = fmaxf(tf(o + 3) * (1.0f - imp) / imp, 1e-15f);
+      const float R = fmaxf(tf(o + 3) * (1.0f - imp) * frcp(imp), 1e-15f);
       float vel[4];
       contact_jx(L, p, slot, SL, SR, vel);
       for (int e = 0; e < 4; e++) {
         const int row = R_CON + 4 * slot + e;
-        L[Ly::RD + row] = active ? 1.0f / R : 0.0f;
+        L[Ly::RD + row] = active ? frcp(R) : 0.0f;
         L[Ly::AREF + row] = active ? (-b * vel[e] - k * imp * pos) : 0.0f;
       }
     }
@@ -1235,7 +1243,7 @@ struct TPhys {
     if (lane < NFRIC) {
       const int r = lane;
       const float D = L[Ly::RD + r], x = L[Ly::JA + r], f = L[Ly::DFRIC + fric_dof(r)];
-      const float rf = f / D;
+      const float rf = f * frcp(D);
       cost += x <= -rf ? (-f * x - 0.5f * rf * f) : (x >= rf ? (f * x - 0.5f * rf * f) : 0.5f * D * x * x);
     }
     for (int r = R_LIM + lane; r < NROW; r += TEAM) {
@@ -1441,7 +1449,7 @@ struct TPhys {
   }
 
   static DK float fric_cost(float D, float x, float f) {
-    const float rf = f / D;
+    const float rf = f * frcp(D);
     return x <= -rf ? (-f * x - 0.5f * rf * f) : (x >= rf ? (f * x - 0.5f * rf * f) : 0.5f * D * x * x);
   }
 
@@ -1456,7 +1464,7 @@ struct TPhys {
     float ja[NLR + 4], v[NLR + 4], Q0[NLR + 4], Q1[NLR + 4], Q2[NLR + 4];  // limit rows, then contact edges
   };
   static DK void set_fric(Rows2& R, float D, float ja, float v, float f) {
-    const float rf = f / D;
+    const float rf = f * frcp(D);
     R.fja = ja; R.fv = v; R.frf = rf;
     R.flin0 = -0.5f * rf * f; R.ffja = f * ja; R.ffv = f * v;
     R.fQ0 = 0.5f * D * ja * ja; R.fQ1 = D * v * ja; R.fQ2 = 0.5f * D * v * v;
