@@ -345,8 +345,9 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
                 jr += [int(m.jnt_qposadr[j])] + [f2i(x) for x in m.jnt_axis[j]]
             else:
                 jr += [0, 0, 0, 0]
-        rec += [f2i(x) for x in q] + [f2i(x) for x in pz] + [nj] + jr
-    put("bkin", rec)  # stride 16: quat4 pos3 njnt (qadr, axis3) x 2
+        rec += [f2i(x) for x in q] + [f2i(x) for x in pz] + [nj] + jr + [0]
+    # odd record strides: lane-indexed reads (record per lane) spread over the LDS banks
+    put("bkin", rec)  # stride 17: quat4 pos3 njnt (qadr, axis3) x 2, pad
     rec = []
     for i in range(nv):
         b = int(m.dof_bodyid[i])
@@ -357,13 +358,13 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     rec = []
     for b in range(nb):
         rec += [f2i(x) for x in m.body_ipos[b]] + [f2i(x) for x in quat2mat(m.body_iquat[b]).reshape(-1)] + \
-            [f2i(x) for x in m.body_inertia[b]] + [int(m.body_weldid[b] != 0)]
-    put("binert", rec)  # stride 16: ipos3, imat9, inertia3, moving flag
+            [f2i(x) for x in m.body_inertia[b]] + [int(m.body_weldid[b] != 0), 0]
+    put("binert", rec)  # stride 17: ipos3, imat9, inertia3, moving flag, pad
     rec = []
     for j in range(m.njnt):
         rec += [int(m.jnt_bodyid[j]), int(m.jnt_dofadr[j]), int(m.jnt_qposadr[j]), int(m.jnt_type[j])] + \
-            [f2i(x) for x in m.jnt_axis[j]] + [0]
-    put("jrec", rec)  # stride 8: body, dofadr, qposadr, type, axis3, pad
+            [f2i(x) for x in m.jnt_axis[j]] + [0, 0]
+    put("jrec", rec)  # stride 9: body, dofadr, qposadr, type, axis3, pad2
     put("damp", [f2i(x) for x in m.dof_damping])
     rec = []
     for a in range(m.nu):

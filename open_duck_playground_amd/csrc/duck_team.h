@@ -199,7 +199,7 @@ struct TPhys {
     // body per lane, off the serial chain
     for (int b = 2 + lane; b < NB; b += TEAM) {
       if (!moving(b)) continue;
-      const int o = Md::B_BKIN + 16 * b;
+      const int o = Md::B_BKIN + 17 * b;
       float q[4] = {tf(o), tf(o + 1), tf(o + 2), tf(o + 3)};
       const int nj = ti(o + 7);
 #pragma unroll
@@ -274,7 +274,7 @@ struct TPhys {
       if (!moving(b)) continue;
       float R[9], t[3], ip[3];
       for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
-      for (int k = 0; k < 3; k++) ip[k] = (b == 1) ? L[Ly::DIPOS + k] : tf(Md::B_BINERT + 16 * b + k);
+      for (int k = 0; k < 3; k++) ip[k] = (b == 1) ? L[Ly::DIPOS + k] : tf(Md::B_BINERT + 17 * b + k);
       mulmv3(t, R, ip);
       const float m = L[Ly::DMASS + b];
       ms += m;
@@ -289,7 +289,7 @@ struct TPhys {
       for (int k = 0; k < 3; k++) L[Ly::COM + k] = com[k];
     for (int b = 1 + lane; b < NB; b += TEAM) {
       if (!moving(b)) continue;
-      const int ob = Md::B_BINERT + 16 * b;
+      const int ob = Md::B_BINERT + 17 * b;
       float R[9], t[3], ip[3], Ri[9], Bi[9];
       for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
       for (int k = 0; k < 3; k++) ip[k] = (b == 1) ? L[Ly::DIPOS + k] : tf(ob + k);
@@ -315,7 +315,7 @@ struct TPhys {
       L[o + 9] = m;
     }
     for (int j = lane; j < NJ; j += TEAM) {
-      const int oj = Md::B_JREC + 8 * j, b = ti(oj), da = ti(oj + 1);
+      const int oj = Md::B_JREC + 9 * j, b = ti(oj), da = ti(oj + 1);
       const float off[3] = {com[0] - L[Ly::XPOS + 3 * b], com[1] - L[Ly::XPOS + 3 * b + 1], com[2] - L[Ly::XPOS + 3 * b + 2]};
       if (ti(oj + 3) == 0) {
         for (int k = 0; k < 3; k++)
@@ -1748,7 +1748,7 @@ struct TPhys {
       for (int k = 0; k < 4; k++) L[Ly::QPOS + 3 + k] = q[k];
     }
     for (int j = 1 + lane; j < NJ; j += TEAM) {
-      const int oj = Md::B_JREC + 8 * j;
+      const int oj = Md::B_JREC + 9 * j;
       L[Ly::QPOS + ti(oj + 2)] += dt * L[Ly::QVEL + ti(oj + 1)];
     }
     TSYNC();
