@@ -717,7 +717,8 @@ struct TPhys {
     (sol_fwd<Md::T_PORD[NV - 1 - J]>(F, x, lane), ...);
   }
 
-  // factor F.col (lower triangle of a tree-sparse SPD matrix, zeros elsewhere) in place and
+  // factor F.col (tree-sparse SPD matrix; only the lower triangle is read, entries right of
+  // the diagonal may hold anything) in place and
   // solve for x (lane l holds x[l], x[l+16])
   static DK void factor_solve(Fac& F, float* x, int lane) {
 #pragma unroll
@@ -751,7 +752,9 @@ struct TPhys {
         const int a = madr(r, cc);
         if (lower_only && r < TEAM * s) { col[s][r] = 0.0f; continue; }  // above the diagonal
         const float v = L[HOFF + (a >= 0 ? a : 0)];  // unconditional load: no branch per entry
-        col[s][r] = (c < NV && a >= 0 && (!lower_only || r >= c)) ? v : 0.0f;
+        // (with lower_only the entries right of the diagonal may stay: the factorization's lower
+        // triangle never reads them, and factor_solve drops them afterwards)
+        col[s][r] = (c < NV && a >= 0) ? v : 0.0f;
       }
     }
   }
@@ -836,7 +839,7 @@ struct TPhys {
       }
       g[s] = valid ? gr : 0.0f;
 #pragma unroll
-      for (int r = 0; r < NV; r++) F.col[s][r] = (r >= TEAM * s && r >= c) ? Mc[s][r] + (r == c ? diag : 0.0f) : 0.0f;
+      for (int r = 0; r < NV; r++) F.col[s][r] = r >= TEAM * s ? Mc[s][r] + (r == c ? diag : 0.0f) : 0.0f;
     }
     STAGE_MARK(16);
     // contact rows of each floor pair: per-foot 6x6 J'DJ block and J'force, by team sums
@@ -887,7 +890,7 @@ struct TPhys {
           if (!((msk >> r) & 1u) || r < TEAM * s) continue;  // compile-time: chain rows on or below the diagonal
           float h = 0.0f;
           for (int k = 0; k < 6; k++) h += L[Ly::CDOF + 6 * r + k] * kc[k];
-          F.col[s][r] += r >= c ? h : 0.0f;
+          F.col[s][r] += h;  // (entries right of the diagonal are dropped after the factorization)
         }
       }
     }
