@@ -297,6 +297,81 @@ DK void write_obs(const KArgs& A, int e, Slice<WG> L, const FA& F, const OS& out
   }
 }
 
+#if DUCK_TEAM
+// write_obs with the team's lanes splitting the rows (step_kernel): lane a < NU takes actuator
+// a's entries, lanes 0-2 the 3-vectors, lanes 0-1 the pairs; same values at the same offsets
+template <class Md, class FA, class OS, class RT>
+DK void write_obs_team(const KArgs& A, int lane, Slice<SW> L, const FA& F, const OS& out, const RT& r,
+                       int imitation_i) {
+  using Ly = Lay<Md>;
+  const duck_env_config& c = A.cfg;
+  const duck_layout& Lo = A.lay;
+  constexpr int NU = Md::NU;
+  static_assert(NU <= TEAM, "an actuator per lane");
+  const bool joystick = Lo.task == DUCK_TASK_JOYSTICK;
+  const float nl = c.noise_level;
+  // state row offsets (joystick.py:544-560 / standing.py)
+  const int OQ = 13, OV = OQ + NU, O1 = OV + NU, O2 = O1 + NU, O3 = O2 + NU, OM = O3 + NU;
+  const int OC = joystick ? OM + NU : OM;  // contacts
+  const int P = OC + 2 + (joystick ? 2 : 0);  // privileged row continues after the state row
+  const int PQ = P + 15, PV = PQ + NU, PZ = PV + NU, PA = PZ + 1, PC = PA + NU, PF = PC + 2, PT = PF + 6, PR = PT + 2;
+  const int PI = PR + (Lo.imitation ? 40 : 0);
+  if (lane < 3) {
+    const int k = lane;
+    const float gyro = L[Ly::SENS + c.sens_gyro + k], acc = L[Ly::SENS + c.sens_accelerometer + k];
+    const float grav = -L[Ly::IMUR + k];
+    const float ngrav = grav + (2.0f * r.u(SLOT_GRAVITY + k) - 1.0f) * nl * c.noise_gravity;
+    // IMU delay history (joystick.py:521-530): shift by one sample, the delayed one is never emitted
+    const float h0 = F[Lo.imu_history + k], h1 = F[Lo.imu_history + 3 + k];
+    F[Lo.imu_history + 6 + k] = h1;
+    F[Lo.imu_history + 3 + k] = h0;
+    F[Lo.imu_history + k] = ngrav;
+    out(k, gyro + (2.0f * r.u(SLOT_GYRO + k) - 1.0f) * nl * c.noise_gyro);
+    out(3 + k, acc + (2.0f * r.u(SLOT_ACCEL + k) - 1.0f) * nl * c.noise_accelerometer);
+    out(P + k, gyro);
+    out(P + 3 + k, acc);
+    out(P + 6 + k, grav);
+    out(P + 9 + k, L[Ly::SENS + c.sens_local_linvel + k]);
+    out(P + 12 + k, L[Ly::SENS + c.sens_global_angvel + k]);
+    out(PF + k, L[Ly::SENS + c.sens_left_foot_linvel + k]);
+    out(PF + 3 + k, L[Ly::SENS + c.sens_right_foot_linvel + k]);
+  }
+  if (lane < 7) out(6 + lane, F[Lo.command + lane]);
+  if (lane < NU) {
+    const int a = lane;
+    float ja = L[Ly::QPOS + c.actuator_qposadr[a]];
+    if (c.backlash_qposadr[a] >= 0) ja += L[Ly::QPOS + c.backlash_qposadr[a]];
+    const float jv = L[Ly::QVEL + c.actuator_qveladr[a]];
+    out(OQ + a, ja + (2.0f * r.u(SLOT_QPOS + a) - 1.0f) * nl * c.qpos_noise_scale[a] - c.default_actuator[a]);
+    out(OV + a, (jv + (2.0f * r.u(SLOT_QVEL + a) - 1.0f) * nl * c.noise_joint_vel) * c.dof_vel_scale);
+    out(O1 + a, F[Lo.last_act + a]);
+    out(O2 + a, F[Lo.last_last_act + a]);
+    out(O3 + a, F[Lo.last_last_last_act + a]);
+    if (joystick) out(OM + a, F[Lo.motor_targets + a]);
+    out(PQ + a, ja - c.default_actuator[a]);
+    out(PV + a, jv);
+    out(PA + a, L[Ly::AF + a]);
+  }
+  if (lane < 2) {
+    const float con = L[Ly::OCON + lane];
+    out(OC + lane, con);
+    out(PC + lane, con);
+    out(PT + lane, F[Lo.feet_air_time + lane]);
+    if (joystick) {
+      const float ph = F[Lo.imitation_phase + lane];
+      out(OC + 2 + lane, ph);
+      out(PI + 1 + lane, ph);
+    }
+  }
+  if (lane == 0) {
+    out(PZ, L[Ly::QPOS + 2]);
+    if (joystick) out(PI, (float)imitation_i);
+  }
+  if (Lo.imitation)
+    for (int k = lane; k < 40; k += TEAM) out(PR + k, F[Lo.ref_motion + k]);
+}
+#endif
+
 template <class Md, int WG>
 __global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
   using Ly = Lay<Md>;
@@ -381,6 +456,7 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   const duck_layout& Lo = A.lay;
   constexpr int NQ = Md::NQ, NV = Md::NV, NU = Md::NU;
   const int n = A.n;
+  STAGE_T0();
   auto iget = [&](int k) { return A.is[(size_t)k * n + e]; };
   auto iset = [&](int k, int32_t v) { A.is[(size_t)k * n + e] = v; };
   const float dt = c.ctrl_dt;
@@ -433,8 +509,10 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   load_dyn<Md, SW>(A, e, L);
   // physics (joystick.py:420)
   float* scr = A.scratch ? A.scratch + e : nullptr;
+  STAGE_MARK(29);
   for (int s = 0; s < c.n_substeps; s++)
     phys_step<Md>(L, lane, true, s == c.n_substeps - 1, nullptr, 0, scr, n, A.hfield);
+  STAGE_RESET();
   for (int a = 0; a < NU; a++) { F[Lo.motor_targets + a] = L[Ly::CTRL + a]; F[Lo.ctrl + a] = L[Ly::CTRL + a]; }
   const float con[2] = {L[Ly::OCON], L[Ly::OCON + 1]};
   // feet bookkeeping (joystick.py:424-435)
@@ -445,11 +523,13 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   if constexpr (STAGE_OBS) {
     static_assert(DUCK_OBS_SIZE(NU) + 15 + 3 * NU + 1 + 2 + 6 + 2 + 40 + 1 + 2 <= Md::NM + 4 * Ly::NROW,
                   "privileged row must fit in the H/row storage");
-    write_obs<Md, SW>(A, e, L, F, SObs<SW>{L, Ly::H}, r, 0, imitation_i);
+    write_obs_team<Md>(A, lane, L, F, SObs<SW>{L, Ly::H}, r, imitation_i);
+    TSYNC();
   } else {
     write_obs<Md, SW>(A, e, L, F, GObs{A.obs + (size_t)e * Lo.obs_size, A.priv + (size_t)e * Lo.priv_size, Lo.obs_size},
                       r, 0, imitation_i);
   }
+  STAGE_MARK(30);
   // termination (joystick.py:483-485)
   bool nan = false;
   for (int i = 0; i < NQ; i++) nan = nan || isnan(L[Ly::QPOS + i]);
@@ -600,6 +680,7 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   F[Lo.truncation] = trunc;
   A.reward[e] = reward;
   A.done[e] = done;
+  STAGE_MARK(31);
   if constexpr (STAGE_OBS) {  // coalesced rows: lane k of the team stores elements k, k + 16, ...
     TSYNC();
     float* priv = A.priv + (size_t)e * Lo.priv_size;

@@ -35,6 +35,7 @@ typedef __attribute__((address_space(3))) float lds_float;
 #ifdef DUCK_STAGE_PROF
 static __device__ unsigned long long g_stage_cycles[32];
 #define STAGE_T0() unsigned long long _t0 = wall_clock64(), _c0 = clock64()
+#define STAGE_RESET() (_c0 = clock64())
 #define STAGE_MARK(k)                                                             \
   do {                                                                            \
     asm volatile("s_waitcnt lgkmcnt(0) vmcnt(0)" ::: "memory");                   \
@@ -48,6 +49,9 @@ static __device__ unsigned long long g_stage_cycles[32];
   do {             \
   } while (0)
 #define STAGE_MARK(k) \
+  do {                \
+  } while (0)
+#define STAGE_RESET() \
   do {                \
   } while (0)
 #endif

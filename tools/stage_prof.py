@@ -22,6 +22,7 @@ SUB = {24: "kinematics:local", 21: "rne:A vel/acc", 22: "rne:A+B forces", 19: "c
        26: "collision:floor", 9: "solve:warmstart", 10: "solve:newton_dir", 16: "  newton:grad+diag",
        17: "  newton:+J'DJ", 18: "  newton:+factor_solve", 11: "solve:(dense fallback)", 12: "solve:jmul+mulM",
        13: "solve:linesearch"}
+ENV = {29: "env: pre-physics (per env-step)", 30: "env: contacts+obs", 31: "env: termination+rewards+state"}
 
 
 def main():
@@ -53,6 +54,8 @@ def main():
     for k, name in SUB.items():
         print(f"{name:28s} {per_sub(k):10.0f}")
     per = lambda k: buf[k] / (nwg * steps)
+    for k, name in ENV.items():
+        print(f"{name:28s} {per(k):10.0f} cycles/env-step/wave")
     kern = per(14) + per(15)
     print(f"{'kernel (per env-step)':28s} {kern:10.0f} cycles/env-step/wave")
     print(f"{'  model-table copy':28s} {per(14):10.0f}  {100 * per(14) / kern:5.1f}%")
