@@ -513,7 +513,10 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   for (int s = 0; s < c.n_substeps; s++)
     phys_step<Md>(L, lane, true, s == c.n_substeps - 1, nullptr, 0, scr, n, A.hfield);
   STAGE_RESET();
-  for (int a = 0; a < NU; a++) { F[Lo.motor_targets + a] = L[Ly::CTRL + a]; F[Lo.ctrl + a] = L[Ly::CTRL + a]; }
+  for (int a = STAGE_OBS ? lane : 0; a < NU; a += STAGE_OBS ? TEAM : 1) {
+    F[Lo.motor_targets + a] = L[Ly::CTRL + a];
+    F[Lo.ctrl + a] = L[Ly::CTRL + a];
+  }
   const float con[2] = {L[Ly::OCON], L[Ly::OCON + 1]};
   // feet bookkeeping (joystick.py:424-435)
   for (int k = 0; k < 2; k++) {
@@ -530,10 +533,19 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
                       r, 0, imitation_i);
   }
   STAGE_MARK(30);
+  // team mode: the per-actuator / per-dof loops below are split over the team's lanes and
+  // their sums combined by DPP row reductions (single-lane mode: TS = 1, plain loops)
+  constexpr int TS = STAGE_OBS ? TEAM : 1;
+  const int l0 = STAGE_OBS ? lane : 0;
+  auto red = [&](float v) {
+    if constexpr (STAGE_OBS) return tsum(v);
+    else return v;
+  };
   // termination (joystick.py:483-485)
-  bool nan = false;
-  for (int i = 0; i < NQ; i++) nan = nan || isnan(L[Ly::QPOS + i]);
-  for (int i = 0; i < NV; i++) nan = nan || isnan(L[Ly::QVEL + i]);
+  float nanp = 0.0f;
+  for (int i = l0; i < NQ; i += TS) nanp += isnan(L[Ly::QPOS + i]) ? 1.0f : 0.0f;
+  for (int i = l0; i < NV; i += TS) nanp += isnan(L[Ly::QVEL + i]) ? 1.0f : 0.0f;
+  const bool nan = red(nanp) > 0.0f;
   float done = (L[Ly::SENS + c.sens_upvector + 2] < 0.0f || nan) ? 1.0f : 0.0f;
   // rewards (joystick.py:622-669, common/rewards.py:11-125, custom_rewards.py:4-148)
   float cmd[7];
@@ -545,13 +557,28 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   const float ey = fmaxf(fabsf(lv1 - cmd[1]) - 0.1f, 0.0f);
   const float r_lin = nan_to_num(expf(-(ex + ey * ey) / sigma));
   const float r_ang = nan_to_num(expf(-((cmd[2] - gz) * (cmd[2] - gz)) / sigma));
-  float torq = 0.0f, pc = 0.0f, vc = 0.0f;
-  for (int a = 0; a < NU; a++) {
+  const bool standing = Lo.task == DUCK_TASK_STANDING;
+  float torq = 0.0f, pc = 0.0f, vc = 0.0f, lpc = 0.0f, lvc = 0.0f, hp = 0.0f;
+  for (int a = l0; a < NU; a += TS) {
     const float f = L[Ly::AF + a];
+    const float q = L[Ly::QPOS + c.actuator_qposadr[a]], qd = fabsf(L[Ly::QVEL + c.actuator_qveladr[a]]);
+    const float dq = fabsf(q - c.default_actuator[a]);
     torq += f * f;
-    pc += fabsf(L[Ly::QPOS + c.actuator_qposadr[a]] - c.default_actuator[a]);
-    vc += fabsf(L[Ly::QVEL + c.actuator_qveladr[a]]);
+    pc += dq;
+    vc += qd;
+    if (standing) {
+      if (a < 5 || a >= NU - 5) {  // legs: qpos[:5] and qpos[9:]
+        lpc += dq;
+        lvc += qd;
+      } else {  // head joints qpos[5:9] vs cmd[3:]
+        const float d = q - cmd[3 + a - 5];
+        hp += d * d;
+      }
+    }
   }
+  torq = red(torq);
+  pc = red(pc);
+  vc = red(vc);
   const float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1] + cmd[2] * cmd[2]);
   const float r_still = nan_to_num(pc + vc) * (cn < 0.01f ? 1.0f : 0.0f);
   float imit = 0.0f;
@@ -567,7 +594,7 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
     const float lin_xy = expf(-8.0f * lxy), lin_z = expf(-8.0f * dz * dz);
     const float ang_xy = expf(-2.0f * axy) * 0.5f, ang_z = expf(-2.0f * dwz * dwz) * 0.5f;
     float jp = 0.0f, jv = 0.0f;
-    for (int k = 0; k < 5; k++) {
+    for (int k = l0; k < 5; k += TS) {
       const float q1 = L[Ly::QPOS + c.actuator_qposadr[k]] - F[R0 + k];
       const float q2 = L[Ly::QPOS + c.actuator_qposadr[NU - 5 + k]] - F[R0 + 11 + k];
       const float v1 = L[Ly::QVEL + c.actuator_qveladr[k]] - F[R0 + 16 + k];
@@ -575,6 +602,8 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
       jp += q1 * q1 + q2 * q2;
       jv += v1 * v1 + v2 * v2;
     }
+    jp = red(jp);
+    jv = red(jv);
     float contact_r = 0.0f;
     for (int k = 0; k < 2; k++) contact_r += (con[k] == (F[R0 + 32 + k] > 0.5f ? 1.0f : 0.0f)) ? 1.0f : 0.0f;
     float rr = lin_xy + lin_z + ang_xy + ang_z + (-jp * 15.0f) + (-jv * 1e-3f) + contact_r;
@@ -582,21 +611,13 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
     imit = nan_to_num(rr);
   }
   float terms[7];
-  if (Lo.task == DUCK_TASK_STANDING) {
+  if (standing) {
     // Standing._get_reward (standing.py:584-606): orientation, torques, action_rate, alive,
     // stand_still(ignore_head=True), head_pos (common/rewards.py:45-46,93-117,131-147)
+    lpc = red(lpc);
+    lvc = red(lvc);
+    hp = red(hp);
     const float ux = L[Ly::SENS + c.sens_upvector], uy = L[Ly::SENS + c.sens_upvector + 1];
-    float lpc = 0.0f, lvc = 0.0f, hp = 0.0f;
-    for (int a = 0; a < NU; a++) {
-      const float q = L[Ly::QPOS + c.actuator_qposadr[a]];
-      if (a < 5 || a >= NU - 5) {  // legs: qpos[:5] and qpos[9:]
-        lpc += fabsf(q - c.default_actuator[a]);
-        lvc += fabsf(L[Ly::QVEL + c.actuator_qveladr[a]]);
-      } else {  // head joints qpos[5:9] vs cmd[3:]
-        const float d = q - cmd[3 + a - 5];
-        hp += d * d;
-      }
-    }
     terms[0] = nan_to_num(ux * ux + uy * uy) * c.scale_orientation;
     terms[1] = nan_to_num(torq) * c.scale_torques;
     terms[2] = nan_to_num(arate) * c.scale_action_rate;
@@ -621,7 +642,7 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   F[Lo.push + 1] = push[1];
   int step = step_prev + 1;
   iset(Lo.push_step, push_step + 1);
-  for (int a = 0; a < NU; a++) {
+  for (int a = l0; a < NU; a += TS) {
     F[Lo.last_last_last_act + a] = F[Lo.last_last_act + a];
     F[Lo.last_last_act + a] = F[Lo.last_act + a];
     F[Lo.last_act + a] = F[Lo.action_history + a];  // this step's action
@@ -640,7 +661,6 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
     F[Lo.swing_peak + k] = F[Lo.swing_peak + k] * (con[k] != 0.0f ? 0.0f : 1.0f);
   }
   // metrics: reward/<k> = term, cost/<k> = -term (joystick.py:467-474, standing.py:424-431)
-  const bool standing = Lo.task == DUCK_TASK_STANDING;
   const float scales[7] = {standing ? c.scale_orientation : c.scale_tracking_lin_vel,
                            standing ? c.scale_torques : c.scale_tracking_ang_vel,
                            standing ? c.scale_action_rate : c.scale_torques,
@@ -661,9 +681,9 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
     iset(Lo.ep_steps, ep_steps);
   }
   if (restore) {
-    for (int i = 0; i < NQ; i++) F[Lo.qpos + i] = G[Lo.first_qpos + i];
-    for (int i = 0; i < NV; i++) { F[Lo.qvel + i] = G[Lo.first_qvel + i]; F[Lo.qacc_warmstart + i] = G[Lo.first_qacc_warmstart + i]; }
-    for (int a = 0; a < NU; a++) F[Lo.ctrl + a] = G[Lo.first_ctrl + a];
+    for (int i = l0; i < NQ; i += TS) F[Lo.qpos + i] = G[Lo.first_qpos + i];
+    for (int i = l0; i < NV; i += TS) { F[Lo.qvel + i] = G[Lo.first_qvel + i]; F[Lo.qacc_warmstart + i] = G[Lo.first_qacc_warmstart + i]; }
+    for (int a = l0; a < NU; a += TS) F[Lo.ctrl + a] = G[Lo.first_ctrl + a];
     if constexpr (STAGE_OBS) {
       TSYNC();
       for (int k = lane; k < Lo.priv_size; k += TEAM) L[Ly::H + k] = G[Lo.first_priv + k];  // state = its prefix
@@ -672,8 +692,8 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
       for (int k = 0; k < Lo.priv_size; k++) A.priv[(size_t)e * Lo.priv_size + k] = G[Lo.first_priv + k];
     }
   } else {
-    for (int i = 0; i < NQ; i++) F[Lo.qpos + i] = L[Ly::QPOS + i];
-    for (int i = 0; i < NV; i++) { F[Lo.qvel + i] = L[Ly::QVEL + i]; F[Lo.qacc_warmstart + i] = L[Ly::WARM + i]; }
+    for (int i = l0; i < NQ; i += TS) F[Lo.qpos + i] = L[Ly::QPOS + i];
+    for (int i = l0; i < NV; i += TS) { F[Lo.qvel + i] = L[Ly::QVEL + i]; F[Lo.qacc_warmstart + i] = L[Ly::WARM + i]; }
   }
   F[Lo.reward] = reward;
   F[Lo.done] = done;
