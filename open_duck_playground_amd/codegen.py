@@ -386,6 +386,9 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
             [f2i(x) for x in m.site_pos[st]] + [f2i(x) for x in quat2mat(m.site_quat[st]).reshape(-1)] + \
             [f2i(x) for x in m.site_quat[st]]
     put("sens", rec)  # stride 20: type, site, adr, body, spos3, smat9, squat4
+    # nominal per-env model block, in Lay order DMASS (nb), DIPOS (3), DARM, DFRIC (nv), DQ0 (nq), DKP (nu)
+    put("nom", [f2i(x) for x in np.concatenate([m.body_mass, m.body_ipos[1], m.dof_armature, m.dof_frictionloss,
+                                                 m.qpos0, m.actuator_kp])])
     put("br", br_arr.reshape(-1))  # [T_NBR][T_BRLEN] limb bodies
     put("brdof", brdof.reshape(-1))  # [T_NBR][2 T_BRLEN] their dofs
     dch = np.full((nv, mc), -1)

@@ -186,6 +186,32 @@ DK void load_dyn(const KArgs& A, int e, Slice<WG> L) {
   }
 }
 
+#if DUCK_TEAM
+// load_dyn with the team's lanes: nominal block from the LDS model blob, then the env's DR record
+template <class Md>
+DK void load_dyn_team(const KArgs& A, int e, Slice<SW> L, int lane) {
+  using Ly = Lay<Md>;
+  using TP = TPhys<Md>;
+  constexpr int NDYN = Md::NB + 3 + 2 * Md::NV + Md::NQ + Md::NU;
+  static_assert(Ly::DKP + Md::NU - Ly::DMASS == NDYN, "contiguous per-env model block");
+  for (int k = lane; k < NDYN; k += TEAM) L[Ly::DMASS + k] = TP::tf(Md::B_NOM + k);
+  if (A.dr) {
+    TSYNC();
+    const duck_dr_layout& D = A.drl;
+    const int n = A.n;
+    if (lane < 3) L[Ly::DIPOS + lane] = A.dr[(size_t)(D.base_ipos + lane) * n + e];
+    for (int b = lane; b < Md::NB; b += TEAM) L[Ly::DMASS + b] = A.dr[(size_t)(D.body_mass + b) * n + e];
+    if (lane < Md::NU) {
+      const int a = lane, o = Md::B_ACT + 12 * a, dof = TP::ti(o + 5), qadr = TP::ti(o + 4);
+      L[Ly::DFRIC + dof] = A.dr[(size_t)(D.frictionloss + a) * n + e];
+      L[Ly::DARM + dof] = A.dr[(size_t)(D.armature + a) * n + e];
+      L[Ly::DQ0 + qadr] = A.dr[(size_t)(D.qpos0 + a) * n + e];
+      L[Ly::DKP + a] = A.dr[(size_t)(D.kp + a) * n + e];
+    }
+  }
+}
+#endif
+
 // Joystick._get_obs (joystick.py:487-620) / Standing._get_obs (standing.py:462-575); reads the
 // last forward's outputs from the slice
 // Observation sinks: GObs writes obs/priv rows in HBM directly; SObs stages the privileged row
@@ -481,7 +507,7 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   // action delay (joystick.py:362-376): history = [a_t, a_{t-1}, a_{t-2}]
   const int didx = r.randint(SLOT_ACTION_DELAY, c.action_min_delay, c.action_max_delay);
   float arate = 0.0f;
-  for (int a = 0; a < NU; a++) {
+  for (int a = STAGE_OBS ? lane : 0; a < NU; a += STAGE_OBS ? TEAM : 1) {
     const float act = A.action[(size_t)e * NU + a];
     const float h1 = F[Lo.action_history + a], h2 = F[Lo.action_history + NU + a];
     F[Lo.action_history + a] = act;
@@ -502,11 +528,22 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   const float mag = r.uniform(SLOT_PUSH_MAG, c.push_magnitude_range[0], c.push_magnitude_range[1]);
   const float gate = ((push_step + 1) % push_interval == 0) ? 1.0f : 0.0f;
   const float push[2] = {cosf(theta) * gate * (float)c.push_enable, sinf(theta) * gate * (float)c.push_enable};
-  for (int i = 0; i < NQ; i++) L[Ly::QPOS + i] = F[Lo.qpos + i];
-  for (int i = 0; i < NV; i++) { L[Ly::QVEL + i] = F[Lo.qvel + i]; L[Ly::WARM + i] = F[Lo.qacc_warmstart + i]; }
-  L[Ly::QVEL + 0] += push[0] * mag;
-  L[Ly::QVEL + 1] += push[1] * mag;
-  load_dyn<Md, SW>(A, e, L);
+  if constexpr (STAGE_OBS) {  // team: lane-split copies, sums by DPP
+    arate = tsum(arate);
+    for (int i = lane; i < NQ; i += TEAM) L[Ly::QPOS + i] = F[Lo.qpos + i];
+    for (int i = lane; i < NV; i += TEAM) {
+      L[Ly::QVEL + i] = F[Lo.qvel + i] + (i == 0 ? push[0] * mag : (i == 1 ? push[1] * mag : 0.0f));
+      L[Ly::WARM + i] = F[Lo.qacc_warmstart + i];
+    }
+    load_dyn_team<Md>(A, e, L, lane);
+    TSYNC();
+  } else {
+    for (int i = 0; i < NQ; i++) L[Ly::QPOS + i] = F[Lo.qpos + i];
+    for (int i = 0; i < NV; i++) { L[Ly::QVEL + i] = F[Lo.qvel + i]; L[Ly::WARM + i] = F[Lo.qacc_warmstart + i]; }
+    L[Ly::QVEL + 0] += push[0] * mag;
+    L[Ly::QVEL + 1] += push[1] * mag;
+    load_dyn<Md, SW>(A, e, L);
+  }
   // physics (joystick.py:420)
   float* scr = A.scratch ? A.scratch + e : nullptr;
   STAGE_MARK(29);
