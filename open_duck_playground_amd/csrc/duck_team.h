@@ -438,32 +438,43 @@ struct TPhys {
     }
     TSYNC();
     STAGE_MARK(22);
-    // (C) subtree sums
-    float S[6] = {0, 0, 0, 0, 0, 0};
+    // (C) subtree sums of the body forces (rne) and of the body inertias (mj_crb's composite
+    // inertias, which overwrite CIN: phase B has read the body inertias), in one pass
+    float S[6] = {0, 0, 0, 0, 0, 0}, SI[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     {
-      float fb[BL][6];
+      float fb[BL][6], C[BL][10];
 #pragma unroll
       for (int d = 0; d < BL; d++) {
         const int bc = bb[d] >= 0 ? bb[d] : 1;
         for (int k = 0; k < 6; k++) fb[d][k] = L[RFB + 6 * bc + k];
+        for (int k = 0; k < 10; k++) C[d][k] = L[Ly::CIN + 10 * bc + k];
       }
 #pragma unroll
       for (int d = BL - 1; d >= 0; d--) {
-        if (limb && bb[d] >= 0)
+        if (limb && bb[d] >= 0) {
           for (int k = 0; k < 6; k++) { S[k] += fb[d][k]; L[Ly::CFRC + 6 * bb[d] + k] = S[k]; }
+          for (int k = 0; k < 10; k++) { SI[k] += C[d][k]; L[Ly::CIN + 10 * bb[d] + k] = SI[k]; }
+        }
       }
     }
     for (int k = 0; k < 6; k++) S[k] = tsum(S[k]);
+    for (int k = 0; k < 10; k++) SI[k] = tsum(SI[k]);
     {
-      float fr[NR][6];
+      float fr[NR][6], Rr[NR][10];
 #pragma unroll
-      for (int r = 0; r < NR; r++)
+      for (int r = 0; r < NR; r++) {
         for (int k = 0; k < 6; k++) fr[r][k] = L[RFB + 6 * Md::T_ROOT[r] + k];
+        for (int k = 0; k < 10; k++) Rr[r][k] = L[Ly::CIN + 10 * Md::T_ROOT[r] + k];
+      }
+      TSYNC();
 #pragma unroll
       for (int r = NR - 1; r >= 0; r--) {
         for (int k = 0; k < 6; k++) S[k] += fr[r][k];
-        if (lane == 0)
+        for (int k = 0; k < 10; k++) SI[k] += Rr[r][k];
+        if (lane == 0) {
           for (int k = 0; k < 6; k++) L[Ly::CFRC + 6 * Md::T_ROOT[r] + k] = S[k];
+          for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * Md::T_ROOT[r] + k] = SI[k];
+        }
       }
     }
     TSYNC();
@@ -476,50 +487,11 @@ struct TPhys {
     TSYNC();
   }
 
-  // ---------------- mj_crb: composite inertias (limb sums, then the root path) and the sparse M ----
+  // ---------------- mj_crb: the sparse M from the composite inertias (summed in rne) ----
   static DK void crb(LP L, int lane) {
     STAGE_T0();
     constexpr int BL = Md::T_BRLEN, MC = Md::MAXCHAIN;
-    // composite inertias: each limb lane loads its bodies' cinert first (no store in between,
-    // so the loads issue together), forms suffix sums, then stores; the trunk sums the limbs
-    float S[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    {
-      int bb[BL];
-      float C[BL][10];
-#pragma unroll
-      for (int d = 0; d < BL; d++) bb[d] = lane < Md::T_NBR ? limb_body(lane, d) : -1;
-#pragma unroll
-      for (int d = 0; d < BL; d++) {
-        const int bc = bb[d] >= 0 ? bb[d] : 1;
-        for (int k = 0; k < 10; k++) C[d][k] = L[Ly::CIN + 10 * bc + k];
-      }
-#pragma unroll
-      for (int d = BL - 1; d >= 0; d--)
-        for (int k = 0; k < 10; k++) {
-          S[k] += bb[d] >= 0 ? C[d][k] : 0.0f;
-          C[d][k] = S[k];
-        }
-#pragma unroll
-      for (int d = 0; d < BL; d++)
-        if (bb[d] >= 0)
-          for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * bb[d] + k] = C[d][k];
-    }
-    for (int k = 0; k < 10; k++) S[k] = tsum(S[k]);
-    {
-      float Rr[Md::T_NROOT][10];
-#pragma unroll
-      for (int r = 0; r < Md::T_NROOT; r++)
-        for (int k = 0; k < 10; k++) Rr[r][k] = L[Ly::CIN + 10 * Md::T_ROOT[r] + k];
-#pragma unroll
-      for (int r = Md::T_NROOT - 1; r >= 0; r--)
-        for (int k = 0; k < 10; k++) { S[k] += Rr[r][k]; Rr[r][k] = S[k]; }
-      TSYNC();
-      if (lane == 0)
-#pragma unroll
-        for (int r = 0; r < Md::T_NROOT; r++)
-          for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * Md::T_ROOT[r] + k] = Rr[r][k];
-    }
-    TSYNC();
+    // (the composite inertias were summed in rne's subtree pass)
     STAGE_MARK(19);
     // M row i (lane i, i + 16): F_i = crb_{body(i)} cdof_i stays in registers;
     // M[i][j] = cdof_j . F_i over the ancestors j of i (the row is contiguous in M)
