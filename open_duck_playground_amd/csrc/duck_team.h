@@ -1087,6 +1087,9 @@ struct TPhys {
         }
       } else {
         TSYNC();
+#ifdef DUCK_STAGE_PROF
+        if (lane == 0) atomicAdd(&g_stage_cycles[27], 1ull);  // how often the SAT path runs
+#endif
         P1::collide_hulls(Ls, s1, s2, 4 * p);  // rare: every lane runs the single-lane path
       }
     }

@@ -56,6 +56,7 @@ def main():
     per = lambda k: buf[k] / (nwg * steps)
     for k, name in ENV.items():
         print(f"{name:28s} {per(k):10.0f} cycles/env-step/wave")
+    print(f"{'foot/foot SAT runs':28s} {buf[27] / steps:10.1f} per env-step (all {n} envs)")
     kern = per(14) + per(15)
     print(f"{'kernel (per env-step)':28s} {kern:10.0f} cycles/env-step/wave")
     print(f"{'  model-table copy':28s} {per(14):10.0f}  {100 * per(14) / kern:5.1f}%")
