@@ -494,6 +494,9 @@ def model_header(m: Model, variant: str) -> str:
            ]
     out.append(_arr("gravity", m.opt_gravity, "float"))
     out.append(_arr("hull_center", hc, "float"))
+    # the hull's box in its mesh frame (conservative prefilter of the foot/foot SAT)
+    out.append(_arr("hull_box_c", 0.5 * (hull.vert.min(axis=0) + hull.vert.max(axis=0)), "float"))
+    out.append(_arr("hull_box_h", 0.5 * (hull.vert.max(axis=0) - hull.vert.min(axis=0)), "float"))
     for name in ("body_parentid", "body_jntnum", "body_jntadr", "body_dofnum", "body_dofadr", "body_weldid"):
         out.append(_arr(name, m.arrays[name], "int"))
     for name in ("body_pos", "body_quat", "body_ipos", "body_mass", "body_inertia", "body_invweight0"):

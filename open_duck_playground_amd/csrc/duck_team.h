@@ -1060,6 +1060,44 @@ struct TPhys {
     }
   }
 
+  // Are the boxes enclosing the two hulls (mesh frames p, R) separated? 15-axis box/box SAT
+  // (face axes of both boxes and their 9 edge-pair axes), with a 1e-5 m margin so that only a
+  // clear separation rejects: then the hulls inside are separated too and the full hull SAT
+  // would report no contact.
+  static DK bool boxes_separated(const float* p1, const float* R1, const float* p2, const float* R2) {
+    const float* h = Md::hull_box_h;
+    float c1[3], c2[3], t[3], T[3], Ta[3], Rr[3][3], Ar[3][3];
+    mulmv3(t, R1, Md::hull_box_c);
+    for (int k = 0; k < 3; k++) c1[k] = p1[k] + t[k];
+    mulmv3(t, R2, Md::hull_box_c);
+    for (int k = 0; k < 3; k++) c2[k] = p2[k] + t[k];
+    for (int k = 0; k < 3; k++) T[k] = c2[k] - c1[k];
+    mulmtv3(Ta, R1, T);  // center offset in box 1's axes
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {  // Rr[i][j] = axis i of box 1 . axis j of box 2
+        Rr[i][j] = R1[i] * R2[j] + R1[3 + i] * R2[3 + j] + R1[6 + i] * R2[6 + j];
+        Ar[i][j] = fabsf(Rr[i][j]) + 1e-6f;
+      }
+    constexpr float MARGIN = 1e-5f;
+    bool sep = false;
+    for (int i = 0; i < 3; i++)
+      sep = sep || fabsf(Ta[i]) > h[i] + h[0] * Ar[i][0] + h[1] * Ar[i][1] + h[2] * Ar[i][2] + MARGIN;
+    for (int j = 0; j < 3; j++) {
+      const float tb = Ta[0] * Rr[0][j] + Ta[1] * Rr[1][j] + Ta[2] * Rr[2][j];
+      sep = sep || fabsf(tb) > h[j] + h[0] * Ar[0][j] + h[1] * Ar[1][j] + h[2] * Ar[2][j] + MARGIN;
+    }
+    for (int i = 0; i < 3; i++) {
+      const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+      for (int j = 0; j < 3; j++) {
+        const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+        const float ra = h[i1] * Ar[i2][j] + h[i2] * Ar[i1][j];
+        const float rb = h[j1] * Ar[i][j2] + h[j2] * Ar[i][j1];
+        sep = sep || fabsf(Ta[i2] * Rr[i1][j] - Ta[i1] * Rr[i2][j]) > ra + rb + MARGIN;
+      }
+    }
+    return sep;
+  }
+
   static DK void collision(LP L, int lane, const float* hf) {
     STAGE_T0();
     collide_planes(L, lane, hf);
@@ -1079,7 +1117,7 @@ struct TPhys {
       mulmv3(t, R2, hc);
       for (int a = 0; a < 3; a++) c2[a] = p2[a] + t[a];
       const float cc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
-      if (dot3(cc, cc) > 4.0f * Md::hull_radius * Md::hull_radius) {
+      if (dot3(cc, cc) > 4.0f * Md::hull_radius * Md::hull_radius || boxes_separated(p1, R1, p2, R2)) {
         if (lane < 4) {
           const float nofr[9] = {0, 0, 1, 0, 1, 0, -1, 0, 0};
           const float zero[3] = {L[Ly::COM], L[Ly::COM + 1], L[Ly::COM + 2]};

@@ -139,3 +139,33 @@ def test_flight_obeys_newton_euler(task, gpu):
     print(f"{task}: force p50 {np.median(f):.2e} max {f.max():.2e}; moment p50 {np.median(mom):.2e} max {mom.max():.2e}")
     assert np.isfinite(g["qacc"]).all()
     assert np.quantile(r, 0.99) < 1e-5 and r.max() < 3e-5, (np.quantile(r, 0.99), r.max())
+
+
+def test_foot_foot_contacts_match_oracle(gpu):
+    """Foot/foot (hull/hull) contacts at 4096 robots in flight (flight_states seed 7: feet touch
+    in a few dozen): the HIP path (bounding sphere, then box/box SAT prefilter, then the hull SAT)
+    reports the same active contacts as the oracle's full hull SAT."""
+    from tests.physics_laws import flight_states
+    n = 4096
+    env = Joystick("flat_terrain", num_envs=1, device=gpu, use_imitation=False)
+    m = env.mj_model
+    qpos, qvel, ctrl = flight_states(m, n, seed=7)
+    T = lambda a: torch.tensor(np.ascontiguousarray(a.T), dtype=torch.float32, device=gpu)
+    tq, tv, tw, tc = T(qpos), T(qvel), T(np.zeros((n, m.nv))), T(ctrl)
+    aux = torch.zeros(env.aux_size() * n, dtype=torch.float32, device=gpu).view(-1, n)
+    env.physics_step(tq, tv, tw, tc, 0, aux)
+    torch.cuda.synchronize()
+    g = parse_aux(m, aux.cpu().numpy().astype(np.float64))["con_dist"][:, :4]
+    om = OracleModel(m)
+    q32 = qpos.astype(np.float32).astype(np.float64)
+    r = []
+    for e in range(n):
+        d = om.new_data(qpos=q32[e], qvel=qvel[e], ctrl=ctrl[e])
+        om.forward(d)
+        r.append(d.arr("con_dist", 4 * m.npair)[:4].copy())
+    r = np.array(r)
+    act_r, act_g = (r < 0).any(axis=1), (g < 0).any(axis=1)
+    assert act_r.sum() >= 10
+    assert (act_r == act_g).mean() > 0.999, (act_r.sum(), act_g.sum())
+    both = act_r & act_g
+    np.testing.assert_allclose(np.where(r[both] < 0, r[both], 0), np.where(g[both] < 0, g[both], 0), atol=1e-5)
