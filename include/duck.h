@@ -46,7 +46,7 @@ const char* duck_last_error(void);
 int duck_layout_get(int nq, int nv, int nu, int imitation, int task, duck_layout* out);
 /* size in floats of the per-env debug record written by duck_physics_step(aux) */
 int duck_aux_size(const duck_sim* sim);
-/* debug: per-stage cycle counters of a -DDUCK_STAGE_PROF build (32 x uint64, optionally
+/* debug: per-stage cycle counters of a -DDUCK_STAGE_PROF build (32 + 1024 x uint64: 32 stage counters, then per-wave cycles of the last launch; optionally
  * reset); DUCK_EUNSUPPORTED in a regular build */
 int duck_debug_stage_cycles(const duck_sim* sim, unsigned long long* out, int reset);
 

@@ -751,6 +751,9 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
 template <class Md, int WG>
 __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   STAGE_T0();
+#ifdef DUCK_ANY_PROF
+  const unsigned long long kstart = clock64();
+#endif
 #if DUCK_TEAM
   {
     extern __shared__ float lds_t[];
@@ -795,6 +798,9 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   step_env<Md, Col<0>, false>(A, e, lane, L, G, G, r);
 #endif
   STAGE_MARK(15);
+#ifdef DUCK_ANY_PROF
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_stage_cycles[32 + 4 * blockIdx.x + threadIdx.x / 64] = clock64() - kstart;
+#endif
 }
 
 template <class Md, int WG>
@@ -965,10 +971,10 @@ static int launch_physics(duck_sim* s, int n, float* qpos, float* qvel, float* w
 }
 
 static int stage_cycles_of(unsigned long long* out, int reset) {
-#ifdef DUCK_STAGE_PROF
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), sizeof(unsigned long long) * 32);
+#ifdef DUCK_ANY_PROF
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), sizeof(unsigned long long) * (32 + 1024));
   if (e == hipSuccess && reset) {
-    unsigned long long z[32] = {0};
+    static unsigned long long z[32 + 1024] = {0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, sizeof(z));
   }
   return e == hipSuccess ? 0 : DUCK_EHIP;

@@ -31,9 +31,17 @@
 // vector-memory pipe)
 typedef __attribute__((address_space(3))) float lds_float;
 
-// optional per-stage cycle counters (build with -DDUCK_STAGE_PROF; read by duck_debug_stage_cycles)
+// optional per-stage cycle counters (build with -DDUCK_STAGE_PROF; read by duck_debug_stage_cycles);
+// -DDUCK_WAVE_PROF records only the per-wave launch cycles (no stage marks perturbing wave 0)
+#if defined(DUCK_STAGE_PROF) || defined(DUCK_WAVE_PROF)
+#define DUCK_ANY_PROF 1
+#endif
+#ifdef DUCK_ANY_PROF
+static __device__ unsigned long long g_stage_cycles[32 + 1024];
+#endif
 #ifdef DUCK_STAGE_PROF
-static __device__ unsigned long long g_stage_cycles[32];
+// g_stage_cycles: [0, 32) stage counters; [32, 32 + 1024) cycles of each of the first 1024 waves
+// of the last step_kernel launch (wave = 4 * workgroup + wave-in-workgroup), for the launch tail
 #define STAGE_T0() unsigned long long _t0 = wall_clock64(), _c0 = clock64()
 #define STAGE_RESET() (_c0 = clock64())
 #define STAGE_MARK(k)                                                             \

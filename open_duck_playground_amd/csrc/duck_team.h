@@ -1578,6 +1578,9 @@ struct TPhys {
       STAGE_MARK(11);
     } else {
       TSYNC();
+#ifdef DUCK_STAGE_PROF
+      if (lane == 0) atomicAdd(&g_stage_cycles[23], 1ull);  // dense Newton fallbacks
+#endif
       S1 Ls{L};
       P1::newton_direction(Ls);  // all lanes, identical values
       P1::dense_direction(Ls, scratch, stride);

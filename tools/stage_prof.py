@@ -38,7 +38,7 @@ def main():
     for i in range(20):
         env.step(st, pool[i % len(pool)])
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * 32)()
+    buf = (C.c_ulonglong * (32 + 1024))()
     lib = native.lib()
     lib.duck_debug_stage_cycles(env._sim, buf, 1)
     steps = 5
@@ -48,7 +48,7 @@ def main():
     lib.duck_debug_stage_cycles(env._sim, buf, 1)
     nwg = (n + 15) // 16
     per_sub = lambda k: buf[k] / (nwg * steps * 10)
-    tot = sum(buf[k] for k in TOP)
+    tot = sum(buf[k] for k in TOP) or 1  # (0 in a -DDUCK_WAVE_PROF build: wave times only)
     for k, name in TOP.items():
         print(f"{name:28s} {per_sub(k):10.0f} cycles/substep/wave  {100 * buf[k] / tot:5.1f}%")
     for k, name in SUB.items():
@@ -56,8 +56,23 @@ def main():
     per = lambda k: buf[k] / (nwg * steps)
     for k, name in ENV.items():
         print(f"{name:28s} {per(k):10.0f} cycles/env-step/wave")
+    import numpy as np
+    w = np.array([buf[32 + i] for i in range(min(1024, 4 * nwg))], dtype=np.float64)
+    w = w[w > 0]
+    if len(w):
+        print(f"{'wave cycles (last launch)':28s} mean {w.mean():.0f}  p50 {np.median(w):.0f}  p99 {np.quantile(w, 0.99):.0f}  "
+              f"max {w.max():.0f}  max/mean {w.max() / w.mean():.3f}")
+        if len(w) == 4 * nwg and "--waves" in sys.argv:
+            wg = w.reshape(-1, 4)
+            print("  per-workgroup max/min spread: mean %.3f" % (wg.max(1) / wg.min(1)).mean())
+            print("  per-XCD (blockIdx % 8) mean wave cycles:", [int(wg[x::8].mean()) for x in range(8)])
+            print("  per wave-in-workgroup mean:", [int(wg[:, k].mean()) for k in range(4)])
+            print("  slowest workgroups:", list(np.argsort(wg.max(1))[-8:]))
+    print(f"{'dense Newton fallbacks':28s} {buf[23] / steps:10.1f} per env-step (all {n} envs)")
     print(f"{'foot/foot SAT runs':28s} {buf[27] / steps:10.1f} per env-step (all {n} envs)")
     kern = per(14) + per(15)
+    if kern == 0:
+        return
     print(f"{'kernel (per env-step)':28s} {kern:10.0f} cycles/env-step/wave")
     print(f"{'  model-table copy':28s} {per(14):10.0f}  {100 * per(14) / kern:5.1f}%")
     print(f"{'  10 substeps':28s} {tot / (nwg * steps):10.0f}  {100 * tot / (nwg * steps) / kern:5.1f}%")
