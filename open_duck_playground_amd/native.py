@@ -53,7 +53,7 @@ def build(verbose: bool = False, defines=(), out: str = None) -> str:
     # multi-instruction sequences: the physics tolerances are fp32-vs-fp64 anyway; fp32
     # denormals flushed (no frexp/ldexp range scaling around v_rcp/v_sqrt/sincos)
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-hip-fp32-correctly-rounded-divide-sqrt",
-             "-fgpu-flush-denormals-to-zero"] + \
+             "-fgpu-flush-denormals-to-zero", "-fno-slp-vectorize"] + \
         [f"-D{d}" for d in defines]
     with tempfile.TemporaryDirectory() as tmp:
         objs, procs = [], []
