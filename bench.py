@@ -173,6 +173,14 @@ def main():
         t = json.load(open(tpath)).get(args.config)
         if t and n == CONFIGS[args.config]["envs"]:
             traffic = t["bytes_per_launch"]
+    issue = None
+    spath = os.path.join(ROOT, "profiles", "r01_sq_c2.json")
+    if args.config == "C2" and n == CONFIGS["C2"]["envs"] and os.path.exists(spath):
+        # the step kernel's own bound: one wave per SIMD on a dependent chain;
+        # SQ issue fractions of the committed rocprofv3 --pmc run of this config
+        q = json.load(open(spath))
+        issue = {k: round(q[k], 3) for k in ("valu_busy_frac", "waitcnt_frac", "lds_busy_frac", "salu_frac")}
+        issue["source"] = "profiles/r01_sq_c2.json"
     if rank == 0:
         B = algorithmic_bytes(env)
         achieved = B * n / (kern_ms * 1e-3) / 1e9
@@ -191,6 +199,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "step_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": B},
             "cpu_baseline": cpu,
+            "issue": issue,
             "finite": ok,
         }
         print(json.dumps(line), flush=True)
