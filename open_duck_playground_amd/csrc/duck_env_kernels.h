@@ -766,35 +766,55 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   if (t < 0) return;
   const int e = blockIdx.x * WG + t;
   const int n = A.n;
-  if (e >= n) return;
   extern __shared__ float lds[];
+#if DUCK_TEAM
+  using TL = TLay<Md>;
+  if constexpr (TL::ES_LDS) {
+    // hot state <-> LDS by the whole workgroup, field-major: a wave instruction moves 4 fields
+    // x 16 consecutive envs (four 64-B segments of the [field][env] rows) instead of 16 fields x
+    // 4 envs; the step's 64 random draws are made by each team in parallel into the same region
+    const int j = threadIdx.x % WG, ej = blockIdx.x * WG + j;
+    lds_float* esj = (lds_float*)(lds + TL::ES + j * TL::ESTRIDE);
+    if (ej < n)
+      for (int k = threadIdx.x / WG; k < TL::HOT; k += TPB / WG) esj[k] = A.fs[(size_t)k * n + ej];
+    __syncthreads();
+    if (e < n) {
+      const Slice<SW> L = env_slice<Md>(lds, t);
+      const Col<0> G{A.fs + e, n};  // global row: the auto-reset snapshot (first_*) stays in HBM
+      const duck_layout& Lo = A.lay;
+      lds_float* esp = (lds_float*)(lds + TL::ES + t * TL::ESTRIDE);
+      RngTab rt;
+      rt.k0 = (uint32_t)A.is[(size_t)Lo.rng_key * n + e];
+      rt.k1 = (uint32_t)A.is[(size_t)(Lo.rng_key + 1) * n + e];
+      rt.ctr = (uint32_t)A.is[(size_t)Lo.rng_ctr * n + e];
+      rt.tab = esp + TL::HOT;
+      rt.fill(esp + TL::HOT, lane);
+      TSYNC();
+      step_env<Md, LCol, true>(A, e, lane, L, LCol{esp}, G, rt);
+    }
+    __syncthreads();
+    if (ej < n)
+      for (int k = threadIdx.x / WG; k < TL::HOT; k += TPB / WG) A.fs[(size_t)k * n + ej] = esj[k];
+  } else {
+    if (e >= n) return;
+    const Slice<SW> L = env_slice<Md>(lds, t);
+    const Col<0> G{A.fs + e, n};
+    const duck_layout& Lo = A.lay;
+    Rng r;
+    r.k0 = (uint32_t)A.is[(size_t)Lo.rng_key * n + e];
+    r.k1 = (uint32_t)A.is[(size_t)(Lo.rng_key + 1) * n + e];
+    r.ctr = (uint32_t)A.is[(size_t)Lo.rng_ctr * n + e];
+    step_env<Md, Col<0>, true>(A, e, lane, L, G, G, r);
+  }
+#else
+  if (e >= n) return;
   const Slice<SW> L = env_slice<Md>(lds, t);
-  const Col<0> G{A.fs + e, n};  // global row: the auto-reset snapshot (first_*) stays in HBM
+  const Col<0> G{A.fs + e, n};
   const duck_layout& Lo = A.lay;
   Rng r;
   r.k0 = (uint32_t)A.is[(size_t)Lo.rng_key * n + e];
   r.k1 = (uint32_t)A.is[(size_t)(Lo.rng_key + 1) * n + e];
   r.ctr = (uint32_t)A.is[(size_t)Lo.rng_ctr * n + e];
-#if DUCK_TEAM
-  using TL = TLay<Md>;
-  if constexpr (TL::ES_LDS) {
-    // hot state -> LDS: the team's 16 lanes issue the env's loads together (one latency),
-    // and write it back together at the end; the step's 64 random draws are made by the
-    // team in parallel into the same region
-    lds_float* esp = (lds_float*)(lds + TL::ES + t * TL::ESTRIDE);
-    for (int k = lane; k < TL::HOT; k += TEAM) esp[k] = A.fs[(size_t)k * n + e];
-    RngTab rt;
-    rt.k0 = r.k0; rt.k1 = r.k1; rt.ctr = r.ctr;
-    rt.tab = esp + TL::HOT;
-    rt.fill(esp + TL::HOT, lane);
-    TSYNC();
-    step_env<Md, LCol, true>(A, e, lane, L, LCol{esp}, G, rt);
-    TSYNC();
-    for (int k = lane; k < TL::HOT; k += TEAM) A.fs[(size_t)k * n + e] = esp[k];
-  } else {
-    step_env<Md, Col<0>, true>(A, e, lane, L, G, G, r);
-  }
-#else
   step_env<Md, Col<0>, false>(A, e, lane, L, G, G, r);
 #endif
   STAGE_MARK(15);
