@@ -155,3 +155,55 @@ def test_env_offset_shards_are_bit_identical(gpu):
         got = torch.cat([s.obs[key] for s in sp])
         assert torch.equal(got, sf.obs[key]), key
     assert torch.equal(torch.cat([s.reward for s in sp]), sf.reward)
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C4", "C5"])
+def test_full_size_runs_are_deterministic(cfg, gpu):
+    """At the bench's sizes (C2 4096 flat, C4 8192 rough + DR, C5 4096 rough + DR + backlash), two
+    runs from the same seeds give bit-identical obs, privileged obs, rewards and dones: no races
+    between the team's lanes or the workgroup's staging, no order-dependent reductions."""
+    from bench import CONFIGS
+    c = CONFIGS[cfg]
+    n = c["envs"]
+    g = torch.Generator(device=gpu)
+    g.manual_seed(5)
+    acts = [torch.rand(n, 14, device=gpu, generator=g) * 2 - 1 for _ in range(6)]
+    out = []
+    for run in range(2):
+        env = wrap_for_brax_training(Joystick(c["task"], num_envs=n, device=gpu, use_imitation=c["imitation"]),
+                                     episode_length=1000, randomization_fn=domain_randomize if c["dr"] else None)
+        st = env.reset(rng=3)
+        for a in acts:
+            env.step(st, a)
+        torch.cuda.synchronize()
+        out.append([st.obs["state"].clone(), st.obs["privileged_state"].clone(), st.reward.clone(), st.done.clone()])
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
+
+
+def test_full_size_long_rollout_with_auto_reset(gpu):
+    """4096 envs x 300 env-steps of U(-1,1) actions with a 100-step episode limit: every row stays
+    finite and the EpisodeWrapper/AutoReset bookkeeping holds for every env: an env is done at the
+    latest on its 100th step since its last reset, truncation marks exactly those, falls are the
+    other dones (BraxAutoResetWrapper semantics, common/runner.py:117)."""
+    n = 4096
+    env = wrap_for_brax_training(Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False),
+                                 episode_length=100)
+    st = env.reset(rng=0)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(1234)
+    ep = torch.zeros(n, device=gpu)
+    falls = truncs = 0
+    for t in range(300):
+        env.step(st, torch.rand(n, 14, device=gpu, generator=g) * 2 - 1)
+        ep += 1
+        done, trunc = st.done, st.info["truncation"]
+        assert bool((trunc <= done).all())
+        assert bool(((ep >= 100) <= (done == 1)).all())          # nobody runs past the limit
+        assert bool(((trunc == 1) <= (ep == 100)).all())         # truncation only at the limit
+        falls += int((done - trunc).sum().item())
+        truncs += int(trunc.sum().item())
+        ep = torch.where(done == 1, torch.zeros_like(ep), ep)
+        if t % 50 == 49:
+            assert torch.isfinite(st.obs["state"]).all() and torch.isfinite(st.obs["privileged_state"]).all()
+    assert truncs > 0 and falls > 0
