@@ -66,6 +66,20 @@ DK float tsum(float v) {
   v += dppf<0x140>(v);  // row_mirror
   return v;
 }
+DK float tmaxf(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  v = fmaxf(v, dppf<0x140>(v));
+  return v;
+}
+DK int tmini(int v) {
+  v = min(v, dppi<0xB1>(v));
+  v = min(v, dppi<0x4E>(v));
+  v = min(v, dppi<0x141>(v));
+  v = min(v, dppi<0x140>(v));
+  return v;
+}
 // reductions over the 8-lane halves of a team
 DK float hmax8(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
@@ -1098,6 +1112,166 @@ struct TPhys {
     return sep;
   }
 
+  // Hull/hull (foot/foot) SAT with the team: mjx / oracle collide_convex_convex semantics, the
+  // axes split over the lanes. Face axes (both hulls, 60) then edge-pair axes (45 x 45); a
+  // separating axis anywhere means no contact (the 4 slots stay inactive); otherwise the best
+  // face (largest separation, first index among equal ones) unless the best edge pair beats it
+  // by 1e-9 (declared deviation: the single-lane scan applies that margin per step, here it is
+  // applied to the edges' maximum). Vertices and edge directions in world coordinates are kept
+  // in registers (vertices) and in the dead H / constraint-row storage (edges).
+  static DK void collide_hulls_team(LP L, int lane, int slot0, const float* p1, const float* R1, const float* p2,
+                                    const float* R2, const float* cc) {
+    constexpr int NH = Md::NHV, NF = Md::NHF, NE = Md::NHE;
+    constexpr int EA = Ly::H, EB = EA + 3 * NE;
+    static_assert(EB + 3 * NE <= Ly::CR, "edge scratch must fit in the H / row storage");
+    S1 Ls{L};
+    if (lane < 4) {
+      const float nofr[9] = {0, 0, 1, 0, 1, 0, -1, 0, 0};
+      const float zero[3] = {L[Ly::COM], L[Ly::COM + 1], L[Ly::COM + 2]};
+      P1::store_contact(Ls, slot0 + lane, 1.0f, zero, nofr);
+    }
+    float V1[NH][3], V2[NH][3], t[3];
+#pragma unroll
+    for (int k = 0; k < NH; k++) {
+      const float v[3] = {tf(Md::B_HULL + 3 * k), tf(Md::B_HULL + 3 * k + 1), tf(Md::B_HULL + 3 * k + 2)};
+      mulmv3(t, R1, v);
+      for (int q = 0; q < 3; q++) V1[k][q] = p1[q] + t[q];
+      mulmv3(t, R2, v);
+      for (int q = 0; q < 3; q++) V2[k][q] = p2[q] + t[q];
+    }
+    const int(*HE)[2] = Md::hull_edge_d();
+    const float(*HN)[3] = Md::hull_face_normal_d();
+    for (int e = lane; e < NE; e += TEAM) {
+      const int a0 = HE[e][0], a1 = HE[e][1];
+      float d[3];
+      for (int q = 0; q < 3; q++) d[q] = tf(Md::B_HULL + 3 * a1 + q) - tf(Md::B_HULL + 3 * a0 + q);
+      mulmv3(t, R1, d);
+      for (int q = 0; q < 3; q++) L[EA + 3 * e + q] = t[q];
+      mulmv3(t, R2, d);
+      for (int q = 0; q < 3; q++) L[EB + 3 * e + q] = t[q];
+    }
+    TSYNC();
+    auto sep_of = [&](const float* u) {
+      float mx1 = -1e30f, mn2 = 1e30f;
+#pragma unroll
+      for (int k = 0; k < NH; k++) {
+        mx1 = fmaxf(mx1, dot3(u, V1[k]));
+        mn2 = fminf(mn2, dot3(u, V2[k]));
+      }
+      return mn2 - mx1;
+    };
+    constexpr int NONE = 1 << 20;
+    // face axes a = side * NF + f
+    float bsep = -1e30f, bu[3] = {0.0f, 0.0f, 1.0f};
+    int bidx = NONE;
+    float anysep = 0.0f;
+    for (int a = lane; a < 2 * NF; a += TEAM) {
+      const int side = a / NF, f = a - side * NF;
+      float u[3];
+      mulmv3(u, side == 0 ? R1 : R2, HN[f]);
+      if (side == 1) { u[0] = -u[0]; u[1] = -u[1]; u[2] = -u[2]; }
+      const float sp = sep_of(u);
+      anysep += sp > 0.0f ? 1.0f : 0.0f;
+      if (sp > bsep) { bsep = sp; bidx = a; bu[0] = u[0]; bu[1] = u[1]; bu[2] = u[2]; }
+    }
+    if (tsum(anysep) > 0.0f) return;
+    float best = tmaxf(bsep);
+    const int fbest = tmini(bsep == best ? bidx : NONE);
+    int btype = fbest / NF, bi = fbest - btype * NF, bj = 0;
+    float u_best[3];
+    for (int q = 0; q < 3; q++) u_best[q] = __shfl(bu[q], fbest % TEAM, TEAM);
+    // edge-pair axes q = e1 * NE + e2, 16 per round; any separation ends the test
+    float esep = -1e30f, eu[3] = {0.0f, 0.0f, 1.0f};
+    int eidx = NONE;
+    for (int base = 0; base < NE * NE; base += TEAM) {
+      const int q = base + lane;
+      float sepq = 0.0f;
+      if (q < NE * NE) {
+        const int e1 = q / NE, e2 = q - e1 * NE;
+        const float ea[3] = {L[EA + 3 * e1], L[EA + 3 * e1 + 1], L[EA + 3 * e1 + 2]};
+        const float eb[3] = {L[EB + 3 * e2], L[EB + 3 * e2 + 1], L[EB + 3 * e2 + 2]};
+        float u[3];
+        cross3(u, ea, eb);
+        const float un = sqrtf(dot3(u, u));
+        if (!(un < 1e-6f * sqrtf(dot3(ea, ea)) * sqrtf(dot3(eb, eb)))) {
+          u[0] /= un; u[1] /= un; u[2] /= un;
+          if (dot3(u, cc) < 0.0f) { u[0] = -u[0]; u[1] = -u[1]; u[2] = -u[2]; }
+          const float sp = sep_of(u);
+          sepq = sp > 0.0f ? 1.0f : 0.0f;
+          if (sp > esep) { esep = sp; eidx = q; eu[0] = u[0]; eu[1] = u[1]; eu[2] = u[2]; }
+        }
+      }
+      if (tsum(sepq) > 0.0f) return;
+    }
+    const float em = tmaxf(esep);
+    const int ebest = tmini(esep == em ? eidx : NONE);
+    float u_edge[3];
+    for (int q = 0; q < 3; q++) u_edge[q] = __shfl(eu[q], ebest % TEAM, TEAM);
+    if (ebest < NONE && em > best + 1e-9f) {
+      best = em;
+      btype = 2;
+      bi = ebest / NE;
+      bj = ebest - bi * NE;
+      for (int q = 0; q < 3; q++) u_best[q] = u_edge[q];
+    }
+    // the contact, uniform over the team (the single-lane code's tail)
+    TSYNC();
+    float fr[9];
+    make_frame(fr, u_best);
+    if (btype == 2) {
+      float a0[3], a1[3], b0[3], b1[3];
+      pick3<NH>(V1, HE[bi][0], a0);
+      pick3<NH>(V1, HE[bi][1], a1);
+      pick3<NH>(V2, HE[bj][0], b0);
+      pick3<NH>(V2, HE[bj][1], b1);
+      float d1[3], d2[3], r[3];
+      for (int a = 0; a < 3; a++) { d1[a] = a1[a] - a0[a]; d2[a] = b1[a] - b0[a]; r[a] = a0[a] - b0[a]; }
+      const float A = dot3(d1, d1), E = dot3(d2, d2), F = dot3(d2, r), C = dot3(d1, r), B = dot3(d1, d2);
+      const float den = A * E - B * B;
+      float sc = den > 1e-15f ? (B * F - C * E) / den : 0.0f;
+      sc = fminf(fmaxf(sc, 0.0f), 1.0f);
+      float tt = E > 1e-15f ? (B * sc + F) / E : 0.0f;
+      if (tt < 0.0f) { tt = 0.0f; sc = A > 1e-15f ? -C / A : 0.0f; }
+      else if (tt > 1.0f) { tt = 1.0f; sc = A > 1e-15f ? (B - C) / A : 0.0f; }
+      sc = fminf(fmaxf(sc, 0.0f), 1.0f);
+      float pos[3];
+      for (int a = 0; a < 3; a++) pos[a] = 0.5f * (a0[a] + sc * d1[a] + b0[a] + tt * d2[a]);
+      if (lane == 0) P1::store_contact(Ls, slot0, best, pos, fr);
+      return;
+    }
+    const float* Rr = btype == 0 ? R1 : R2;
+    const float* pr = btype == 0 ? p1 : p2;
+    float fn[3];
+    mulmv3(fn, Rr, HN[bi]);
+    const float off = Md::hull_face_offset_d()[bi] + dot3(fn, pr);
+    float support[NH];
+    bool mask[NH];
+    float smax = -1e30f;
+#pragma unroll
+    for (int k = 0; k < NH; k++) {
+      const float* v = btype == 0 ? V2[k] : V1[k];
+      support[k] = off - dot3(fn, v);
+      smax = fmaxf(smax, support[k]);
+    }
+    const float thr = fmaxf(smax - 1e-3f, 0.0f);
+#pragma unroll
+    for (int k = 0; k < NH; k++) mask[k] = support[k] > thr;
+    int idx[4];
+    if (btype == 0) manifold_points<NH>(V2, mask, fn, idx);
+    else manifold_points<NH>(V1, mask, fn, idx);
+    if (lane < 4) {
+      const int c = lane;
+      bool unique = true;
+      for (int e = 0; e < 4; e++) unique = unique && !(e < c && idx[e] == idx[c]);
+      const float dist = unique ? -pick1<NH>(support, idx[c]) : 1.0f;
+      float v[3], pos[3];
+      if (btype == 0) pick3<NH>(V2, idx[c], v);
+      else pick3<NH>(V1, idx[c], v);
+      for (int a = 0; a < 3; a++) pos[a] = v[a] - 0.5f * dist * fn[a];
+      P1::store_contact(Ls, slot0 + c, dist, pos, fr);
+    }
+  }
+
   static DK void collision(LP L, int lane, const float* hf) {
     STAGE_T0();
     collide_planes(L, lane, hf);
@@ -1128,7 +1302,7 @@ struct TPhys {
 #ifdef DUCK_STAGE_PROF
         if (lane == 0) atomicAdd(&g_stage_cycles[27], 1ull);  // how often the SAT path runs
 #endif
-        P1::collide_hulls(Ls, s1, s2, 4 * p);  // rare: every lane runs the single-lane path
+        collide_hulls_team(L, lane, 4 * p, p1, R1, p2, R2, cc);  // rare: the boxes overlap
       }
     }
     TSYNC();
