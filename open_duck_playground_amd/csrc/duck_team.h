@@ -721,6 +721,61 @@ struct TPhys {
     for (int s = 0; s < NC; s++) x[s] = x[s] * __builtin_amdgcn_rcpf(F.dg[s]);
     fwd_all(F, x, lane, std::make_integer_sequence<int, NV>{});
   }
+  // out of line so the rare dense path does not share the hot path's code layout / registers
+  static DNI void newton_dense(LP L, int lane) {
+    float Mc[NC][NV];
+    load_cols(L, lane, Ly::M, Mc, false);
+    newton_fused<true>(L, lane, Mc);
+  }
+  // dense variant (a full lower triangle): pivots in natural order NV-1 .. 0, each updating every
+  // row above it; then the same mask-free solves, also in natural order
+  template <int K, int I>
+  static DK void fac_rows_dense(Fac& F, float inv) {
+    if constexpr (I >= 0) {
+      const float t = bc<I % TEAM>(F.col[I / TEAM][K]) * inv;
+#pragma unroll
+      for (int s = 0; s < NC; s++)
+        if (TEAM * s <= I) F.col[s][I] -= t * F.col[s][K];
+      fac_rows_dense<K, I - 1>(F, inv);
+    }
+  }
+  template <int K>
+  static DK void fac_pass_dense(Fac& F, int lane) {
+    constexpr int ks = K / TEAM, kl = K % TEAM;
+    const float dk = bc<kl>(F.col[ks][K]);
+    F.dg[ks] = lane == kl ? F.col[ks][K] : F.dg[ks];
+    const float inv = __builtin_amdgcn_rcpf(dk);
+    fac_rows_dense<K, K - 1>(F, inv);
+#pragma unroll
+    for (int s = 0; s < NC; s++)
+      if (TEAM * s <= K) F.col[s][K] *= inv;
+  }
+  template <int... J>
+  static DK void fac_all_dense(Fac& F, int lane, std::integer_sequence<int, J...>) {
+    (fac_pass_dense<NV - 1 - J>(F, lane), ...);
+  }
+  template <int... J>
+  static DK void back_all_dense(const Fac& F, float* x, std::integer_sequence<int, J...>) {
+    (sol_back<NV - 1 - J>(F, x), ...);
+  }
+  template <int... J>
+  static DK void fwd_all_dense(const Fac& F, float* x, int lane, std::integer_sequence<int, J...>) {
+    (sol_fwd<J>(F, x, lane), ...);
+  }
+  static DK void factor_solve_dense(Fac& F, float* x, int lane) {
+#pragma unroll
+    for (int s = 0; s < NC; s++) F.dg[s] = 1.0f;
+    fac_all_dense(F, lane, std::make_integer_sequence<int, NV>{});
+#pragma unroll
+    for (int s = 0; s < NC; s++)
+#pragma unroll
+      for (int r = TEAM * s + 1; r < NV; r++) F.col[s][r] = lane < r - TEAM * s ? F.col[s][r] : 0.0f;
+    back_all_dense(F, x, std::make_integer_sequence<int, NV>{});
+#pragma unroll
+    for (int s = 0; s < NC; s++) x[s] = x[s] * __builtin_amdgcn_rcpf(F.dg[s]);
+    fwd_all_dense(F, x, lane, std::make_integer_sequence<int, NV>{});
+  }
+
   static DK void set_desc(Fac& F, int lane) {
 #pragma unroll
     for (int s = 0; s < NC; s++) {
@@ -792,12 +847,18 @@ struct TPhys {
   // Newton direction at (QACC, JA, MA) with H = M + J'DJ assembled directly into register
   // columns (mjx _update_gradient + the Cholesky solve): SRCH = -H^-1 grad. Returns false
   // (nothing written) when foot/foot contact rows are active.
+  // FF = false: the common case, tree-sparse H (returns false, nothing written, when foot/foot
+  // contact rows are active). FF = true: those rows included — their Jacobian J_geom2 - J_geom1
+  // couples the two legs, so H is assembled densely and factored by factor_solve_dense.
+  template <bool FF>
   static DK bool newton_fused(LP L, int lane, const float (*Mc)[NV]) {
     STAGE_T0();
-    if (Md::FOOT_PAIR >= 0) {
-      const int row = R_CON + 16 * Md::FOOT_PAIR + lane;
-      const float act = (L[Ly::JA + row] < 0.0f && L[Ly::RD + row] != 0.0f) ? 1.0f : 0.0f;
-      if (tsum(act) > 0.0f) return false;
+    if constexpr (!FF) {
+      if (Md::FOOT_PAIR >= 0) {
+        const int row = R_CON + 16 * Md::FOOT_PAIR + lane;
+        const float act = (L[Ly::JA + row] < 0.0f && L[Ly::RD + row] != 0.0f) ? 1.0f : 0.0f;
+        if (tsum(act) > 0.0f) return false;
+      }
     }
     Fac F;
     float g[NC];
@@ -880,8 +941,63 @@ struct TPhys {
         }
       }
     }
+    if constexpr (FF) {
+      if constexpr (Md::FOOT_PAIR >= 0) {
+        // foot/foot rows: J = a . (S_2 - S_1) with S_k the cdof columns of geom k's body chain
+        // (shared free-joint dofs cancel); K_ff, F_ff by team sums, then signed projections
+        constexpr int p = Md::FOOT_PAIR;
+        constexpr int g1 = cgeom_slot<Md>(Md::pair_geom1[p]), g2 = cgeom_slot<Md>(Md::pair_geom2[p]);
+        constexpr unsigned M1 = chain_mask(g1 == 1 ? Md::LFOOT_BODY : Md::RFOOT_BODY);
+        constexpr unsigned M2 = chain_mask(g2 == 1 ? Md::LFOOT_BODY : Md::RFOOT_BODY);
+        const float mu = tf(Md::B_PAIR + PAIRW * p + 2);
+        const int slot = 4 * p + (lane >> 2), e = lane & 3, row = R_CON + 4 * slot + e;
+        const float D = L[Ly::RD + row], x = L[Ly::JA + row];
+        const float w = (x < 0.0f && D != 0.0f) ? D : 0.0f;
+        const float force = -w * x;
+        const int t = 1 + (e >> 1);
+        const float sg = (e & 1) ? -mu : mu;
+        float u[3], r3[3], a[6];
+        for (int q = 0; q < 3; q++) {
+          u[q] = L[Ly::CFR + 9 * slot + q] + sg * L[Ly::CFR + 9 * slot + 3 * t + q];
+          r3[q] = L[Ly::CR + 3 * slot + q];
+        }
+        cross3(a, r3, u);
+        a[3] = u[0]; a[4] = u[1]; a[5] = u[2];
+        float K[21], Fv[6];
+        {
+          int o = 0;
+          for (int q = 0; q < 6; q++)
+            for (int kk = q; kk < 6; kk++) { K[o] = tsum(w * a[q] * a[kk]); o++; }
+          for (int q = 0; q < 6; q++) Fv[q] = tsum(force * a[q]);
+        }
+#pragma unroll
+        for (int s = 0; s < NC; s++) {
+          const int c = TEAM * s + lane, cc = c < NV ? c : 0;
+          const float sc = c < NV ? (float)((int)((M2 >> cc) & 1u) - (int)((M1 >> cc) & 1u)) : 0.0f;
+          float cdc[6], kc[6];
+          for (int k = 0; k < 6; k++) cdc[k] = sc * L[Ly::CDOF + 6 * cc + k];
+          float gf = 0.0f;
+          for (int q = 0; q < 6; q++) {
+            float sacc = 0.0f;
+            for (int k = 0; k < 6; k++) sacc += K[kidx(q, k)] * cdc[k];
+            kc[q] = sacc;
+            gf += cdc[q] * Fv[q];
+          }
+          g[s] -= gf;
+#pragma unroll
+          for (int r = 0; r < NV; r++) {
+            const int sr = (int)((M2 >> r) & 1u) - (int)((M1 >> r) & 1u);
+            if (sr == 0 || r < TEAM * s) continue;  // compile-time after unrolling
+            float h = 0.0f;
+            for (int k = 0; k < 6; k++) h += L[Ly::CDOF + 6 * r + k] * kc[k];
+            F.col[s][r] += sr > 0 ? h : -h;
+          }
+        }
+      }
+    }
     STAGE_MARK(17);
-    factor_solve(F, g, lane);
+    if constexpr (FF) factor_solve_dense(F, g, lane);
+    else factor_solve(F, g, lane);
     STAGE_MARK(18);
 #pragma unroll
     for (int s = 0; s < NC; s++) {
@@ -1746,7 +1862,7 @@ struct TPhys {
     }
     TSYNC();
     STAGE_MARK(9);
-    const bool sparse_ok = newton_fused(L, lane, Mc);
+    const bool sparse_ok = newton_fused<false>(L, lane, Mc);
     STAGE_MARK(10);
     if (sparse_ok) {
       STAGE_MARK(11);
@@ -1755,9 +1871,7 @@ struct TPhys {
 #ifdef DUCK_STAGE_PROF
       if (lane == 0) atomicAdd(&g_stage_cycles[23], 1ull);  // dense Newton fallbacks
 #endif
-      S1 Ls{L};
-      P1::newton_direction(Ls);  // all lanes, identical values
-      P1::dense_direction(Ls, scratch, stride);
+      newton_dense(L, lane);  // rare: foot/foot contact rows active (dense H)
       TSYNC();
     }
     // J.search and M.search in one pass; rows go straight to registers
