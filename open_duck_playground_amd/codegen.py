@@ -21,6 +21,8 @@ import numpy as np
 from .mjcf import JNT_FREE, Model, quat2mat
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# hull/hull SAT tie tolerance (m): axes within it of the best count as ties
+HULL_SAT_TIE = 1e-5
 
 
 def _f(x) -> str:
@@ -430,6 +432,20 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     return dev, acc
 
 
+def hull_edge_faces(hull) -> np.ndarray:
+    """The two faces adjacent to each hull edge (from the merged polygons): edge e is the
+    Gauss-map arc between the normals of faces [e][0] and [e][1] — the edge-pair filter of the
+    hull/hull SAT (oracle/duck_oracle.c derives the same table from the face planes)."""
+    adj = {}
+    for f, poly in enumerate(hull.face_vert):
+        for i in range(len(poly)):
+            a, b = poly[i], poly[(i + 1) % len(poly)]
+            adj.setdefault((min(a, b), max(a, b)), []).append(f)
+    out = [sorted(adj[(int(a), int(b))]) for a, b in hull.edge]
+    assert all(len(x) == 2 for x in out), "every hull edge must join exactly two faces"
+    return np.array(out, dtype=np.int64)
+
+
 def model_header(m: Model, variant: str) -> str:
     nb, nv, nq, nu, nj = m.nbody, m.nv, m.nq, m.nu, m.njnt
     rows, adr, nm = sparse_pattern(m)
@@ -464,16 +480,19 @@ def model_header(m: Model, variant: str) -> str:
     assert m.nsite <= 8 and len(m.hulls) == 1
     hc = hull.vert.mean(axis=0)
     hr = float(np.max(np.linalg.norm(hull.vert - hc, axis=1)))
+    hef = hull_edge_faces(hull)
     pre = f"DuckModel_{variant}"
     dev = [f"__device__ const float {pre}_hull_vert_d[{len(hull.vert)}][3] = {_arr('x', hull.vert, 'float').split('= ', 1)[1]}",
            f"__device__ const float {pre}_hull_face_normal_d[{len(hull.face_normal)}][3] = {_arr('x', hull.face_normal, 'float').split('= ', 1)[1]}",
            f"__device__ const float {pre}_hull_face_offset_d[{len(hull.face_offset)}] = {_arr('x', hull.face_offset, 'float').split('= ', 1)[1]}",
            f"__device__ const int {pre}_hull_edge_d[{len(hull.edge)}][2] = {_arr('x', hull.edge, 'int').split('= ', 1)[1]}",
+           f"__device__ const int {pre}_hull_edge_face_d[{len(hef)}][2] = {_arr('x', hef, 'int').split('= ', 1)[1]}",
            f"__device__ const int {pre}_chain_d[{nb}][{maxchain}] = {_arr('x', chain_arr, 'int').split('= ', 1)[1]}"]
     acc = [f"  static __device__ __forceinline__ const float (*hull_vert_d())[3] {{ return {pre}_hull_vert_d; }}\n",
            f"  static __device__ __forceinline__ const float (*hull_face_normal_d())[3] {{ return {pre}_hull_face_normal_d; }}\n",
            f"  static __device__ __forceinline__ const float* hull_face_offset_d() {{ return {pre}_hull_face_offset_d; }}\n",
            f"  static __device__ __forceinline__ const int (*hull_edge_d())[2] {{ return {pre}_hull_edge_d; }}\n",
+           f"  static __device__ __forceinline__ const int (*hull_edge_face_d())[2] {{ return {pre}_hull_edge_face_d; }}\n",
            f"  static __device__ __forceinline__ const int (*chain_d())[{maxchain}] {{ return {pre}_chain_d; }}\n"]
     out = [f"// generated by open_duck_playground_amd/codegen.py from assets/{m.name} — do not edit\n",
            "#pragma once\n\n"] + dev + [
@@ -491,6 +510,7 @@ def model_header(m: Model, variant: str) -> str:
            f"  static constexpr float meaninertia = {_f(m.stat_meaninertia)};\n",
            f"  static constexpr int iterations = {m.opt_iterations}, ls_iterations = {m.opt_ls_iterations};\n",
            f"  static constexpr float hull_radius = {_f(hr)};\n",
+           f"  static constexpr float HULL_SAT_TIE = {_f(HULL_SAT_TIE)};  // = DUCK_HULL_SAT_TIE, oracle/duck_oracle.c\n",
            ]
     out.append(_arr("gravity", m.opt_gravity, "float"))
     out.append(_arr("hull_center", hc, "float"))

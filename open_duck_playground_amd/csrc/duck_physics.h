@@ -46,7 +46,7 @@ static __device__ unsigned long long g_stage_cycles[32 + 1024];
 #define STAGE_RESET() (_c0 = clock64())
 #define STAGE_MARK(k)                                                             \
   do {                                                                            \
-    asm volatile("s_waitcnt lgkmcnt(0) vmcnt(0)" ::: "memory");                   \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                            \
     const unsigned long long _c1 = clock64();                                     \
     if (threadIdx.x == 0) atomicAdd(&g_stage_cycles[k], _c1 - _c0);               \
     _c0 = _c1;                                                                    \

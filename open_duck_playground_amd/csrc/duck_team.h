@@ -1256,7 +1256,12 @@ struct TPhys {
       for (int q = 0; q < 3; q++) V2[k][q] = p2[q] + t[q];
     }
     const int(*HE)[2] = Md::hull_edge_d();
+    const int(*HEF)[2] = Md::hull_edge_face_d();
     const float(*HN)[3] = Md::hull_face_normal_d();
+    // world face normals: hull 1 as is, hull 2 negated (the Gauss map of -B, whose faces are
+    // also the face axes of side 1)
+    constexpr int FA = EB + 3 * NE, FB = FA + 3 * NF;
+    static_assert(FB + 3 * NF <= Ly::CR, "face-normal scratch must fit in the H / row storage");
     for (int e = lane; e < NE; e += TEAM) {
       const int a0 = HE[e][0], a1 = HE[e][1];
       float d[3];
@@ -1265,6 +1270,12 @@ struct TPhys {
       for (int q = 0; q < 3; q++) L[EA + 3 * e + q] = t[q];
       mulmv3(t, R2, d);
       for (int q = 0; q < 3; q++) L[EB + 3 * e + q] = t[q];
+    }
+    for (int f = lane; f < NF; f += TEAM) {
+      mulmv3(t, R1, HN[f]);
+      for (int q = 0; q < 3; q++) L[FA + 3 * f + q] = t[q];
+      mulmv3(t, R2, HN[f]);
+      for (int q = 0; q < 3; q++) L[FB + 3 * f + q] = -t[q];
     }
     TSYNC();
     auto sep_of = [&](const float* u) {
@@ -1277,44 +1288,86 @@ struct TPhys {
       return mn2 - mx1;
     };
     constexpr int NONE = 1 << 20;
-    // face axes a = side * NF + f
-    float bsep = -1e30f, bu[3] = {0.0f, 0.0f, 1.0f};
-    int bidx = NONE;
-    float anysep = 0.0f;
-    for (int a = lane; a < 2 * NF; a += TEAM) {
-      const int side = a / NF, f = a - side * NF;
-      float u[3];
-      mulmv3(u, side == 0 ? R1 : R2, HN[f]);
-      if (side == 1) { u[0] = -u[0]; u[1] = -u[1]; u[2] = -u[2]; }
-      const float sp = sep_of(u);
-      anysep += sp > 0.0f ? 1.0f : 0.0f;
-      if (sp > bsep) { bsep = sp; bidx = a; bu[0] = u[0]; bu[1] = u[1]; bu[2] = u[2]; }
+    // Near-equal axes (parallel faces of the two feet, an edge axis equal to a face normal)
+    // differ only by rounding, so the choice among them is made with a tolerance both the fp32
+    // kernel and the fp64 oracle resolve the same way: the lowest-index face within TIE of the
+    // best face, and an edge pair only when it beats that face by more than TIE.
+    constexpr float TIE = Md::HULL_SAT_TIE;
+    // face axes a = side * NF + f (u = FA[f] or FB[f]), NFL per lane kept in registers
+    constexpr int NFL = (2 * NF + TEAM - 1) / TEAM;
+    float fs[NFL], fmx = -1e30f, anysep = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NFL; k++) {
+      const int a = lane + TEAM * k;
+      fs[k] = -1e30f;
+      if (a < 2 * NF) {
+        const int o = a < NF ? FA + 3 * a : FB + 3 * (a - NF);
+        const float u[3] = {L[o], L[o + 1], L[o + 2]};
+        const float sp = sep_of(u);
+        anysep += sp > 0.0f ? 1.0f : 0.0f;
+        fs[k] = sp;
+      }
+      fmx = fmaxf(fmx, fs[k]);
     }
     if (tsum(anysep) > 0.0f) return;
-    float best = tmaxf(bsep);
-    const int fbest = tmini(bsep == best ? bidx : NONE);
+    const float ftop = tmaxf(fmx);
+    int mine = NONE;
+#pragma unroll
+    for (int k = NFL - 1; k >= 0; k--)
+      if (fs[k] >= ftop - TIE) mine = lane + TEAM * k;
+    const int fbest = tmini(mine);
+    float myf = fs[0];
+#pragma unroll
+    for (int k = 1; k < NFL; k++) myf = fbest / TEAM == k ? fs[k] : myf;
+    float best = __shfl(myf, fbest % TEAM, TEAM);
     int btype = fbest / NF, bi = fbest - btype * NF, bj = 0;
     float u_best[3];
-    for (int q = 0; q < 3; q++) u_best[q] = __shfl(bu[q], fbest % TEAM, TEAM);
-    // edge-pair axes q = e1 * NE + e2, 16 per round; any separation ends the test
+    {
+      const int o = btype == 0 ? FA + 3 * bi : FB + 3 * bi;
+      for (int q = 0; q < 3; q++) u_best[q] = L[o + q];
+    }
+    // edge-pair axes q = e1 * NE + e2 (lane: e2 = lane + 16 k), only pairs whose Gauss-map arcs
+    // cross (a face of the Minkowski difference; the others are never the deepest axis but can
+    // tie with it and would place the contact at a clamped segment end); any separation ends
+    // the test
+    constexpr int NEL = (NE + TEAM - 1) / TEAM;
+    float EBr[NEL][3], Cr[NEL][3], Dr[NEL][3], DxC[NEL][3];
+#pragma unroll
+    for (int k = 0; k < NEL; k++) {
+      const int e2 = lane + TEAM * k, e2c = e2 < NE ? e2 : 0;
+      const int fc = HEF[e2c][0], fd = HEF[e2c][1];
+      for (int q = 0; q < 3; q++) {
+        EBr[k][q] = L[EB + 3 * e2c + q];
+        Cr[k][q] = L[FB + 3 * fc + q];
+        Dr[k][q] = L[FB + 3 * fd + q];
+      }
+      cross3(DxC[k], Dr[k], Cr[k]);
+    }
     float esep = -1e30f, eu[3] = {0.0f, 0.0f, 1.0f};
     int eidx = NONE;
-    for (int base = 0; base < NE * NE; base += TEAM) {
-      const int q = base + lane;
+    for (int e1 = 0; e1 < NE; e1++) {
+      const float ea[3] = {L[EA + 3 * e1], L[EA + 3 * e1 + 1], L[EA + 3 * e1 + 2]};
+      const int fa = HEF[e1][0], fb = HEF[e1][1];
+      const float A[3] = {L[FA + 3 * fa], L[FA + 3 * fa + 1], L[FA + 3 * fa + 2]};
+      const float B[3] = {L[FA + 3 * fb], L[FA + 3 * fb + 1], L[FA + 3 * fb + 2]};
+      float BxA[3];
+      cross3(BxA, B, A);
       float sepq = 0.0f;
-      if (q < NE * NE) {
-        const int e1 = q / NE, e2 = q - e1 * NE;
-        const float ea[3] = {L[EA + 3 * e1], L[EA + 3 * e1 + 1], L[EA + 3 * e1 + 2]};
-        const float eb[3] = {L[EB + 3 * e2], L[EB + 3 * e2 + 1], L[EB + 3 * e2 + 2]};
-        float u[3];
-        cross3(u, ea, eb);
-        const float un = sqrtf(dot3(u, u));
-        if (!(un < 1e-6f * sqrtf(dot3(ea, ea)) * sqrtf(dot3(eb, eb)))) {
-          u[0] /= un; u[1] /= un; u[2] /= un;
-          if (dot3(u, cc) < 0.0f) { u[0] = -u[0]; u[1] = -u[1]; u[2] = -u[2]; }
-          const float sp = sep_of(u);
-          sepq = sp > 0.0f ? 1.0f : 0.0f;
-          if (sp > esep) { esep = sp; eidx = q; eu[0] = u[0]; eu[1] = u[1]; eu[2] = u[2]; }
+#pragma unroll
+      for (int k = 0; k < NEL; k++) {
+        const int e2 = lane + TEAM * k;
+        const float CBA = dot3(Cr[k], BxA), DBA = dot3(Dr[k], BxA), ADC = dot3(A, DxC[k]), BDC = dot3(B, DxC[k]);
+        if (e2 < NE && CBA * DBA < 0.0f && ADC * BDC < 0.0f && CBA * BDC > 0.0f) {
+          float u[3];
+          cross3(u, ea, EBr[k]);
+          const float un = sqrtf(dot3(u, u));
+          if (!(un < 1e-6f * sqrtf(dot3(ea, ea)) * sqrtf(dot3(EBr[k], EBr[k])))) {
+            u[0] /= un; u[1] /= un; u[2] /= un;
+            if (dot3(u, cc) < 0.0f) { u[0] = -u[0]; u[1] = -u[1]; u[2] = -u[2]; }
+            const float sp = sep_of(u);
+            sepq += sp > 0.0f ? 1.0f : 0.0f;
+            if (sp > esep) { esep = sp; eidx = e1 * NE + e2; eu[0] = u[0]; eu[1] = u[1]; eu[2] = u[2]; }
+          }
         }
       }
       if (tsum(sepq) > 0.0f) return;
@@ -1322,8 +1375,8 @@ struct TPhys {
     const float em = tmaxf(esep);
     const int ebest = tmini(esep == em ? eidx : NONE);
     float u_edge[3];
-    for (int q = 0; q < 3; q++) u_edge[q] = __shfl(eu[q], ebest % TEAM, TEAM);
-    if (ebest < NONE && em > best + 1e-9f) {
+    for (int q = 0; q < 3; q++) u_edge[q] = __shfl(eu[q], (ebest % NE) % TEAM, TEAM);  // lane of e2
+    if (ebest < NONE && em > best + TIE) {
       best = em;
       btype = 2;
       bi = ebest / NE;
@@ -1388,6 +1441,24 @@ struct TPhys {
     }
   }
 
+  // out of line (frames recomputed) so the rare hull/hull SAT does not share the hot path's
+  // code layout and registers
+  static DNI void collide_hulls_rare(LP L, int lane) {
+    constexpr int p = Md::FOOT_PAIR < 0 ? 0 : Md::FOOT_PAIR;
+    const int s1 = cgeom_slot<Md>(Md::pair_geom1[p]), s2 = cgeom_slot<Md>(Md::pair_geom2[p]);
+    S1 Ls{L};
+    float p1[3], R1[9], p2[3], R2[9], t[3], c1[3], c2[3];
+    P1::geom_frame(Ls, s1, p1, R1);
+    P1::geom_frame(Ls, s2, p2, R2);
+    const float hc[3] = {Md::hull_center[0], Md::hull_center[1], Md::hull_center[2]};
+    mulmv3(t, R1, hc);
+    for (int a = 0; a < 3; a++) c1[a] = p1[a] + t[a];
+    mulmv3(t, R2, hc);
+    for (int a = 0; a < 3; a++) c2[a] = p2[a] + t[a];
+    const float cc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+    collide_hulls_team(L, lane, 4 * p, p1, R1, p2, R2, cc);
+  }
+
   static DK void collision(LP L, int lane, const float* hf) {
     STAGE_T0();
     collide_planes(L, lane, hf);
@@ -1418,7 +1489,7 @@ struct TPhys {
 #ifdef DUCK_STAGE_PROF
         if (lane == 0) atomicAdd(&g_stage_cycles[27], 1ull);  // how often the SAT path runs
 #endif
-        collide_hulls_team(L, lane, 4 * p, p1, R1, p2, R2, cc);  // rare: the boxes overlap
+        collide_hulls_rare(L, lane);  // rare: the boxes overlap
       }
     }
     TSYNC();

@@ -20,6 +20,7 @@
 #define MAXIMP 0.9999
 #define MAXEFC 128
 #define NV DUCK_MAXV
+#define DUCK_HULL_SAT_TIE 1e-5 /* m; = codegen.HULL_SAT_TIE */
 
 struct oracle_model {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
@@ -46,6 +47,7 @@ struct oracle_model {
   int hull_nvert, hull_nface, hull_nedge;
   double hull_vert[DUCK_MAXHULLV][3], hull_face_normal[DUCK_MAXHULLF][3], hull_face_offset[DUCK_MAXHULLF];
   int hull_edge[DUCK_MAXHULLE][2];
+  int hull_edge_face[DUCK_MAXHULLE][2]; /* the two faces whose planes hold the edge */
   double hull_center[3], hull_radius;
   int hfield_nrow, hfield_ncol;
   double hfield_size[4];
@@ -130,6 +132,23 @@ oracle_model* oracle_model_create(const duck_model_desc* s) {
     m->hull_face_offset[f] = s->hull_face_offset[f];
   }
   for (int e = 0; e < s->hull_nedge; e++) { m->hull_edge[e][0] = s->hull_edge[2 * e]; m->hull_edge[e][1] = s->hull_edge[2 * e + 1]; }
+  /* edge -> adjacent faces: both endpoints on the face plane (vertices of other faces are
+   * >= 2.7e-6 m off it for the Open Duck foot hull; codegen.hull_edge_faces builds the same
+   * table from the polygons) */
+  for (int e = 0; e < s->hull_nedge; e++) {
+    int n = 0;
+    for (int f = 0; f < s->hull_nface && n <= 2; f++) {
+      const double *fnm = m->hull_face_normal[f], *va = m->hull_vert[m->hull_edge[e][0]],
+                   *vb = m->hull_vert[m->hull_edge[e][1]];
+      double da = fnm[0] * va[0] + fnm[1] * va[1] + fnm[2] * va[2] - m->hull_face_offset[f];
+      double db = fnm[0] * vb[0] + fnm[1] * vb[1] + fnm[2] * vb[2] - m->hull_face_offset[f];
+      if (fabs(da) < 1e-7 && fabs(db) < 1e-7) {
+        if (n < 2) m->hull_edge_face[e][n] = f;
+        n++;
+      }
+    }
+    if (n != 2) { free(m); return NULL; }
+  }
   m->hfield_nrow = s->hfield_nrow; m->hfield_ncol = s->hfield_ncol; CP(m->hfield_size, s->hfield_size, 4);
   if (s->hfield_nrow > 0) {
     m->hfield_data = (double*)malloc(sizeof(double) * (size_t)s->hfield_nrow * s->hfield_ncol);
@@ -702,31 +721,50 @@ static void collide_convex_convex(const oracle_model* m, oracle_data* d, int g1,
     mulmv3(t, R2, m->hull_vert[k]);
     for (int a = 0; a < 3; a++) V2[k][a] = p2[a] + t[a];
   }
-  /* best axis: max separation; type 0 = face of 1, 1 = face of 2, 2 = edge pair */
-  double best = -1e30, bu[3] = {0, 0, 1};
-  int btype = -1, bi = -1, bj = -1;
-  for (int side = 0; side < 2; side++) {
-    const double* R = side == 0 ? R1 : R2;
-    for (int f = 0; f < m->hull_nface; f++) {
-      double u[3];
-      mulmv3(u, R, m->hull_face_normal[f]);
-      if (side == 1) { u[0] = -u[0]; u[1] = -u[1]; u[2] = -u[2]; }
-      double mx1 = -1e30, mn2 = 1e30;
-      for (int k = 0; k < nv; k++) {
-        double a1 = dot3(u, V1[k]), a2 = dot3(u, V2[k]);
-        if (a1 > mx1) mx1 = a1;
-        if (a2 < mn2) mn2 = a2;
-      }
-      double sep = mn2 - mx1;
-      if (sep > 0) return;
-      if (sep > best) { best = sep; memcpy(bu, u, sizeof(u)); btype = side; bi = f; }
+  /* best axis: max separation; type 0 = face of 1, 1 = face of 2, 2 = edge pair. Near-equal
+   * axes (parallel faces of the two feet, an edge axis equal to a face normal) differ only by
+   * rounding, so the choice among them uses a tolerance the fp32 kernel resolves the same way:
+   * the lowest-index face within DUCK_HULL_SAT_TIE of the best face; an edge pair only when it
+   * beats that face by more than the tolerance (codegen.HULL_SAT_TIE, TPhys::collide_hulls_team). */
+  const int nf = m->hull_nface;
+  double FN[2 * DUCK_MAXHULLF][3], fsep[2 * DUCK_MAXHULLF], ftop = -1e30;
+  for (int a = 0; a < 2 * nf; a++) {
+    const int side = a / nf, f = a - side * nf;
+    mulmv3(FN[a], side == 0 ? R1 : R2, m->hull_face_normal[f]);
+    if (side == 1) { FN[a][0] = -FN[a][0]; FN[a][1] = -FN[a][1]; FN[a][2] = -FN[a][2]; }
+    double mx1 = -1e30, mn2 = 1e30;
+    for (int k = 0; k < nv; k++) {
+      double a1 = dot3(FN[a], V1[k]), a2 = dot3(FN[a], V2[k]);
+      if (a1 > mx1) mx1 = a1;
+      if (a2 < mn2) mn2 = a2;
     }
+    fsep[a] = mn2 - mx1;
+    if (fsep[a] > 0) return;
+    if (fsep[a] > ftop) ftop = fsep[a];
   }
+  int fbest = 0;
+  while (fsep[fbest] < ftop - DUCK_HULL_SAT_TIE) fbest++;
+  double best = fsep[fbest], bu[3];
+  memcpy(bu, FN[fbest], sizeof(bu));
+  int btype = fbest / nf, bi = fbest - btype * nf, bj = -1;
+  /* edge pairs: only those whose Gauss-map arcs cross (arc of edge e1 between its two face
+   * normals on hull 1, arc of e2 on -hull 2: a face of the Minkowski difference; Gregorius,
+   * "The Separating Axis Test between Convex Polyhedra", GDC 2013). The others are never the
+   * deepest axis but can tie with it, and their closest points clamp to a segment end. */
+  double emax = -1e30, eu[3] = {0, 0, 1};
+  int ei = -1, ej = -1;
   for (int e1 = 0; e1 < m->hull_nedge; e1++) {
-    double ea[3], eb[3], tmp[3];
+    double ea[3], eb[3], tmp[3], BxA[3];
     for (int a = 0; a < 3; a++) tmp[a] = m->hull_vert[m->hull_edge[e1][1]][a] - m->hull_vert[m->hull_edge[e1][0]][a];
     mulmv3(ea, R1, tmp);
+    const double *A = FN[m->hull_edge_face[e1][0]], *B = FN[m->hull_edge_face[e1][1]];
+    cross3(BxA, B, A);
     for (int e2 = 0; e2 < m->hull_nedge; e2++) {
+      const double *C = FN[nf + m->hull_edge_face[e2][0]], *D = FN[nf + m->hull_edge_face[e2][1]];
+      double DxC[3];
+      cross3(DxC, D, C);
+      const double CBA = dot3(C, BxA), DBA = dot3(D, BxA), ADC = dot3(A, DxC), BDC = dot3(B, DxC);
+      if (!(CBA * DBA < 0 && ADC * BDC < 0 && CBA * BDC > 0)) continue;
       for (int a = 0; a < 3; a++) tmp[a] = m->hull_vert[m->hull_edge[e2][1]][a] - m->hull_vert[m->hull_edge[e2][0]][a];
       mulmv3(eb, R2, tmp);
       double u[3];
@@ -743,9 +781,10 @@ static void collide_convex_convex(const oracle_model* m, oracle_data* d, int g1,
       }
       double sep = mn2 - mx1;
       if (sep > 0) return;
-      if (sep > best + 1e-9) { best = sep; memcpy(bu, u, sizeof(u)); btype = 2; bi = e1; bj = e2; }
+      if (sep > emax) { emax = sep; memcpy(eu, u, sizeof(u)); ei = e1; ej = e2; }
     }
   }
+  if (ei >= 0 && emax > best + DUCK_HULL_SAT_TIE) { best = emax; memcpy(bu, eu, sizeof(bu)); btype = 2; bi = ei; bj = ej; }
   double fr[9];
   make_frame(fr, bu);
   if (btype == 2) {

@@ -144,7 +144,8 @@ def test_flight_obeys_newton_euler(task, gpu):
 def test_foot_foot_contacts_match_oracle(gpu):
     """Foot/foot (hull/hull) contacts at 4096 robots in flight (flight_states seed 7: feet touch
     in a few dozen): the HIP path (bounding sphere, then box/box SAT prefilter, then the hull SAT)
-    reports the same active contacts as the oracle's full hull SAT."""
+    reports the same active contacts as the oracle's hull SAT, at the same point, and the dense
+    Newton direction those rows need gives the oracle's qacc."""
     from tests.physics_laws import flight_states
     n = 4096
     env = Joystick("flat_terrain", num_envs=1, device=gpu, use_imitation=False)
@@ -155,17 +156,26 @@ def test_foot_foot_contacts_match_oracle(gpu):
     aux = torch.zeros(env.aux_size() * n, dtype=torch.float32, device=gpu).view(-1, n)
     env.physics_step(tq, tv, tw, tc, 0, aux)
     torch.cuda.synchronize()
-    g = parse_aux(m, aux.cpu().numpy().astype(np.float64))["con_dist"][:, :4]
+    ga = parse_aux(m, aux.cpu().numpy().astype(np.float64))
+    g = ga["con_dist"][:, :4]
     om = OracleModel(m)
     q32 = qpos.astype(np.float32).astype(np.float64)
-    r = []
+    r, rq, rp = [], [], []
     for e in range(n):
         d = om.new_data(qpos=q32[e], qvel=qvel[e], ctrl=ctrl[e])
         om.forward(d)
         r.append(d.arr("con_dist", 4 * m.npair)[:4].copy())
-    r = np.array(r)
+        rq.append(d.arr("qacc", m.nv).copy())
+        rp.append(np.array(d.arr("con_pos", 4 * m.npair)[0]))
+    r, rq, rp = np.array(r), np.array(rq), np.array(rp)
     act_r, act_g = (r < 0).any(axis=1), (g < 0).any(axis=1)
     assert act_r.sum() >= 10
     assert (act_r == act_g).mean() > 0.999, (act_r.sum(), act_g.sum())
     both = act_r & act_g
     np.testing.assert_allclose(np.where(r[both] < 0, r[both], 0), np.where(g[both] < 0, g[both], 0), atol=1e-5)
+    # the Newton step with the foot/foot rows active (dense H: the pair's rows couple the legs);
+    # same contact axis and point as the oracle (tie-tolerant SAT, Minkowski-face edge pairs)
+    rel = np.abs(ga["qacc"] - rq).max(axis=1) / (1 + np.abs(rq).max(axis=1))
+    np.testing.assert_allclose(ga["con_pos"][both, :3], rp[both], atol=2e-5)
+    assert rel[both].max() < 1e-3, np.sort(rel[both])[-5:]
+    assert np.median(rel[~both]) < 1e-5
