@@ -36,7 +36,7 @@ class DuckLayout(C.Structure):
         "rng_key", "rng_ctr", "step", "push_step", "push_interval", "imitation_i", "ep_steps", "nint")]
 
 
-def build(verbose: bool = False, defines=(), out: str = None) -> str:
+def build(verbose: bool = False, defines=(), out: str = None, extra_flags=()) -> str:
     """Compile libduck.so for gfx950 with hipcc (in-tree, so it travels with the repo).
 
     One translation unit per model variant (variant_*.hip) plus the C ABI (duck_capi.hip),
@@ -46,7 +46,7 @@ def build(verbose: bool = False, defines=(), out: str = None) -> str:
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
         [os.path.join(CSRC, "generated", f) for f in os.listdir(os.path.join(CSRC, "generated"))] + \
         [os.path.join(ROOT, "include", f) for f in ("duck.h", "duck_env.h", "duck_model.h")]
-    if not defines and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
+    if not defines and not extra_flags and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
     import tempfile
     # fp32 division and sqrt as v_rcp/v_sqrt (1-2 ulp) instead of the correctly rounded
@@ -54,12 +54,18 @@ def build(verbose: bool = False, defines=(), out: str = None) -> str:
     # denormals flushed (no frexp/ldexp range scaling around v_rcp/v_sqrt/sincos)
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-hip-fp32-correctly-rounded-divide-sqrt",
              "-fgpu-flush-denormals-to-zero", "-fno-slp-vectorize"] + \
-        [f"-D{d}" for d in defines]
+        [f"-D{d}" for d in defines] + list(extra_flags)
+    # the machine scheduler's max-ILP strategy: the step kernel runs one wave per SIMD, so
+    # occupancy-driven scheduling buys nothing and latency hiding must come from the wave's own
+    # instruction stream (same-box A/B: +3 % env-steps/s). Not for the rough + backlash scene:
+    # its substep parity fails under that schedule (open issue).
+    ilp = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+    no_ilp = ("variant_rough_backlash.hip",)
     with tempfile.TemporaryDirectory() as tmp:
         objs, procs = [], []
         for src in srcs:
             obj = os.path.join(tmp, os.path.basename(src) + ".o")
-            cmd = ["hipcc"] + flags + ["-c", "-o", obj, src]
+            cmd = ["hipcc"] + flags + ([] if os.path.basename(src) in no_ilp else ilp) + ["-c", "-o", obj, src]
             if verbose:
                 print(" ".join(cmd))
             procs.append((src, subprocess.Popen(cmd, cwd=CSRC)))
