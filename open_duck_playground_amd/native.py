@@ -57,8 +57,9 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=()) ->
         [f"-D{d}" for d in defines] + list(extra_flags)
     # the machine scheduler's max-ILP strategy: the step kernel runs one wave per SIMD, so
     # occupancy-driven scheduling buys nothing and latency hiding must come from the wave's own
-    # instruction stream (same-box A/B: +3 % env-steps/s). Not for the rough + backlash scene:
-    # its substep parity fails under that schedule (open issue).
+    # instruction stream (same-box A/B: +3 % env-steps/s). Not for the rough + backlash unit: its
+    # test-harness physics_kernel (512 VGPRs + 80 spilled) computes a wrong Newton step under that
+    # schedule while its step_kernel passes env parity (open issue).
     ilp = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
     no_ilp = ("variant_rough_backlash.hip",)
     with tempfile.TemporaryDirectory() as tmp:
