@@ -586,7 +586,10 @@ struct Phys {
   }
 
   // convex vs convex (foot/foot): SAT over face normals and edge pairs, then a 4-point
-  // manifold against the reference face or one edge-edge point (oracle collide_convex_convex)
+  // manifold against the reference face or one edge-edge point (oracle collide_convex_convex).
+  // Single-lane debug build (-DDUCK_TEAM=0) only: it tests every edge pair and keeps the exact
+  // maximum, without the Minkowski-face filter and tie tolerance of TPhys::collide_hulls_team and
+  // the oracle, so near-tied axes may resolve differently there.
   static DNI void collide_hulls(S L, int s1, int s2, int slot0) {
     constexpr int NH = Md::NHV;
     const float nofr[9] = {0, 0, 1, 0, 1, 0, -1, 0, 0};
