@@ -140,17 +140,24 @@ def main():
     for i in range(args.warmup):
         env.step(state, pool[i % len(pool)])
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    # launch durations from HIP events on every 8th timed launch: bracketing every launch puts two
+    # event records between back-to-back kernels and cost 2.3 % of the wall time (same box, 400
+    # steps: 0.2815 vs 0.2753 ms per step) without changing the measured launch duration
+    EV_EVERY = int(os.environ.get("DUCK_EV_EVERY", "8"))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if i % EV_EVERY == 0 else None
+          for i in range(K)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(K):
-        s, e = ev[i]
-        s.record()
-        env.step(state, pool[i % len(pool)])
-        e.record()
+        if ev[i] is not None:
+            ev[i][0].record()
+            env.step(state, pool[i % len(pool)])
+            ev[i][1].record()
+        else:
+            env.step(state, pool[i % len(pool)])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -159,7 +166,7 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern_ms = float(np.mean([p[0].elapsed_time(p[1]) for p in ev if p is not None]))
     ok = bool(torch.isfinite(state.obs["state"]).all().item())
 
     cpu = None
