@@ -81,6 +81,12 @@ DK int tmini(int v) {
   return v;
 }
 // reductions over the 8-lane halves of a team
+DK float hsum8(float v) {
+  v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dppf<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dppf<0x141>(v);  // row_half_mirror
+  return v;
+}
 DK float hmax8(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));
@@ -889,32 +895,52 @@ struct TPhys {
       for (int r = 0; r < NV; r++) F.col[s][r] = r >= TEAM * s ? Mc[s][r] + (r == c ? diag : 0.0f) : 0.0f;
     }
     STAGE_MARK(16);
-    // contact rows of each floor pair: per-foot 6x6 J'DJ block and J'force, by team sums
+    // contact rows of each floor pair: per-foot 6x6 J'DJ block and J'force. Lanes 0-7 take the
+    // 16 rows of side 0's pair, lanes 8-15 side 1's (two rows per lane), each half sums its
+    // 27 values over 8 lanes; each side's sums are then broadcast from lane 0 or 8
+    float Kh[21], Fh[6];
+    {
+      const int hs = lane >> 3, l8 = lane & 7;
+      const int p = hs == 0 ? Md::PLANE_PAIR[0] : Md::PLANE_PAIR[1];
+      const float mu = tf(Md::B_PAIR + PAIRW * p + 2);
+#pragma unroll
+      for (int k = 0; k < 21; k++) Kh[k] = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 6; k++) Fh[k] = 0.0f;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; h2++) {
+        const int j = l8 + 8 * h2, slot = 4 * p + (j >> 2), e = j & 3, row = R_CON + 4 * slot + e;
+        const float D = L[Ly::RD + row], x = L[Ly::JA + row];
+        const float w = (x < 0.0f && D != 0.0f) ? D : 0.0f;
+        const float force = -w * x;
+        const int t = 1 + (e >> 1);
+        const float sg = (e & 1) ? -mu : mu;
+        float u[3], r3[3], a[6];
+        for (int q = 0; q < 3; q++) {
+          u[q] = L[Ly::CFR + 9 * slot + q] + sg * L[Ly::CFR + 9 * slot + 3 * t + q];
+          r3[q] = L[Ly::CR + 3 * slot + q];
+        }
+        cross3(a, r3, u);
+        a[3] = u[0]; a[4] = u[1]; a[5] = u[2];
+        int o = 0;
+        for (int q = 0; q < 6; q++)
+          for (int kk = q; kk < 6; kk++) { Kh[o] += w * a[q] * a[kk]; o++; }
+        for (int q = 0; q < 6; q++) Fh[q] += force * a[q];
+      }
+#pragma unroll
+      for (int k = 0; k < 21; k++) Kh[k] = hsum8(Kh[k]);
+#pragma unroll
+      for (int k = 0; k < 6; k++) Fh[k] = hsum8(Fh[k]);
+    }
 #pragma unroll
     for (int side = 0; side < 2; side++) {
       const int p = Md::PLANE_PAIR[side];
       const int foot = cgeom_slot<Md>(Md::pair_geom2[p]);  // 1 left, 2 right
-      const float mu = tf(Md::B_PAIR + PAIRW * p + 2);
-      const int slot = 4 * p + (lane >> 2), e = lane & 3, row = R_CON + 4 * slot + e;
-      const float D = L[Ly::RD + row], x = L[Ly::JA + row];
-      const float w = (x < 0.0f && D != 0.0f) ? D : 0.0f;
-      const float force = -w * x;
-      const int t = 1 + (e >> 1);
-      const float sg = (e & 1) ? -mu : mu;
-      float u[3], r3[3], a[6];
-      for (int q = 0; q < 3; q++) {
-        u[q] = L[Ly::CFR + 9 * slot + q] + sg * L[Ly::CFR + 9 * slot + 3 * t + q];
-        r3[q] = L[Ly::CR + 3 * slot + q];
-      }
-      cross3(a, r3, u);
-      a[3] = u[0]; a[4] = u[1]; a[5] = u[2];
       float K[21], Fv[6];
-      {
-        int o = 0;
-        for (int q = 0; q < 6; q++)
-          for (int kk = q; kk < 6; kk++) { K[o] = tsum(w * a[q] * a[kk]); o++; }
-        for (int q = 0; q < 6; q++) Fv[q] = tsum(force * a[q]);
-      }
+#pragma unroll
+      for (int k = 0; k < 21; k++) K[k] = side == 0 ? bc<0>(Kh[k]) : bc<8>(Kh[k]);
+#pragma unroll
+      for (int k = 0; k < 6; k++) Fv[k] = side == 0 ? bc<0>(Fh[k]) : bc<8>(Fh[k]);
       constexpr unsigned MASKL = chain_mask(Md::LFOOT_BODY), MASKR = chain_mask(Md::RFOOT_BODY);
       const unsigned msk = foot == 1 ? MASKL : MASKR;
 #pragma unroll
