@@ -512,6 +512,7 @@ static void rne_bias(const oracle_model* m, oracle_data* d, const fwd_ws* w) {
 
 /* argmax with a tie band: first index whose value is within tol of the maximum */
 static int argmax_tol(const double* v, int n, double tol) {
+  if (n <= 0) return 0;
   double mx = v[0];
   for (int i = 1; i < n; i++)
     if (v[i] > mx) mx = v[i];
@@ -523,7 +524,7 @@ static int argmax_tol(const double* v, int n, double tol) {
 
 /* mjx collision_convex._manifold_points: 4 points of approximately maximal area */
 static void manifold_points(const double (*poly)[3], const int* mask, int n, const double* nrm, int idx[4]) {
-  double dm[DUCK_MAXHULLV], s[2 * DUCK_MAXHULLV];
+  double dm[DUCK_MAXHULLV] = {0}, s[2 * DUCK_MAXHULLV];
   for (int k = 0; k < n; k++) dm[k] = mask[k] ? 0.0 : -1e6;
   int a = argmax_tol(dm, n, 0.0);
   for (int k = 0; k < n; k++) {
