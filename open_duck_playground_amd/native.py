@@ -51,9 +51,12 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=()) ->
     import tempfile
     # fp32 division and sqrt as v_rcp/v_sqrt (1-2 ulp) instead of the correctly rounded
     # multi-instruction sequences: the physics tolerances are fp32-vs-fp64 anyway; fp32
-    # denormals flushed (no frexp/ldexp range scaling around v_rcp/v_sqrt/sincos)
+    # denormals flushed (no frexp/ldexp range scaling around v_rcp/v_sqrt/sincos); x/y as
+    # x*rcp(y) and signed zeros ignored (+0.8 % same-box, parity unchanged) -- NaN/Inf stay
+    # honoured: the termination check and the auto-reset NaN guard depend on them
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-hip-fp32-correctly-rounded-divide-sqrt",
-             "-fgpu-flush-denormals-to-zero", "-fno-slp-vectorize"] + \
+             "-fgpu-flush-denormals-to-zero", "-fno-slp-vectorize",
+             "-fno-signed-zeros", "-fno-trapping-math", "-fno-math-errno", "-freciprocal-math"] + \
         [f"-D{d}" for d in defines] + list(extra_flags)
     # the machine scheduler's max-ILP strategy: the step kernel runs one wave per SIMD, so
     # occupancy-driven scheduling buys nothing and latency hiding must come from the wave's own
