@@ -214,6 +214,7 @@ struct TPhys {
   }
 
   static DK void kinematics(LP L, int lane) {
+#pragma clang fp reassociate(on)
     STAGE_T0();
     // K1: local transform (body quat x joint rotations, body pos) of every moving body, a
     // body per lane, off the serial chain
@@ -289,6 +290,7 @@ struct TPhys {
 
   // ---------------- mj_comPos: subtree com (team reduction), cinert, cdof ----------------
   static DK void com_pos(LP L, int lane) {
+#pragma clang fp reassociate(on)
     float ms = 0.0f, cx = 0.0f, cy = 0.0f, cz = 0.0f;
     for (int b = 1 + lane; b < NB; b += TEAM) {
       if (!moving(b)) continue;
@@ -398,6 +400,7 @@ struct TPhys {
   }
 
   static DK void rne(LP L, int lane) {
+#pragma clang fp reassociate(on)
     STAGE_T0();
     constexpr int NR = Md::T_NROOT, BL = Md::T_BRLEN, MD = Md::T_BRMD;  // dofs per limb body (2: backlash)
     static_assert(Md::T_NBR <= TEAM, "a limb per lane");
@@ -509,6 +512,7 @@ struct TPhys {
 
   // ---------------- mj_crb: the sparse M from the composite inertias (summed in rne) ----
   static DK void crb(LP L, int lane) {
+#pragma clang fp reassociate(on)
     STAGE_T0();
     constexpr int BL = Md::T_BRLEN, MC = Md::MAXCHAIN;
     // (the composite inertias were summed in rne's subtree pass)
