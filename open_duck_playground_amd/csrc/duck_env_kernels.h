@@ -104,6 +104,17 @@ DK void phys_step(Slice<SW> L, int lane, bool integrate, bool want_out, float* a
 #endif
 }
 
+// the physics_kernel (mjx_env.step / mjx.forward parity entry) runs its substeps through one
+// out-of-line copy: no values hoisted across substeps, one call site for both modes, so the
+// test harness stays well inside the register file (two inlined copies plus the rare-path calls
+// needed 512 VGPRs + 86 spilled, the pressure under which the allocator misplaced split copies
+// ahead of an exec restore)
+template <class Md>
+__device__ __noinline__ void phys_step_dni(Slice<SW> L, int lane, bool integrate, bool want_out, float* aux,
+                                           int aux_stride, float* scratch, int sstride, const float* hfield) {
+  phys_step<Md>(L, lane, integrate, want_out, aux, aux_stride, scratch, sstride, hfield);
+}
+
 template <int WG>
 struct Col {  // SoA accessor for env e
   float* p;
@@ -847,11 +858,9 @@ __global__ void __launch_bounds__(TPB) physics_kernel(KArgs A, float* qpos_g, fl
   load_dyn<Md, SW>(A, e, L);
   float* ax = aux ? aux + e : nullptr;
   float* scr = A.scratch ? A.scratch + e : nullptr;
-  if (nsub == 0) {
-    phys_step<Md>(L, lane, false, true, ax, n, scr, n, A.hfield);
-  } else {
-    for (int s = 0; s < nsub; s++) phys_step<Md>(L, lane, true, s == nsub - 1, ax, n, scr, n, A.hfield);
-  }
+  // nsub = 0: one forward (mjx.forward), no integration
+  const int ns = nsub > 0 ? nsub : 1;
+  for (int s = 0; s < ns; s++) phys_step_dni<Md>(L, lane, nsub > 0, s == ns - 1, ax, n, scr, n, A.hfield);
   for (int i = 0; i < Md::NQ; i++) qpos_g[(size_t)i * n + e] = L[Ly::QPOS + i];
   for (int i = 0; i < Md::NV; i++) { qvel_g[(size_t)i * n + e] = L[Ly::QVEL + i]; warm_g[(size_t)i * n + e] = L[Ly::WARM + i]; }
 }

@@ -1255,6 +1255,10 @@ struct Phys {
     for (int s = 0; s < NCON; s++)
       for (int a = 0; a < 3; a++) aux[(o++) * stride] = L[Ly::CR + 3 * s + a] + L[Ly::COM + a];
     for (int k = 0; k < Md::NM; k++) aux[(o++) * stride] = L[Ly::M + k];
+#ifdef DUCK_AUX_LDS
+    // debug builds: the whole env slice (Lay fields + the team's chain/spatial scratch)
+    for (int k = 0; k < Ly::TOTAL + 12 * Md::MAXCHAIN + 24; k++) aux[(o++) * stride] = L[k];
+#endif
   }
 
   // ---------------- semi-implicit Euler (eulerdamp disabled) ----------------
@@ -1314,5 +1318,9 @@ struct Phys {
 
 template <class Md>
 constexpr int aux_size() {
-  return 4 * Md::NV + Md::NU + Md::NSENSORDATA + 4 * Lay<Md>::NCON + Md::NM;
+  return 4 * Md::NV + Md::NU + Md::NSENSORDATA + 4 * Lay<Md>::NCON + Md::NM
+#ifdef DUCK_AUX_LDS
+         + Lay<Md>::TOTAL + 12 * Md::MAXCHAIN + 24
+#endif
+      ;
 }

@@ -109,6 +109,11 @@ struct TLay {
   static constexpr int STRIDE = ((USED + 15) / 32) * 32 + 16;  // = 16 (mod 32), >= USED
   static_assert(STRIDE >= USED && STRIDE % 32 == 16, "stride");
   static constexpr int FTMP = Ly::JA;                  // crb: F_i = I_b cdof_i (dead row storage)
+  // per-lane dump slots for branchless conditional stores (L[ok ? addr : SINK + lane] = v): a
+  // lane-divergent `if` leaves a join block whose exec restore the register allocator may put
+  // live-range split copies in front of (tools/isa_exec_check.py), so the hot
+  // path avoids such regions where a select does the job. KC is dead storage in the fused solver.
+  static constexpr int SINK = KC;
   // scratch of the flattened tree passes: the H + constraint-row storage is dead until the
   // constraint stage (kinematics / rne / crb run before it)
   static constexpr int TMP = Ly::H;
@@ -1519,7 +1524,9 @@ struct TPhys {
 #ifdef DUCK_STAGE_PROF
         if (lane == 0) atomicAdd(&g_stage_cycles[27], 1ull);  // how often the SAT path runs
 #endif
+#ifndef DUCK_DIAG_NO_RARE_CALLS
         collide_hulls_rare(L, lane);  // rare: the boxes overlap
+#endif
       }
     }
     TSYNC();
@@ -1912,14 +1919,16 @@ struct TPhys {
     mul_cols(L, lane, Mc, Ly::WARM, Ly::MA);
     TSYNC();
     float cwp = 0.0f, csp = 0.0f, gwp = 0.0f;
-    if (lane < NFRIC) {
-      const int r = lane, i = fric_dof(r);
+    {
+      // branchless (no lane-divergent region: see TL::SINK)
+      const bool fr = lane < NFRIC;
+      const int r = fr ? lane : 0, i = fric_dof(r);
       const float D = L[Ly::RD + r], f = L[Ly::DFRIC + i], ar = L[Ly::AREF + r];
       const float jw = L[Ly::WARM + i] - ar, js = L[Ly::QSM + i] - ar;
-      cwp += fric_cost(D, jw, f);
-      csp += fric_cost(D, js, f);
-      L[Ly::JA + r] = jw;
-      L[Ly::JV + r] = js;
+      cwp += fr ? fric_cost(D, jw, f) : 0.0f;
+      csp += fr ? fric_cost(D, js, f) : 0.0f;
+      L[fr ? Ly::JA + r : TL::SINK + lane] = jw;
+      L[fr ? Ly::JV + r : TL::SINK + TEAM + lane] = js;
     }
     for (int r = lane; r < NLIM; r += TEAM) {
       const int i = lim_dof(r), row = R_LIM + r;
@@ -1972,7 +1981,9 @@ struct TPhys {
 #ifdef DUCK_STAGE_PROF
       if (lane == 0) atomicAdd(&g_stage_cycles[23], 1ull);  // dense Newton fallbacks
 #endif
+#ifndef DUCK_DIAG_NO_RARE_CALLS
       newton_dense(L, lane);  // rare: foot/foot contact rows active (dense H)
+#endif
       TSYNC();
     }
     // J.search and M.search in one pass; rows go straight to registers
@@ -2006,6 +2017,14 @@ struct TPhys {
       }
     }
     float sn = 0.0f, sMa = 0.0f, sf = 0.0f, sMv = 0.0f;
+#ifdef DUCK_LS_DUMP
+    {
+      const unsigned long long ex = __builtin_amdgcn_read_exec();
+      L[TL::KC + 88 + lane] = __int_as_float((int)(ex & 0xffffffffull));
+      L[TL::KC + 104 + lane] = __int_as_float((int)(ex >> 32));
+      L[TL::KC + 120 + lane] = L[Ly::SRCH + lane];
+    }
+#endif
     for (int i = lane; i < NV; i += TEAM) {
       const float sv = L[Ly::SRCH + i];
       sn += sv * sv;
@@ -2013,6 +2032,10 @@ struct TPhys {
       sf += sv * L[Ly::FSM + i];
       sMv += sv * L[Ly::GRAD + i];
     }
+#ifdef DUCK_LS_DUMP
+    L[TL::KC + 56 + lane] = (float)lane;
+    L[TL::KC + 72 + lane] = sn;
+#endif
     sn = tsum(sn); sMa = tsum(sMa); sf = tsum(sf); sMv = tsum(sMv);
     STAGE_MARK(12);
     const float gtol = Md::tolerance * Md::ls_tolerance * sqrtf(sn) * Md::meaninertia * (float)(NV > 1 ? NV : 1);
@@ -2030,6 +2053,11 @@ struct TPhys {
     {
       float q0 = 0, q1 = 0, q2 = 0;
       quad2(R, 0.0f, q0, q1, q2);
+#ifdef DUCK_LS_DUMP
+      // debug builds: the line search's inputs, into the (dead) KC scratch of the env slice
+      L[TL::KC + 8 + 3 * lane] = q0; L[TL::KC + 9 + 3 * lane] = q1; L[TL::KC + 10 + 3 * lane] = q2;
+      if (lane == 0) { L[TL::KC] = G0; L[TL::KC + 1] = G1; L[TL::KC + 2] = G2; L[TL::KC + 3] = gtol; L[TL::KC + 4] = sn; }
+#endif
       p0 = mk(0.0f, q0, q1, q2);
     }
     Pt lo;
@@ -2042,17 +2070,38 @@ struct TPhys {
     Pt hi;
     if (lo.d0 < p0.d0) { hi = p0; } else { hi = lo; lo = p0; }
     bool swap = true;
+#ifdef DUCK_LS_NOBREAK
+    bool stop = false;
+#pragma unroll
+    for (int it = 0; it < Md::ls_iterations; it++) {
+      bool done = stop || !swap;
+      done = done || ((lo.d0 < 0.0f) && (lo.d0 > -gtol));
+      done = done || ((hi.d0 > 0.0f) && (hi.d0 < gtol));
+      stop = done;
+#else
     for (int it = 0; it < Md::ls_iterations; it++) {
       bool done = !swap;
       done = done || ((lo.d0 < 0.0f) && (lo.d0 > -gtol));
       done = done || ((hi.d0 > 0.0f) && (hi.d0 < gtol));
       if (done) break;
+#endif
       const float al = lo.alpha - lo.d0 / lo.d1, ah = hi.alpha - hi.d0 / hi.d1, am = 0.5f * (lo.alpha + hi.alpha);
       float a0 = 0, a1 = 0, a2 = 0, b0 = 0, b1 = 0, b2 = 0, c0 = 0, c1 = 0, c2 = 0;
       quad2(R, al, a0, a1, a2);
       quad2(R, ah, b0, b1, b2);
       quad2(R, am, c0, c1, c2);
       const Pt lo_next = mk(al, a0, a1, a2), hi_next = mk(ah, b0, b1, b2), mid = mk(am, c0, c1, c2);
+#ifdef DUCK_LS_NOBREAK
+      const bool s1 = !done && ((lo.d0 > 0.0f) || (lo.d0 < lo_next.d0));
+      if (s1) lo = lo_next;
+      const bool s2 = !done && (mid.d0 < 0.0f) && (lo.d0 < mid.d0);
+      if (s2) lo = mid;
+      const bool s3 = !done && ((hi.d0 < 0.0f) || (hi.d0 > hi_next.d0));
+      if (s3) hi = hi_next;
+      const bool s4 = !done && (mid.d0 > 0.0f) && (hi.d0 > mid.d0);
+      if (s4) hi = mid;
+      swap = done ? swap : (s1 || s2 || s3 || s4);
+#else
       const bool s1 = (lo.d0 > 0.0f) || (lo.d0 < lo_next.d0);
       if (s1) lo = lo_next;
       const bool s2 = (mid.d0 < 0.0f) && (lo.d0 < mid.d0);
@@ -2062,6 +2111,7 @@ struct TPhys {
       const bool s4 = (mid.d0 > 0.0f) && (hi.d0 > mid.d0);
       if (s4) hi = mid;
       swap = s1 || s2 || s3 || s4;
+#endif
     }
     const bool improved = (lo.cost < p0.cost) || (hi.cost < p0.cost);
     const float alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;

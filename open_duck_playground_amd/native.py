@@ -36,16 +36,17 @@ class DuckLayout(C.Structure):
         "rng_key", "rng_ctr", "step", "push_step", "push_interval", "imitation_i", "ep_steps", "nint")]
 
 
-def build(verbose: bool = False, defines=(), out: str = None, extra_flags=()) -> str:
+def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no_ilp=(), isa_check: bool = True) -> str:
     """Compile libduck.so for gfx950 with hipcc (in-tree, so it travels with the repo).
 
     One translation unit per model variant (variant_*.hip) plus the C ABI (duck_capi.hip),
     compiled in parallel and linked into one shared library."""
-    out = out or LIB_PATH
+    out = os.path.abspath(out or LIB_PATH)
     srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
         [os.path.join(CSRC, "generated", f) for f in os.listdir(os.path.join(CSRC, "generated"))] + \
-        [os.path.join(ROOT, "include", f) for f in ("duck.h", "duck_env.h", "duck_model.h")]
+        [os.path.join(ROOT, "include", f) for f in ("duck.h", "duck_env.h", "duck_model.h")] + \
+        [os.path.abspath(__file__)]  # the compile flags live here
     if not defines and not extra_flags and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
     import tempfile
@@ -60,11 +61,10 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=()) ->
         [f"-D{d}" for d in defines] + list(extra_flags)
     # the machine scheduler's max-ILP strategy: the step kernel runs one wave per SIMD, so
     # occupancy-driven scheduling buys nothing and latency hiding must come from the wave's own
-    # instruction stream (same-box A/B: +3 % env-steps/s). Not for the rough + backlash unit: its
-    # test-harness physics_kernel (512 VGPRs + 80 spilled) computes a wrong Newton step under that
-    # schedule while its step_kernel passes env parity (open issue).
+    # instruction stream (same-box A/B: +3 % env-steps/s). Every unit uses it; the build is
+    # gated by tools/isa_exec_check.py, which rejects the register-allocation fault that once made
+    # the rough + backlash physics_kernel compute a wrong Newton step.
     ilp = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-    no_ilp = ("variant_rough_backlash.hip",)
     with tempfile.TemporaryDirectory() as tmp:
         objs, procs = [], []
         for src in srcs:
@@ -78,8 +78,27 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=()) ->
         if bad:
             raise DuckError(f"hipcc failed on {bad}")
         subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-shared", "-o", out + ".tmp"] + objs, cwd=CSRC)
+    if isa_check:
+        bad = isa_exec_faults(out + ".tmp")
+        if bad:
+            os.remove(out + ".tmp")
+            raise DuckError("register-allocation fault in the compiled kernels (split copies ahead of an exec "
+                            "restore, tools/isa_exec_check.py):\n" + "\n".join(bad))
     os.replace(out + ".tmp", out)
     return out
+
+
+def isa_exec_faults(so_path: str):
+    """Blocks of the gfx950 code in so_path whose exec-restoring join starts with AGPR/scratch moves
+    (tools/isa_exec_check.py): each is a lane-masked live-range split, i.e. a wrong-result kernel."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("isa_exec_check", os.path.join(ROOT, "tools", "isa_exec_check.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    found = []
+    for text in mod.code_objects(so_path):
+        found += mod.scan(text, os.path.basename(so_path))
+    return [f"{func[:80]}: {len(pre)} move(s) before '{ins}'" for _, func, _, pre, ins in found]
 
 
 _lib = None

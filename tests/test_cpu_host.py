@@ -165,3 +165,50 @@ def test_product_fails_loudly_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(native, "_lib", None)
     with pytest.raises(native.DuckError):
         native.lib()
+
+
+# --- register-allocation fault gate (tools/isa_exec_check.py) ---
+_BAD_JOIN = """
+_Z6kernelv:
+	s_and_saveexec_b64 s[0:1], s[50:51]
+	s_cbranch_execz .LBB0_2
+	v_add_f32_e32 v1, v2, v3
+.LBB0_2:
+	v_accvgpr_write_b32 a81, v107
+	s_or_b64 exec, exec, s[0:1]
+	s_endpgm
+"""
+_GOOD_JOIN = """
+_Z6kernelv:
+	s_and_saveexec_b64 s[0:1], s[50:51]
+	s_cbranch_execz .LBB0_2
+	v_mov_b32_e32 v9, v19
+.LBB0_2:
+	v_mov_b32_e32 v9, v4
+	s_or_b64 exec, exec, s[0:1]
+	v_accvgpr_write_b32 a81, v107
+	s_endpgm
+"""
+
+
+def _isa_check_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("isa_exec_check", os.path.join(ROOT, "tools", "isa_exec_check.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_isa_check_flags_lane_masked_split_copies():
+    """The checker flags an AGPR move ahead of a join's exec restore (the pattern that cost lanes
+    14-15 their LDS row address in the max-ILP physics_kernel) and accepts a region phi copy."""
+    mod = _isa_check_module()
+    assert len(mod.scan(_BAD_JOIN, "bad")) == 1
+    assert mod.scan(_GOOD_JOIN, "good") == []
+
+
+@pytest.mark.skipif(not os.path.exists(native.LIB_PATH), reason="libduck.so not built")
+def test_built_library_has_no_lane_masked_split_copies():
+    """Every kernel of the shipped libduck.so (all four scenes, max-ILP schedule) is free of
+    register moves placed ahead of an exec restore."""
+    assert native.isa_exec_faults(native.LIB_PATH) == []
