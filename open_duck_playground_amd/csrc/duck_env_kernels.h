@@ -537,7 +537,9 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   // push (joystick.py:381-400)
   const float theta = r.uniform(SLOT_PUSH_THETA, 0.0f, 2.0f * PI_F);
   const float mag = r.uniform(SLOT_PUSH_MAG, c.push_magnitude_range[0], c.push_magnitude_range[1]);
-  const float gate = ((push_step + 1) % push_interval == 0) ? 1.0f : 0.0f;
+  // jp.mod(push_step + 1, interval) == 0 (joystick.py:388-390); an interval that rounds to 0 steps
+  // never pushes (XLA integer remainder by zero returns the dividend), and never divides by zero here
+  const float gate = (push_interval != 0 && (push_step + 1) % push_interval == 0) ? 1.0f : 0.0f;
   const float push[2] = {cosf(theta) * gate * (float)c.push_enable, sinf(theta) * gate * (float)c.push_enable};
   if constexpr (STAGE_OBS) {  // team: lane-split copies, sums by DPP
     arate = tsum(arate);

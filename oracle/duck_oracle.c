@@ -1678,6 +1678,11 @@ int oracle_env_reset(const oracle_model* m, const duck_env_config* cfg, const du
   return 0;
 }
 
+/* test aid (tools/tf_outliers.py): when set, oracle_env_step on this thread records every substep's
+ * input state (qpos, qvel, qacc_warmstart, ctrl) into the buffer, n_substeps records */
+static _Thread_local double* g_trace;
+void oracle_set_trace(double* buf) { g_trace = buf; }
+
 /* Joystick.step (joystick.py:323-481) + EpisodeWrapper + BraxAutoResetWrapper when cfg->auto_reset */
 int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref, double* fs,
                     int32_t* is, const double* action, double* obs, double* priv, double* reward_out,
@@ -1713,7 +1718,8 @@ int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duc
   /* push (:381-400) */
   double theta = rng_uniform(&r, SLOT_PUSH_THETA, 0.0, 2 * PI);
   double mag = rng_uniform(&r, SLOT_PUSH_MAG, cfg->push_magnitude_range[0], cfg->push_magnitude_range[1]);
-  double gate = ((is[L.push_step] + 1) % is[L.push_interval] == 0) ? 1.0 : 0.0;
+  /* jp.mod by a zero interval returns the dividend (XLA): no push */
+  double gate = (is[L.push_interval] != 0 && (is[L.push_step] + 1) % is[L.push_interval] == 0) ? 1.0 : 0.0;
   double push[2] = {cos(theta) * gate * cfg->push_enable, sin(theta) * gate * cfg->push_enable};
   oracle_data dd, *d = d_out ? d_out : &dd;
   load_data(&L, fs, d);
@@ -1731,6 +1737,13 @@ int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duc
   }
   /* physics (:420) */
   for (int s = 0; s < cfg->n_substeps; s++) {
+    if (g_trace) { /* test aid: each substep's input state */
+      double* t = g_trace + (size_t)s * (m->nq + 2 * m->nv + nu);
+      memcpy(t, d->qpos, sizeof(double) * m->nq);
+      memcpy(t + m->nq, d->qvel, sizeof(double) * m->nv);
+      memcpy(t + m->nq + m->nv, d->qacc_warmstart, sizeof(double) * m->nv);
+      memcpy(t + m->nq + 2 * m->nv, d->ctrl, sizeof(double) * nu);
+    }
     oracle_forward(m, d);
     euler(m, d);
   }

@@ -68,6 +68,7 @@ void oracle_threefry2x32(const uint32_t key[2], const uint32_t ctr[2], uint32_t 
 /* Joystick env on one env: fstate/istate are this env's columns (stride 1). */
 int oracle_env_reset(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref,
                      uint64_t seed, int64_t env_id, double* fstate, int32_t* istate, double* obs, double* priv);
+void oracle_set_trace(double* buf); /* test aid: record substep inputs of oracle_env_step */
 int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref,
                     double* fstate, int32_t* istate, const double* action, double* obs, double* priv,
                     double* reward, double* done, oracle_data* d_out);

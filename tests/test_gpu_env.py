@@ -120,6 +120,8 @@ def test_domain_randomization_parity(task, gpu):
         env.step(st, torch.tensor(a, device=gpu))
         ob.step(a.astype(np.float64))
         good &= _compare(env, st, ob, L)
+    print(task, "free-running envs within tolerance after 3 steps:", good.mean())
+    assert good.mean() > 0.9
 
 
 def test_edge_sizes(gpu):

@@ -1,0 +1,62 @@
+"""Strict env parity: every env-step of libduck.so from the oracle's own (fp32-rounded) state.
+
+See tests/teacher_forcing.py. Each case steps 256 envs for 6 env-steps; before every step the
+oracle's state is uploaded into the GPU state, so each comparison is one Joystick.step
+(joystick.py:323-481: action delay, push, 10 substeps, obs, rewards, termination, info
+bookkeeping, and the EpisodeWrapper/AutoReset wrappers of common/runner.py:117 where on).
+
+Bar: qpos rel 1e-4, qvel 2e-3, qacc_warmstart 2e-2, every info field / obs / privileged obs / reward
+2e-3 (|gpu - oracle| / (1 + |oracle|)), done and every integer field exact, for >= 99.5 % of
+env-steps; and every env-step outside that bar is explained at substep resolution (the kernel's
+substep from its own input matches the oracle's substep from the same input to 1e-3, or is a
+branch the oracle also takes under a 1e-6/1e-5 input perturbation). Measured on MI355X: median
+errors 1e-7 (qpos) .. 4e-6 (obs), p99 <= 3e-4, at most 2 outliers in 1536 env-steps per case, all
+explained (tools/tf_outliers.py).
+"""
+
+import numpy as np
+import pytest
+
+from tests.teacher_forcing import CASES, explain, run_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_teacher_forced_step_parity(case, gpu):
+    rep = run_case(case, gpu, n=256, steps=6, keep_states=True)
+    s = rep.summary()
+    print(case, {k: v for k, v in s.items()})
+    assert s["good_frac"] >= 0.995, s
+    unexplained = []
+    for t, st in enumerate(rep.steps):
+        out = rep.outliers(st) | st.done_mismatch | st.int_mismatch
+        for e in out.nonzero()[0]:
+            x = explain(rep, t, int(e))
+            print(f"  outlier step {t} env {e}: {x['kind']} max substep err {max(x['substep_err']):.2e} "
+                  f"flips {x.get('flips')}")
+            if x["kind"] != "sensitive":
+                unexplained.append((t, int(e), x))
+    assert not unexplained, unexplained
+
+
+def test_teacher_forced_paths_are_exercised(gpu):
+    """The forced cases really run the rare env paths: pushes, the step-500 command resample and
+    the auto-reset restore (free-running parity never reached them)."""
+    from tests.teacher_forcing import run
+    rep = run("flat_terrain", False, n=64, steps=3, device=gpu, force_push=True, force_resample=True,
+              keep_states=True)
+    env = rep.env
+    L = env._layout
+    fs1 = rep.pre[1][0].reshape(L.nfloat, 64)
+    is1 = rep.pre[1][1].reshape(L.nint, 64)
+    push = fs1[L.off["push"]:L.off["push"] + 2]
+    assert (np.abs(push).sum(axis=0) > 0).sum() >= 64 // 3 - 1       # pushed envs
+    assert (is1[L.ioff["step"]] == 0).sum() >= 64 // 4               # resampled envs restart at step 0
+    assert rep.summary()["good_frac"] >= 0.995
+    rep = run("flat_terrain", False, n=64, steps=4, device=gpu, auto_reset=True, episode_length=3, keep_states=True)
+    L = rep.env._layout
+    is3 = rep.pre[3][1].reshape(L.nint, 64)
+    fs3 = rep.pre[3][0].reshape(L.nfloat, 64)
+    assert (fs3[L.off["done"]] == 1).all() and (is3[L.ioff["ep_steps"]] == 3).all()   # every env restored at 3
+    assert rep.summary()["good_frac"] >= 0.995

@@ -184,3 +184,20 @@ def test_standing_task_surface(m, om):
     np.testing.assert_allclose(b.rew, np.clip(terms.sum(0) * float(np.float32(0.02)), 0, 1e4), rtol=1e-12)
     np.testing.assert_array_equal(met[3], 20.0)  # alive
     np.testing.assert_array_equal(met[5], 0.0)   # head_pos gated off: no walking command
+
+
+def test_push_interval_rounding_to_zero_never_pushes(m, om):
+    """interval_range below ctrl_dt / 2 rounds to a 0-step interval: jp.mod(push_step + 1, 0) is the
+    dividend under XLA (joystick.py:388-390), so no push ever fires -- and nothing divides by zero."""
+    cfgd = default_config()
+    cfgd.push_config.interval_range = [0.0, 0.009]
+    n = 8
+    b = OracleBatch(om, env_config_struct(m, cfgd, False), n)
+    b.reset(seed=4)
+    L = b.L
+    I = b.is_.reshape(L.nint, n)
+    assert (I[L.ioff["push_interval"]] == 0).all()
+    for _ in range(3):
+        b.step(np.zeros((n, m.nu)))
+        F = b.fs.reshape(L.nfloat, n)
+        np.testing.assert_array_equal(F[L.off["push"]:L.off["push"] + 2], 0.0)
