@@ -50,8 +50,16 @@ int duck_aux_size(const duck_sim* sim);
  * reset); DUCK_EUNSUPPORTED in a regular build */
 int duck_debug_stage_cycles(const duck_sim* sim, unsigned long long* out, int reset);
 
-/* Create a simulator for `model` (one of the Open Duck scenes; the kernel is specialised
- * on the model structure and rejects others with DUCK_EUNSUPPORTED). `ref` may be NULL
+/* Identity of a kernel specialisation: FNV-1a 64 over the float32-rounded model values the
+ * kernels bake at compile time (everything in duck_model_desc except the height-field
+ * elevation, which duck_create uploads). Host-only. */
+uint64_t duck_model_fingerprint(const duck_model_desc* model);
+/* 1 if this library holds kernels compiled for `model` (same fingerprint), else 0 */
+int duck_model_supported(const duck_model_desc* model);
+
+/* Create a simulator for `model`. The kernels are specialised on the model at build time
+ * (like MJX specialises its XLA program at jit time); a model none of this library's
+ * variants was compiled for is rejected with DUCK_EUNSUPPORTED. `ref` may be NULL
  * when cfg->use_imitation == 0. `device` is the HIP device ordinal. */
 int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const duck_refmotion* ref, int device,
                 duck_sim** out);

@@ -233,3 +233,73 @@ METRIC_NAMES = ["reward/tracking_lin_vel", "reward/tracking_ang_vel", "cost/torq
 # standing.py:290-297 + :584-606 (slot 6 unused; swing_peak stays in slot 7)
 STANDING_METRIC_NAMES = ["cost/orientation", "cost/torques", "cost/action_rate", "reward/alive", "cost/stand_still",
                          "cost/head_pos", None, "swing_peak"]
+
+
+# --------------------------------------------------------------------------------------
+# model fingerprint (mirror of duck_model_fingerprint in csrc/duck_capi.hip)
+# --------------------------------------------------------------------------------------
+
+def _fp_fields(d: DuckModelDesc):
+    """(kind, name, count) in the hash order of duck_model_fingerprint."""
+    nb, nj, nv, ng, np_, ns, nu = d.nbody, d.njnt, d.nv, d.ngeom, d.npair, d.nsite, d.nu
+    out = []
+    out += [("i", n, nb) for n in ("body_parentid", "body_rootid", "body_weldid", "body_jntnum", "body_jntadr",
+                                   "body_dofnum", "body_dofadr")]
+    out += [("f", "body_pos", 3 * nb), ("f", "body_quat", 4 * nb), ("f", "body_ipos", 3 * nb),
+            ("f", "body_iquat", 4 * nb), ("f", "body_mass", nb), ("f", "body_inertia", 3 * nb),
+            ("f", "body_invweight0", 2 * nb)]
+    out += [("i", n, nj) for n in ("jnt_type", "jnt_qposadr", "jnt_dofadr", "jnt_bodyid", "jnt_limited")]
+    out += [("f", "jnt_pos", 3 * nj), ("f", "jnt_axis", 3 * nj), ("f", "jnt_range", 2 * nj), ("f", "jnt_margin", nj),
+            ("f", "jnt_solref", 2 * nj), ("f", "jnt_solimp", 5 * nj)]
+    out += [("i", n, nv) for n in ("dof_bodyid", "dof_jntid", "dof_parentid")]
+    out += [("f", n, nv) for n in ("dof_armature", "dof_damping", "dof_frictionloss", "dof_invweight0")]
+    out += [("f", "dof_solref", 2 * nv), ("f", "dof_solimp", 5 * nv)]
+    out += [("i", n, ng) for n in ("geom_type", "geom_bodyid", "geom_dataid")]
+    out += [("f", "geom_pos", 3 * ng), ("f", "geom_quat", 4 * ng), ("f", "geom_rbound", ng), ("f", "geom_size", 3 * ng)]
+    out += [("i", n, np_) for n in ("pair_geom1", "pair_geom2", "pair_condim")]
+    out += [("f", "pair_friction", 5 * np_), ("f", "pair_solref", 2 * np_), ("f", "pair_solimp", 5 * np_),
+            ("f", "pair_margin", np_)]
+    return out
+
+
+def model_fingerprint(m: Model) -> int:
+    """Identity of a compiled kernel specialisation: FNV-1a 64 over the float32-rounded model values
+    the generated header bakes (the same bytes duck_model_fingerprint hashes from a duck_model_desc)."""
+    h = ModelDescHolder(m)
+    d = h.desc
+    buf = []
+    buf.append(np.array([d.nq, d.nv, d.nu, d.nbody, d.njnt, d.ngeom, d.nsite, d.nsensor, d.nsensordata, d.npair,
+                         d.iterations, d.ls_iterations, d.eulerdamp], dtype=np.int32).tobytes())
+    buf.append(np.array([d.timestep, *d.gravity, d.impratio, d.tolerance, d.ls_tolerance, d.meaninertia],
+                        dtype=np.float32).tobytes())
+
+    def arr(kind, name, n):
+        if n == 0:
+            return b""
+        p = getattr(d, name)
+        a = np.ctypeslib.as_array(p, shape=(n,))
+        return a.astype(np.int32 if kind == "i" else np.float32).tobytes()
+
+    for kind, name, n in _fp_fields(d):
+        buf.append(arr(kind, name, n))
+    buf.append(np.array([d.hull_nvert, d.hull_nface, d.hull_nedge, d.hfield_nrow, d.hfield_ncol],
+                        dtype=np.int32).tobytes())
+    buf.append(arr("f", "hull_vert", 3 * d.hull_nvert))
+    buf.append(arr("f", "hull_face_normal", 3 * d.hull_nface))
+    buf.append(arr("f", "hull_face_offset", d.hull_nface))
+    buf.append(arr("i", "hull_edge", 2 * d.hull_nedge))
+    buf.append(np.array(list(d.hfield_size), dtype=np.float32).tobytes())
+    ns, nu, nsen = d.nsite, d.nu, d.nsensor
+    buf.append(arr("i", "site_bodyid", ns) + arr("f", "site_pos", 3 * ns) + arr("f", "site_quat", 4 * ns))
+    for n in ("actuator_trnid", "actuator_ctrllimited", "actuator_forcelimited"):
+        buf.append(arr("i", n, nu))
+    for n in ("actuator_kp", "actuator_kv", "actuator_gear"):
+        buf.append(arr("f", n, nu))
+    buf.append(arr("f", "actuator_ctrlrange", 2 * nu) + arr("f", "actuator_forcerange", 2 * nu))
+    for n in ("sensor_type", "sensor_objid", "sensor_adr", "sensor_dim"):
+        buf.append(arr("i", n, nsen))
+    buf.append(arr("f", "qpos0", d.nq))
+    h64 = 1469598103934665603
+    for c in b"".join(buf):
+        h64 = ((h64 ^ c) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h64

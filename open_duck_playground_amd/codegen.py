@@ -18,6 +18,7 @@ from typing import List
 
 import numpy as np
 
+from .cabi import model_fingerprint
 from .mjcf import JNT_FREE, Model, quat2mat
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -511,6 +512,8 @@ def model_header(m: Model, variant: str) -> str:
            f"  static constexpr int iterations = {m.opt_iterations}, ls_iterations = {m.opt_ls_iterations};\n",
            f"  static constexpr float hull_radius = {_f(hr)};\n",
            f"  static constexpr float HULL_SAT_TIE = {_f(HULL_SAT_TIE)};  // = DUCK_HULL_SAT_TIE, oracle/duck_oracle.c\n",
+           f"  // duck_model_fingerprint of the model this header bakes: duck_create binds a model to it\n",
+           f"  static constexpr unsigned long long FINGERPRINT = 0x{model_fingerprint(m):016x}ull;\n",
            ]
     out.append(_arr("gravity", m.opt_gravity, "float"))
     out.append(_arr("hull_center", hc, "float"))
@@ -581,14 +584,33 @@ def model_header(m: Model, variant: str) -> str:
     return "".join(out[:2] + tdev + out[2:])
 
 
+# the scenes libduck.so ships with: (variant name, task asset)
+DEFAULT_VARIANTS = (("flat", "flat_terrain"), ("backlash", "flat_terrain_backlash"), ("rough", "rough_terrain"),
+                    ("rough_backlash", "rough_terrain_backlash"))
+
+
+def variant_unit(variant: str, header: str) -> str:
+    """The translation unit of one compiled model: the kernel templates instantiated on its header."""
+    return (f"// variant_{variant}.hip — kernels for the '{variant}' model ({header}).\n"
+            f"#include \"duck_env_kernels.h\"\n#include \"{header}\"\n\n"
+            f"DUCK_DEFINE_VARIANT({variant}, DuckModel_{variant})\n")
+
+
+def variant_registry(variants) -> str:
+    """duck_variants.inc: the X-macro list duck_capi.hip builds its variant table from."""
+    return "// generated by open_duck_playground_amd/codegen.py — do not edit\n" + \
+        "".join(f"DUCK_VARIANT({v})\n" for v in variants)
+
+
 def main():
     gen = os.path.join(HERE, "csrc", "generated")
     os.makedirs(gen, exist_ok=True)
-    for variant, task in (("flat", "flat_terrain"), ("backlash", "flat_terrain_backlash"),
-                          ("rough", "rough_terrain"), ("rough_backlash", "rough_terrain_backlash")):
+    for variant, task in DEFAULT_VARIANTS:
         m = Model.load(os.path.join(HERE, "assets", f"{task}.npz"))
         with open(os.path.join(gen, f"duck_model_{variant}.h"), "w") as f:
             f.write(model_header(m, variant))
+    with open(os.path.join(gen, "duck_variants.inc"), "w") as f:
+        f.write(variant_registry([v for v, _ in DEFAULT_VARIANTS]))
 
 
 if __name__ == "__main__":

@@ -17,7 +17,12 @@ POLY_COEFFICIENTS = os.path.join(ASSETS, "polynomial_coefficients.npz")
 
 
 def task_to_xml(task_name: str) -> str:
-    """Same keys as constants.task_to_xml (constants.py:28-34); returns the compiled model."""
+    """Same keys as constants.task_to_xml (constants.py:28-34); returns the compiled model.
+
+    A path to an MJCF scene (``.xml``) or a compiled model (``.npz``) is returned as is: the env
+    compiles it and, if no shipped kernel matches it, the kernels for it (native.model_library)."""
+    if task_name.endswith((".xml", ".npz")):
+        return task_name
     return {
         "flat_terrain": FLAT_TERRAIN,
         "rough_terrain": ROUGH_TERRAIN,

@@ -4,12 +4,16 @@
 // thread-local message; no entry allocates, synchronises or throws on the step path.
 #include "duck_common.h"
 
-const VariantOps* duck_variant_flat();
-const VariantOps* duck_variant_backlash();
-const VariantOps* duck_variant_rough();
-const VariantOps* duck_variant_rough_backlash();
-static const VariantOps* const kVariants[] = {duck_variant_flat(), duck_variant_backlash(), duck_variant_rough(),
-                                              duck_variant_rough_backlash()};
+// the compiled model variants of this library (codegen.variant_registry; generated/ for libduck.so,
+// a per-model build directory for a library compiled for another model, native.model_library)
+#define DUCK_VARIANT(name) const VariantOps* duck_variant_##name();
+#include "duck_variants.inc"
+#undef DUCK_VARIANT
+#define DUCK_VARIANT(name) duck_variant_##name(),
+static const VariantOps* const kVariants[] = {
+#include "duck_variants.inc"
+};
+#undef DUCK_VARIANT
 static constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 static thread_local std::string g_err;
@@ -18,9 +22,74 @@ int duck_fail(int code, const std::string& msg) {
   return code;
 }
 
+// FNV-1a 64 over the model values a compiled variant bakes (duck_model_fingerprint)
+namespace {
+struct Fnv {
+  uint64_t h = 1469598103934665603ull;
+  void bytes(const void* p, size_t n) {
+    const unsigned char* c = (const unsigned char*)p;
+    for (size_t i = 0; i < n; i++) { h ^= c[i]; h *= 1099511628211ull; }
+  }
+  void i32(const int* a, int n) {
+    for (int i = 0; i < n; i++) { int32_t v = a ? a[i] : 0; bytes(&v, 4); }
+  }
+  void f32(const double* a, int n) {  // the kernels bake float32: hash what they see
+    for (int i = 0; i < n; i++) { float v = a ? (float)a[i] : 0.0f; bytes(&v, 4); }
+  }
+};
+}  // namespace
+
 extern "C" {
 
+uint64_t duck_model_fingerprint(const duck_model_desc* m) {
+  if (!m) return 0;
+  Fnv f;
+  const int nb = m->nbody, nj = m->njnt, nv = m->nv, ng = m->ngeom, np = m->npair, ns = m->nsite, nu = m->nu;
+  const int sizes[] = {m->nq, m->nv, m->nu, m->nbody, m->njnt, m->ngeom, m->nsite, m->nsensor, m->nsensordata,
+                       m->npair, m->iterations, m->ls_iterations, m->eulerdamp};
+  f.i32(sizes, 13);
+  const double opt[] = {m->timestep, m->gravity[0], m->gravity[1], m->gravity[2], m->impratio, m->tolerance,
+                        m->ls_tolerance, m->meaninertia};
+  f.f32(opt, 8);
+  f.i32(m->body_parentid, nb); f.i32(m->body_rootid, nb); f.i32(m->body_weldid, nb); f.i32(m->body_jntnum, nb);
+  f.i32(m->body_jntadr, nb); f.i32(m->body_dofnum, nb); f.i32(m->body_dofadr, nb);
+  f.f32(m->body_pos, 3 * nb); f.f32(m->body_quat, 4 * nb); f.f32(m->body_ipos, 3 * nb); f.f32(m->body_iquat, 4 * nb);
+  f.f32(m->body_mass, nb); f.f32(m->body_inertia, 3 * nb); f.f32(m->body_invweight0, 2 * nb);
+  f.i32(m->jnt_type, nj); f.i32(m->jnt_qposadr, nj); f.i32(m->jnt_dofadr, nj); f.i32(m->jnt_bodyid, nj);
+  f.i32(m->jnt_limited, nj);
+  f.f32(m->jnt_pos, 3 * nj); f.f32(m->jnt_axis, 3 * nj); f.f32(m->jnt_range, 2 * nj); f.f32(m->jnt_margin, nj);
+  f.f32(m->jnt_solref, 2 * nj); f.f32(m->jnt_solimp, 5 * nj);
+  f.i32(m->dof_bodyid, nv); f.i32(m->dof_jntid, nv); f.i32(m->dof_parentid, nv);
+  f.f32(m->dof_armature, nv); f.f32(m->dof_damping, nv); f.f32(m->dof_frictionloss, nv); f.f32(m->dof_invweight0, nv);
+  f.f32(m->dof_solref, 2 * nv); f.f32(m->dof_solimp, 5 * nv);
+  f.i32(m->geom_type, ng); f.i32(m->geom_bodyid, ng); f.i32(m->geom_dataid, ng);
+  f.f32(m->geom_pos, 3 * ng); f.f32(m->geom_quat, 4 * ng); f.f32(m->geom_rbound, ng); f.f32(m->geom_size, 3 * ng);
+  f.i32(m->pair_geom1, np); f.i32(m->pair_geom2, np); f.i32(m->pair_condim, np);
+  f.f32(m->pair_friction, 5 * np); f.f32(m->pair_solref, 2 * np); f.f32(m->pair_solimp, 5 * np);
+  f.f32(m->pair_margin, np);
+  const int hull[] = {m->hull_nvert, m->hull_nface, m->hull_nedge, m->hfield_nrow, m->hfield_ncol};
+  f.i32(hull, 5);
+  f.f32(m->hull_vert, 3 * m->hull_nvert); f.f32(m->hull_face_normal, 3 * m->hull_nface);
+  f.f32(m->hull_face_offset, m->hull_nface); f.i32(m->hull_edge, 2 * m->hull_nedge);
+  f.f32(m->hfield_size, 4);  // the elevation itself is uploaded by duck_create, not baked
+  f.i32(m->site_bodyid, ns); f.f32(m->site_pos, 3 * ns); f.f32(m->site_quat, 4 * ns);
+  f.i32(m->actuator_trnid, nu); f.i32(m->actuator_ctrllimited, nu); f.i32(m->actuator_forcelimited, nu);
+  f.f32(m->actuator_kp, nu); f.f32(m->actuator_kv, nu); f.f32(m->actuator_gear, nu);
+  f.f32(m->actuator_ctrlrange, 2 * nu); f.f32(m->actuator_forcerange, 2 * nu);
+  f.i32(m->sensor_type, m->nsensor); f.i32(m->sensor_objid, m->nsensor); f.i32(m->sensor_adr, m->nsensor);
+  f.i32(m->sensor_dim, m->nsensor);
+  f.f32(m->qpos0, m->nq);
+  return f.h;
+}
+
 int duck_version(void) { return DUCK_VERSION; }
+
+int duck_model_supported(const duck_model_desc* model) {
+  if (!model) return 0;
+  for (int i = 0; i < kNumVariants; i++)
+    if (kVariants[i]->matches(model)) return 1;
+  return 0;
+}
 const char* duck_last_error(void) { return g_err.c_str(); }
 
 int duck_layout_get(int nq, int nv, int nu, int imitation, int task, duck_layout* out) {
@@ -50,7 +119,8 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
     if (kVariants[i]->matches(model)) v = i;
   if (v < 0)
     return duck_fail(DUCK_EUNSUPPORTED,
-                     "model does not match a compiled Open Duck variant (flat / flat_backlash / rough / rough_backlash)");
+                     "no kernel of this library is compiled for this model (duck_model_fingerprint differs); "
+                     "compile one with native.model_library / codegen");
   if (cfg->use_imitation && !ref) return duck_fail(DUCK_EINVAL, "use_imitation requires a reference-motion table");
   if (cfg->n_substeps < 1 || cfg->action_max_delay < 1 || cfg->action_max_delay > 3)
     return duck_fail(DUCK_EINVAL, "bad config (n_substeps >= 1, 1 <= action_max_delay <= 3)");

@@ -901,29 +901,9 @@ __global__ void randomize_kernel(int n, float* dr, duck_dr_layout D, uint64_t se
 // --------------------------------------------------------------------------------------
 template <class Md>
 static bool matches(const duck_model_desc* m) {
-  if (m->nq != Md::NQ || m->nv != Md::NV || m->nu != Md::NU || m->nbody != Md::NB || m->njnt != Md::NJ) return false;
-  if (m->npair != Md::NPAIR || m->hull_nvert != Md::NHV) return false;
-  auto close = [](double a, float b) { return fabs(a - (double)b) <= 1e-6 * (1.0 + fabs(a)); };
-  for (int b = 0; b < Md::NB; b++) {
-    if (m->body_parentid[b] != Md::body_parentid[b]) return false;
-    if (!close(m->body_mass[b], Md::body_mass[b])) return false;
-    for (int k = 0; k < 3; k++)
-      if (!close(m->body_pos[3 * b + k], Md::body_pos[b][k])) return false;
-  }
-  for (int a = 0; a < Md::NU; a++)
-    if (!close(m->actuator_kp[a], Md::actuator_kp[a])) return false;
-  for (int p = 0; p < Md::NPAIR; p++)
-    if (m->pair_geom1[p] != Md::pair_geom1[p] || m->pair_geom2[p] != Md::pair_geom2[p] ||
-        !close(m->pair_friction[5 * p], Md::pair_friction[p][0]))
-      return false;
-  // floor: mjGEOM_PLANE (0) or mjGEOM_HFIELD (1) with the baked grid size
-  if (m->geom_type[Md::FLOOR_GEOM] != Md::FLOOR_TYPE) return false;
-  if (Md::FLOOR_TYPE == 1) {
-    if (m->hfield_nrow != Md::HF_NROW || m->hfield_ncol != Md::HF_NCOL || !m->hfield_data) return false;
-    for (int k = 0; k < 4; k++)
-      if (!close(m->hfield_size[k], Md::HF_SIZE[k])) return false;
-  }
-  return true;
+  // the header bakes every model value the kernels read: a model binds to this variant only if
+  // it hashes to the same float32 values (duck_model_fingerprint, codegen.model_fingerprint)
+  return duck_model_fingerprint(m) == Md::FINGERPRINT;
 }
 
 template <class Md>

@@ -92,9 +92,13 @@ struct Lay {
   // RNE accumulators live in the H + row storage (dead until smooth()/make_rows())
   static constexpr int CACC = H, CFRC = CACC + 6 * NB;
   static_assert(12 * NB <= Md::NM + 4 * NROW, "RNE scratch must fit in H + rows");
-  // constraint rows
-  static constexpr int JA = H + Md::NM, JV = JA + NROW, RD = JV + NROW, AREF = RD + NROW;
-  static constexpr int LSGN = AREF + NROW;
+  // constraint rows, NROWS apart: the rows, or more when the hull/hull SAT scratch that reuses the
+  // H + row storage (6 floats per hull edge and face) needs it (a model without dof friction rows)
+  static constexpr int SAT_SCRATCH = 6 * (Md::NHE + Md::NHF);
+  static constexpr int NROWS =
+      (Md::NM + 4 * NROW + Md::NLIM >= SAT_SCRATCH) ? NROW : (SAT_SCRATCH - Md::NM - Md::NLIM + 3) / 4;
+  static constexpr int JA = H + Md::NM, JV = JA + NROWS, RD = JV + NROWS, AREF = RD + NROWS;
+  static constexpr int LSGN = AREF + NROWS;
   static constexpr int CR = LSGN + Md::NLIM, CFR = CR + 3 * NCON, CDIST = CFR + 9 * NCON;
   // Newton 6x6 foot blocks live in CIN's storage (composite inertias are dead after crb())
   static constexpr int KL = CIN, KR = KL + 21, KLR = KR + 21, FL = KLR + 36, FR = FL + 6;

@@ -1907,7 +1907,8 @@ struct TPhys {
     }
   }
 
-  // mjx solver.solve, iterations = 1
+  // mjx solver.solve: warm-start choice, then Md::iterations Newton steps (the Open Duck scenes
+  // use 1; a model compiled with more iterates to the MJX stopping rule on the cost improvement)
   static DK void solve(LP L, int lane, float* scratch, int stride) {
     STAGE_T0();
     // M as full symmetric columns in registers for every M.x of the solver
@@ -1972,6 +1973,7 @@ struct TPhys {
     }
     TSYNC();
     STAGE_MARK(9);
+    for (int newton_it = 0;;) {
     const bool sparse_ok = newton_fused<false>(L, lane, Mc);
     STAGE_MARK(10);
     if (sparse_ok) {
@@ -2119,6 +2121,31 @@ struct TPhys {
       for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] += L[Ly::SRCH + i] * alpha;
     TSYNC();
     STAGE_MARK(13);
+    if constexpr (Md::iterations <= 1) {
+      break;
+    } else {
+      // next Newton step from the new point (mjx solver.solve loop): M.qacc and J.qacc - aref move
+      // along the search direction; stop on the iteration count or a cost improvement below
+      // tolerance (the gradient-norm test is not repeated here: at that point the next step's
+      // change is below fp32 resolution)
+      if (++newton_it >= Md::iterations) break;
+      const float a = improved ? alpha : 0.0f;
+      const float cnew = improved ? (lo.cost < hi.cost ? lo.cost : hi.cost) : p0.cost;
+      g0 = G0 + a * G1 + a * a * G2;  // gauss at the new point
+      for (int i = lane; i < NV; i += TEAM) L[Ly::MA + i] += a * L[Ly::GRAD + i];  // GRAD = M.search
+      if (lane < NFRIC) L[Ly::JA + lane] = R.fja + a * R.fv;
+#pragma unroll
+      for (int m = 0; m < NLR; m++) {
+        const int r = lane + TEAM * m;
+        if (r < NLIM) L[Ly::JA + R_LIM + r] = R.ja[m] + a * R.v[m];
+      }
+      if (lane < NCON)
+        for (int e = 0; e < 4; e++) L[Ly::JA + R_CON + 4 * lane + e] = R.ja[NLR + e] + a * R.v[NLR + e];
+      TSYNC();
+      const float scale = 1.0f / (Md::meaninertia * (float)(NV > 1 ? NV : 1));
+      if (scale * (p0.cost - cnew) < Md::tolerance) break;
+    }
+    }
   }
 
   // ---------------- sensors (last substep) ----------------

@@ -32,7 +32,7 @@ from . import constants
 from .cabi import METRIC_NAMES, TASK_JOYSTICK, ModelDescHolder, dr_layout, layout, refmotion_struct
 from .config import ConfigDict, default_config  # noqa: F401  (re-exported like the reference module)
 from .mjcf import JNT_FREE, Model
-from .native import DuckError, check, lib
+from .native import DuckError, check, lib, model_library
 from .refmotion import PolyReferenceMotion
 
 USE_IMITATION_REWARD = cfgmod.USE_IMITATION_REWARD
@@ -71,7 +71,11 @@ class OpenDuckMiniV2Env:
 
     def __init__(self, xml_path: str, config: ConfigDict, config_overrides: Optional[Dict[str, Any]] = None) -> None:
         self._config = cfgmod.apply_overrides(config, config_overrides)
-        self._mj_model = Model.load(xml_path)
+        if xml_path.endswith(".xml"):  # an MJCF scene: compiled here (base.py:53-56 sets the timestep)
+            from .mjcf import compile_mjcf
+            self._mj_model = compile_mjcf(xml_path, timestep=self._config.sim_dt)
+        else:
+            self._mj_model = Model.load(xml_path)
         self._xml_path = xml_path
         maps = cfgmod.AddressMaps(self._mj_model)
         self.floating_base_name = maps.floating_base_name
@@ -197,21 +201,22 @@ class Joystick(OpenDuckMiniV2Env):
         self._ref_struct, self._ref_coeffs = refmotion_struct(table)
         handle = C.c_void_p()
         dev = self.device.index if self.device.index is not None else 0
-        check(lib().duck_create(C.byref(self._desc.desc), C.byref(self._cfg_struct), C.byref(self._ref_struct), dev,
-                                C.byref(handle)))
+        self._lib = lib(model_library(m))
+        check(self._lib.duck_create(C.byref(self._desc.desc), C.byref(self._cfg_struct), C.byref(self._ref_struct),
+                                    dev, C.byref(handle)), self._lib)
         self._sim = handle
         self._scratch = None
 
     def __del__(self):
         try:
             if getattr(self, "_sim", None):
-                lib().duck_destroy(self._sim)
+                self._lib.duck_destroy(self._sim)
         except Exception:
             pass
 
     def _reconfigure(self) -> None:
         if getattr(self, "_sim", None):
-            lib().duck_destroy(self._sim)
+            self._lib.duck_destroy(self._sim)
             self._sim = None
         self._create_sim()
 
@@ -271,10 +276,11 @@ class Joystick(OpenDuckMiniV2Env):
         if mask is not None:
             mask = mask.to(device=dev, dtype=torch.uint8).contiguous()
             mask_ptr = mask.data_ptr()
-        check(lib().duck_reset(self._sim, n, state.fstate.data_ptr(), state.istate.data_ptr(), mask_ptr,
+        check(self._lib.duck_reset(self._sim, n, state.fstate.data_ptr(), state.istate.data_ptr(), mask_ptr,
                                int(rng) & 0xFFFFFFFFFFFFFFFF, self.env_offset,
                                self.dr.data_ptr() if self.dr is not None else None,
-                               state.obs["state"].data_ptr(), state.obs["privileged_state"].data_ptr(), self._stream()))
+                               state.obs["state"].data_ptr(), state.obs["privileged_state"].data_ptr(), self._stream()),
+              self._lib)
         if mask is None:
             state.reward.zero_()
             state.done.zero_()
@@ -286,10 +292,11 @@ class Joystick(OpenDuckMiniV2Env):
         if action.numel() != n * self.action_size:
             raise DuckError(f"action must hold {n} x {self.action_size} values, got {tuple(action.shape)}")
         action = action.to(device=self.device, dtype=torch.float32).reshape(n, self.action_size).contiguous()
-        check(lib().duck_step(self._sim, n, state.fstate.data_ptr(), state.istate.data_ptr(),
+        check(self._lib.duck_step(self._sim, n, state.fstate.data_ptr(), state.istate.data_ptr(),
                               self.dr.data_ptr() if self.dr is not None else None, action.data_ptr(),
                               state.obs["state"].data_ptr(), state.obs["privileged_state"].data_ptr(),
-                              state.reward.data_ptr(), state.done.data_ptr(), self._scratch_ptr(), self._stream()))
+                              state.reward.data_ptr(), state.done.data_ptr(), self._scratch_ptr(), self._stream()),
+              self._lib)
         return state
 
     def _scratch_ptr(self):
@@ -307,13 +314,13 @@ class Joystick(OpenDuckMiniV2Env):
             if not t.is_contiguous() or t.dtype != torch.float32 or t.device != self.device or t.shape[1] != n:
                 raise DuckError("physics_step expects contiguous float32 SoA tensors on the env device")
         scratch = torch.zeros(n * self._mj_model.nv ** 2, dtype=torch.float32, device=self.device)
-        check(lib().duck_physics_step(self._sim, n, qpos.data_ptr(), qvel.data_ptr(), qacc_warmstart.data_ptr(),
+        check(self._lib.duck_physics_step(self._sim, n, qpos.data_ptr(), qvel.data_ptr(), qacc_warmstart.data_ptr(),
                                       ctrl.data_ptr(), self.dr.data_ptr() if self.dr is not None else None,
                                       int(n_substeps), aux.data_ptr() if aux is not None else None,
-                                      scratch.data_ptr(), self._stream()))
+                                      scratch.data_ptr(), self._stream()), self._lib)
 
     def aux_size(self) -> int:
-        return int(lib().duck_aux_size(self._sim))
+        return int(self._lib.duck_aux_size(self._sim))
 
 
 def domain_randomize(env: Joystick, rng: int) -> torch.Tensor:
@@ -325,7 +332,8 @@ def domain_randomize(env: Joystick, rng: int) -> torch.Tensor:
     m = env.mj_model
     D = dr_layout(m.nbody, m.nu)
     dr = torch.zeros(D["nfloat"] * env.num_envs, dtype=torch.float32, device=env.device)
-    check(lib().duck_randomize(env._sim, env.num_envs, dr.data_ptr(), int(rng), env.env_offset, env._stream()))
+    check(env._lib.duck_randomize(env._sim, env.num_envs, dr.data_ptr(), int(rng), env.env_offset, env._stream()),
+          env._lib)
     env.dr = dr
     env._reconfigure()
     return dr

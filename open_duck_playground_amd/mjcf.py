@@ -376,12 +376,14 @@ def compile_mjcf(path: str, timestep: Optional[float] = None, asset_dir: Optiona
 
     # assets
     mesh_files: Dict[str, str] = {}
+    mesh_scale: Dict[str, np.ndarray] = {}
     hfields: Dict[str, Tuple[np.ndarray, np.ndarray]] = {}
     for asset in root.findall("asset"):
         for me in asset.findall("mesh"):
             f = me.get("file")
             nm = me.get("name", os.path.splitext(os.path.basename(f))[0])
             mesh_files[nm] = os.path.join(meshdir, f)
+            mesh_scale[nm] = _vec(me.get("scale"), 3) if me.get("scale") else np.ones(3)  # mesh/@scale
         for hf in asset.findall("hfield"):
             nm = hf.get("name")
             data = read_hfield_png(os.path.join(base_dir, hf.get("file")))
@@ -596,7 +598,7 @@ def compile_mjcf(path: str, timestep: Optional[float] = None, asset_dir: Optiona
     for g in geoms:
         if g["type"] == GEOM_MESH and (g["contype"] or g["conaffinity"]):
             if g["mesh"] not in mesh_hull_id:
-                hulls.append(convex_hull(read_stl(mesh_files[g["mesh"]])))
+                hulls.append(convex_hull(read_stl(mesh_files[g["mesh"]]) * mesh_scale[g["mesh"]]))
                 mesh_hull_id[g["mesh"]] = len(hulls) - 1
             hid = mesh_hull_id[g["mesh"]]
             geom_dataid.append(hid)

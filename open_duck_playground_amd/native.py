@@ -17,8 +17,10 @@ LIB_PATH = os.environ.get("DUCK_LIB") or os.path.join(HERE, "libduck.so")
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 
+BUILD = os.path.join(HERE, "build")  # libraries compiled for other models (model_library)
+
 EXPORTS = ["duck_version", "duck_last_error", "duck_layout_get", "duck_aux_size", "duck_create", "duck_destroy",
-           "duck_debug_stage_cycles",
+           "duck_debug_stage_cycles", "duck_model_fingerprint", "duck_model_supported",
            "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae"]
 
 
@@ -36,15 +38,23 @@ class DuckLayout(C.Structure):
         "rng_key", "rng_ctr", "step", "push_step", "push_interval", "imitation_i", "ep_steps", "nint")]
 
 
-def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no_ilp=(), isa_check: bool = True) -> str:
+def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no_ilp=(), isa_check: bool = True,
+          gen_dir: str = None) -> str:
     """Compile libduck.so for gfx950 with hipcc (in-tree, so it travels with the repo).
 
     One translation unit per model variant (variant_*.hip) plus the C ABI (duck_capi.hip),
-    compiled in parallel and linked into one shared library."""
+    compiled in parallel and linked into one shared library. ``gen_dir`` (model_library) holds
+    the units, headers and variant registry of other models instead of the four shipped scenes."""
     out = os.path.abspath(out or LIB_PATH)
-    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+    if gen_dir is None:
+        srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+        inc = os.path.join(CSRC, "generated")
+    else:
+        srcs = [os.path.join(CSRC, "duck_capi.hip")] + \
+            sorted(os.path.join(gen_dir, f) for f in os.listdir(gen_dir) if f.endswith(".hip"))
+        inc = gen_dir
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
-        [os.path.join(CSRC, "generated", f) for f in os.listdir(os.path.join(CSRC, "generated"))] + \
+        [os.path.join(inc, f) for f in os.listdir(inc)] + \
         [os.path.join(ROOT, "include", f) for f in ("duck.h", "duck_env.h", "duck_model.h")] + \
         [os.path.abspath(__file__)]  # the compile flags live here
     if not defines and not extra_flags and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
@@ -57,7 +67,8 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no
     # honoured: the termination check and the auto-reset NaN guard depend on them
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-hip-fp32-correctly-rounded-divide-sqrt",
              "-fgpu-flush-denormals-to-zero", "-fno-slp-vectorize",
-             "-fno-signed-zeros", "-fno-trapping-math", "-fno-math-errno", "-freciprocal-math"] + \
+             "-fno-signed-zeros", "-fno-trapping-math", "-fno-math-errno", "-freciprocal-math", "-I" + CSRC,
+             "-I" + inc] + \
         [f"-D{d}" for d in defines] + list(extra_flags)
     # the machine scheduler's max-ILP strategy: the step kernel runs one wave per SIMD, so
     # occupancy-driven scheduling buys nothing and latency hiding must come from the wave's own
@@ -88,6 +99,36 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no
     return out
 
 
+def model_library(m, verbose: bool = False) -> str:
+    """The library whose kernels are compiled for model ``m``: libduck.so when ``m`` is one of the
+    shipped scenes, else ``build/libduck_<fingerprint>.so``, generated and compiled on first use
+    (codegen.model_header; the model compiler's structural checks apply). The MI355X analogue of
+    MJX re-specialising its program when the MJCF changes: an edited XML needs no hand edits."""
+    from . import codegen
+    from .cabi import model_fingerprint
+    fp = model_fingerprint(m)
+    for var, task in codegen.DEFAULT_VARIANTS:
+        hdr = os.path.join(CSRC, "generated", f"duck_model_{var}.h")
+        if os.path.exists(hdr) and f"FINGERPRINT = 0x{fp:016x}ull" in open(hdr).read():
+            return LIB_PATH
+    name = f"m{fp:016x}"
+    out = os.path.join(BUILD, f"libduck_{name}.so")
+    if os.path.exists(out) and os.path.getmtime(out) >= max(
+            os.path.getmtime(os.path.join(CSRC, f)) for f in os.listdir(CSRC) if f.endswith((".h", ".hip"))):
+        return out
+    gen = os.path.join(BUILD, f"gen_{name}")
+    os.makedirs(gen, exist_ok=True)
+    files = {f"duck_model_{name}.h": codegen.model_header(m, name),
+             f"variant_{name}.hip": codegen.variant_unit(name, f"duck_model_{name}.h"),
+             "duck_variants.inc": codegen.variant_registry([name])}
+    for fn, text in files.items():
+        path = os.path.join(gen, fn)
+        if not os.path.exists(path) or open(path).read() != text:
+            with open(path, "w") as f:
+                f.write(text)
+    return build(verbose=verbose, out=out, gen_dir=gen)
+
+
 def isa_exec_faults(so_path: str):
     """Blocks of the gfx950 code in so_path whose exec-restoring join starts with AGPR/scratch moves
     (tools/isa_exec_check.py): each is a lane-masked live-range split, i.e. a wrong-result kernel."""
@@ -101,16 +142,16 @@ def isa_exec_faults(so_path: str):
     return [f"{func[:80]}: {len(pre)} move(s) before '{ins}'" for _, func, _, pre, ins in found]
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    """Load libduck.so (raises if it is missing: no fallback path exists)."""
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise DuckError(f"{LIB_PATH} not built; run __graft_entry__.build() or native.build()")
-        L = C.CDLL(LIB_PATH)
+def lib(path: str = None):
+    """Load libduck.so, or the library at ``path`` (raises if it is missing: no fallback path exists)."""
+    path = os.path.abspath(path or LIB_PATH)
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise DuckError(f"{path} not built; run __graft_entry__.build() or native.build()")
+        L = C.CDLL(path)
         vp = C.c_void_p
         L.duck_version.restype = C.c_int
         L.duck_last_error.restype = C.c_char_p
@@ -124,12 +165,16 @@ def lib():
         L.duck_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.duck_randomize.argtypes = [vp, C.c_int, vp, C.c_uint64, C.c_int64, vp]
         L.duck_physics_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp, vp, vp]
-        L.duck_gae.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp]
-        _lib = L
-    return _lib
+        L.duck_model_fingerprint.restype = C.c_uint64
+        L.duck_model_fingerprint.argtypes = [C.POINTER(DuckModelDesc)]
+        L.duck_model_supported.argtypes = [C.POINTER(DuckModelDesc)]
+        if hasattr(L, "duck_gae"):
+            L.duck_gae.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp]
+        _libs[path] = L
+    return _libs[path]
 
 
-def check(rc: int):
+def check(rc: int, L=None):
     if rc != 0:
-        raise DuckError(f"libduck error {rc}: {lib().duck_last_error().decode()}")
+        raise DuckError(f"libduck error {rc}: {(L or lib()).duck_last_error().decode()}")
     return rc

@@ -19,6 +19,7 @@ tie): "sensitive". Anything else is a "defect".
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -167,6 +168,10 @@ CASES = {
                                         episode_length=3, overrides=_short_push()),
     "flat_zero_push_interval": dict(task="flat_terrain", imitation=False,
                                     overrides={"push_config.interval_range": [0.0, 0.009]}),
+    # an edited MJCF scene on its own compiled kernels (native.model_library)
+    "edited_scene": dict(task=os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "models",
+                                           "flat_terrain_edited.npz"), imitation=False, force_push=True,
+                         force_resample=True),
     "standing": dict(task="flat_terrain", imitation=False, force_push=True, force_resample=True, standing=True),
 }
 
