@@ -13,10 +13,16 @@ no collective in the step -> weak scaling; the timed region is bracketed by barr
 synchronize and the max over ranks is reported.
 
 Extra JSON objects:
-  roofline      the step kernel against HBM: algorithmic bytes per env-step
-                x envs per launch / average launch time from HIP events on the launch stream.
-  cpu_baseline  the fp64 C oracle (oracle/, a restatement of the same step) over OpenMP host
-                threads on a bounded sample (rank 0, N=1 only).
+  roofline        the step kernel against HBM: algorithmic bytes per env-step
+                  x envs per launch / average launch time from HIP events on the launch stream.
+  issue_roofline  the same kernel against the FP32 VALU issue rate (its real bound: one wave per
+                  SIMD on a dependent chain), from the SQ counters of the committed rocprofv3 run
+                  of this library (profiles/, checked against the library's sha1).
+  cpu_baseline    the fp64 C oracle (oracle/, a restatement of the same step) over OpenMP on the
+                  host cores this job may use (affinity, capped by the cgroup CPU quota), on a
+                  bounded sample (rank 0, N=1 only), plus BASELINE configs[0] (C1): 1 env, 1 core.
+
+--strong keeps 4096 envs in total over the N ranks (strong scaling) instead of 4096 per rank.
 """
 
 from __future__ import annotations
@@ -38,6 +44,10 @@ from open_duck_playground_amd.joystick import Joystick, domain_randomize, wrap_f
 from open_duck_playground_amd.sharding import shard_from_env  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# FP32 VALU issue peak: 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz = 39.3 T lane-instructions/s (a wave64
+# VALU instruction occupies a SIMD for 4 cycles); = the 157.3 TFLOPS vector spec / 2 (FMA) / 2 (packed)
+VALU_PEAK_TLANE = 256 * 4 * 16 * 2.4e9 / 1e12
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r02_pmc_c2.json")  # tools/gpu_pmc.sh r02 C2
 
 # BASELINE.json configs[1..4] (configs[0] is the reference's 1-env CPU plumbing case)
 CONFIGS = {
@@ -68,6 +78,46 @@ def algorithmic_bytes(env: Joystick) -> int:
     if env.dr is not None:
         rd += 4 * env.dr.numel() // env.num_envs
     return rd + wr
+
+
+def host_cores() -> int:
+    """Host cores this process may use: its CPU affinity, capped by the cgroup CPU quota (the GPU box
+    gives a job a share of a larger machine; nproc/affinity show the whole machine there)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def lib_sha1() -> str:
+    import hashlib
+    from open_duck_playground_amd.native import LIB_PATH
+    return hashlib.sha1(open(LIB_PATH, "rb").read()).hexdigest()
+
+
+def cpu_baseline_c1(task: str, use_imitation: bool, budget_s: float):
+    """BASELINE configs[0]: one env on one core (the reference's CPU plumbing case)."""
+    from open_duck_playground_amd.config import default_config, env_config_struct
+    from open_duck_playground_amd.joystick import OpenDuckMiniV2Env
+    from open_duck_playground_amd import constants
+    from tests.oracle_ffi import OracleBatch, OracleModel
+
+    base = OpenDuckMiniV2Env(xml_path=constants.task_to_xml(task), config=default_config())
+    m = base.mj_model
+    batch = OracleBatch(OracleModel(m), env_config_struct(m, base._config, use_imitation, True, False), 1)
+    batch.reset(seed=0, threads=1)
+    acts = np.random.default_rng(1234).uniform(-1, 1, (4, 1, m.nu))
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        batch.step(acts[steps % 4], threads=1)
+        steps += 1
+    el = time.perf_counter() - t0
+    return {"value": steps / el, "unit": "env-steps/s", "cores": 1, "envs": 1,
+            "sample": f"C1: {task}, 1 env x {steps} env-steps ({el:.1f} s), fp64 oracle, 1 thread"}
 
 
 def cpu_baseline(task: str, use_imitation: bool, budget_s: float, threads: int):
@@ -107,7 +157,8 @@ def main():
                     help="BASELINE.json workload: C2 flat (the metric), C3 +imitation, C4 rough+DR, C5 rough+DR+backlash")
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (0 = the config's)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline sampling (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this job may use")
+    ap.add_argument("--strong", action="store_true", help="4096 envs in total over the ranks (strong scaling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,6 +180,8 @@ def main():
 
     cfg = CONFIGS[args.config]
     n = args.envs or cfg["envs"]
+    if args.strong:
+        n = max(1, n // world)
     shard = shard_from_env(n)
     env = Joystick(cfg["task"], num_envs=n, device=dev, use_imitation=cfg["imitation"], env_offset=shard.env_offset)
     env = wrap_for_brax_training(env, episode_length=1000, randomization_fn=domain_randomize if cfg["dr"] else None)
@@ -151,6 +204,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev_all = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev_all[0].record()
     for i in range(K):
         if ev[i] is not None:
             ev[i][0].record()
@@ -158,6 +213,7 @@ def main():
             ev[i][1].record()
         else:
             env.step(state, pool[i % len(pool)])
+    ev_all[1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -166,36 +222,46 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    kern_ms = float(np.mean([p[0].elapsed_time(p[1]) for p in ev if p is not None]))
+    # average launch duration: events around every 8th launch, never above the events around all
+    # K back-to-back launches on the same stream (a true upper bound: the launches serialise)
+    kern_ms = min(float(np.mean([p[0].elapsed_time(p[1]) for p in ev if p is not None])),
+                  ev_all[0].elapsed_time(ev_all[1]) / K)
     ok = bool(torch.isfinite(state.obs["state"]).all().item())
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
-        thr = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        thr = args.cpu_threads or host_cores()
         cpu = cpu_baseline(cfg["task"], cfg["imitation"], args.cpu_budget, thr)
+        cpu["host_cores"] = host_cores()
+        cpu["c1"] = cpu_baseline_c1(cfg["task"], cfg["imitation"], min(5.0, args.cpu_budget))
 
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):  # PMC bytes per launch from the committed rocprofv3 run of this config
-        t = json.load(open(tpath)).get(args.config)
-        if t and n == CONFIGS[args.config]["envs"]:
-            traffic = t["bytes_per_launch"]
-    issue = None
-    spath = os.path.join(ROOT, "profiles", "r01_sq_c2.json")
-    if args.config == "C2" and n == CONFIGS["C2"]["envs"] and os.path.exists(spath):
-        # the step kernel's own bound: one wave per SIMD on a dependent chain;
-        # SQ issue fractions of the committed rocprofv3 --pmc run of this config
-        q = json.load(open(spath))
-        issue = {k: round(q[k], 3) for k in ("valu_busy_frac", "waitcnt_frac", "lds_busy_frac", "salu_frac")}
-        issue["source"] = "profiles/r01_sq_c2.json"
+    # PMC numbers of the committed rocprofv3 run of this configuration (tools/gpu_pmc.sh); valid
+    # only for the library they were measured on
+    traffic, issue_rf = None, None
+    if os.path.exists(PMC_PROFILE) and args.config == "C2" and n == CONFIGS["C2"]["envs"]:
+        prof = json.load(open(PMC_PROFILE))
+        current = prof.get("lib_sha1") == lib_sha1()
+        src = {"source": os.path.relpath(PMC_PROFILE, ROOT), "lib_sha1_matches": current}
+        if current:
+            traffic = prof["hbm_bytes_per_launch"]
+        valu = prof["SQ_INSTS_VALU"] * 64 / (kern_ms * 1e-3) / 1e12     # lane-instructions / s
+        issue_rf = {"bound": "valu", "achieved": valu, "peak": VALU_PEAK_TLANE, "unit": "T lane-instr/s",
+                    "frac": valu / VALU_PEAK_TLANE, "valu_insts_per_launch": prof["SQ_INSTS_VALU"],
+                    "valu_busy_frac": prof["valu_busy_frac"], "waitcnt_frac": prof["waitcnt_frac"], **src}
     if rank == 0:
         B = algorithmic_bytes(env)
         achieved = B * n / (kern_ms * 1e-3) / 1e9
         total = world * n * K
+        metric = "env steps/sec (all envs) open_duck_mini_v2 flat, 4096 envs, 1/2/4/8 GPUs"  # BASELINE.json
+        if args.config != "C2" or args.strong or n != cfg["envs"]:
+            metric = (f"env steps/sec (all envs) open_duck_mini_v2 {cfg['task']}"
+                      f"{' + imitation' if cfg['imitation'] else ''}{' + DR' if cfg['dr'] else ''}, "
+                      f"{world * n} envs over {world} GPU(s)")
         line = {
-            "metric": "env steps/sec (all envs) open_duck_mini_v2 flat, 4096 envs, 1/2/4/8 GPUs",
+            "metric": metric,
             "value": total / el, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
-            "ms_per_step": el / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step": el / K * 1e3, "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
+            "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (keyframe home + reset randomisation, actions U(-1,1)^14)",
             "config": {"workload": f"{args.config}: {cfg['task']}, {'imitation' if cfg['imitation'] else 'no imitation'}"
                                    f"{', domain randomization' if cfg['dr'] else ''}, {n} envs per GPU, "
@@ -205,8 +271,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "step_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": B},
+            "issue_roofline": issue_rf,
             "cpu_baseline": cpu,
-            "issue": issue,
             "finite": ok,
         }
         print(json.dumps(line), flush=True)
