@@ -105,3 +105,28 @@ def test_onnx_matches_policy(trained):
 def test_varint_encoding():
     assert onnx_export._varint(0) == b"\x00" and onnx_export._varint(300) == b"\xac\x02"
     assert onnx_export._varint(2 ** 63) == b"\x80" * 9 + b"\x01"
+
+
+def test_product_onnx_infer_matches_policy(trained):
+    """onnx_infer.OnnxInfer (the sim2sim loop's runtime: its own protobuf reader + numpy) runs the
+    exported file to the torch policy's deterministic action, awd=True feeding one observation."""
+    from open_duck_playground_amd.onnx_infer import OnnxInfer
+    net, path = trained
+    oi = OnnxInfer(path, awd=True)
+    rng = np.random.default_rng(2)
+    for _ in range(5):
+        obs = rng.normal(2.0, 3.0, size=101)
+        with torch.no_grad():
+            exp = ppo.NormalTanh(net.policy_logits(torch.tensor(obs[None], dtype=torch.float32))).mode().numpy()[0]
+        np.testing.assert_allclose(oi.infer(obs), exp, rtol=1e-5, atol=1e-5)
+    assert oi.graph.inputs == ["obs"] and oi.graph.outputs == ["continuous_actions"]
+
+
+def test_product_onnx_infer_rejects_unknown_ops(trained, tmp_path):
+    from open_duck_playground_amd import onnx_export as ox
+    from open_duck_playground_amd.onnx_infer import OnnxGraph
+    nodes = ox._bytes(1, ox.node("Softmax", ["obs"], ["y"], "sm"))
+    graph = nodes + ox._str(2, "g") + ox._bytes(11, ox.value_info("obs", [1, 3])) + ox._bytes(12, ox.value_info("y", [1, 3]))
+    g = OnnxGraph(ox._int(1, 6) + ox._bytes(7, graph))
+    with pytest.raises(NotImplementedError):
+        g.run({"obs": np.zeros((1, 3))})
