@@ -701,6 +701,113 @@ static void collide_hfield_convex(const oracle_model* m, oracle_data* d, int g1,
   }
 }
 
+/* Prism reference for the height field (measurement aid for DESIGN.md §5, tools/hfield_deviation.py;
+ * not used by oracle_forward). MuJoCo's height-field collision decomposes the field under a convex
+ * geom into triangular prisms (each grid cell's two triangles extruded down to the field's base,
+ * -size[3]) and collides every prism with the geom as a convex-convex pair. This restates that with
+ * an exact separating-axis test per prism (the hull's 30 face normals, the prism's 5, and every hull
+ * edge x prism edge direction), writing for each penetrating prism its depth, the unit normal that
+ * pushes the hull out (world frame) and the deepest hull vertex. Returns the number written. */
+static void sat_axis(const double* u, const double (*A)[3], int na, const double (*B)[3], int nb, double* ov,
+                     double* sgn) {
+  double amin = 1e30, amax = -1e30, bmin = 1e30, bmax = -1e30;
+  for (int i = 0; i < na; i++) { double t = dot3(u, A[i]); amin = fmin(amin, t); amax = fmax(amax, t); }
+  for (int i = 0; i < nb; i++) { double t = dot3(u, B[i]); bmin = fmin(bmin, t); bmax = fmax(bmax, t); }
+  double o1 = bmax - amin, o2 = amax - bmin; /* push A (hull) along +u by o1, or along -u by o2 */
+  if (o1 < o2) { *ov = o1; *sgn = 1; } else { *ov = o2; *sgn = -1; }
+}
+
+int oracle_hfield_prisms(const oracle_model* m, const oracle_data* d, int g_hf, int g_cvx, int max, double* depth,
+                         double* normal, double* point) {
+  if (!m->hfield_data) return 0;
+  const double *hp = d->geom_xpos[g_hf], *HR = d->geom_xmat[g_hf], *cp = d->geom_xpos[g_cvx], *CR = d->geom_xmat[g_cvx];
+  const int nv = m->hull_nvert, nf = m->hull_nface, ne = m->hull_nedge;
+  const int nr = m->hfield_nrow, nc = m->hfield_ncol;
+  const double sx = m->hfield_size[0], sy = m->hfield_size[1], sz = m->hfield_size[2], base = -m->hfield_size[3];
+  const double dx = 2.0 * sx / (nc - 1), dy = 2.0 * sy / (nr - 1);
+  /* hull in the height field's frame */
+  double V[DUCK_MAXHULLV][3], FN[DUCK_MAXHULLF][3], ED[DUCK_MAXHULLE][3], R[9];
+  for (int a = 0; a < 3; a++)
+    for (int b = 0; b < 3; b++) R[3 * a + b] = HR[0 * 3 + a] * CR[0 * 3 + b] + HR[1 * 3 + a] * CR[1 * 3 + b] + HR[2 * 3 + a] * CR[2 * 3 + b];
+  double off[3] = {cp[0] - hp[0], cp[1] - hp[1], cp[2] - hp[2]}, ol[3];
+  mulmtv3(ol, HR, off);
+  double xmin = 1e30, xmax = -1e30, ymin = 1e30, ymax = -1e30;
+  for (int k = 0; k < nv; k++) {
+    mulmv3(V[k], R, m->hull_vert[k]);
+    for (int a = 0; a < 3; a++) V[k][a] += ol[a];
+    xmin = fmin(xmin, V[k][0]); xmax = fmax(xmax, V[k][0]); ymin = fmin(ymin, V[k][1]); ymax = fmax(ymax, V[k][1]);
+  }
+  for (int f = 0; f < nf; f++) mulmv3(FN[f], R, m->hull_face_normal[f]);
+  for (int e = 0; e < ne; e++) {
+    double t[3];
+    for (int a = 0; a < 3; a++) t[a] = m->hull_vert[m->hull_edge[e][1]][a] - m->hull_vert[m->hull_edge[e][0]][a];
+    mulmv3(ED[e], R, t);
+  }
+  int c0 = (int)floor((xmin + sx) / dx), c1 = (int)floor((xmax + sx) / dx);
+  int r0 = (int)floor((ymin + sy) / dy), r1 = (int)floor((ymax + sy) / dy);
+  c0 = c0 < 0 ? 0 : c0; r0 = r0 < 0 ? 0 : r0; c1 = c1 > nc - 2 ? nc - 2 : c1; r1 = r1 > nr - 2 ? nr - 2 : r1;
+  int n = 0;
+  for (int r = r0; r <= r1; r++)
+    for (int c = c0; c <= c1; c++)
+      for (int tri = 0; tri < 2; tri++) {
+        /* the cell's triangles as hfield_point splits it: (00,10,11) where u >= w, (00,11,01) */
+        const int cc[2][3][2] = {{{0, 0}, {1, 0}, {1, 1}}, {{0, 0}, {1, 1}, {0, 1}}};
+        double P[6][3];
+        for (int k = 0; k < 3; k++) {
+          const int ci = c + cc[tri][k][0], ri = r + cc[tri][k][1];
+          P[k][0] = P[k + 3][0] = -sx + ci * dx;
+          P[k][1] = P[k + 3][1] = -sy + ri * dy;
+          P[k][2] = sz * m->hfield_data[ri * nc + ci];
+          P[k + 3][2] = base;
+        }
+        double axes[3 + DUCK_MAXHULLF + 5 + DUCK_MAXHULLE * 7][3];
+        int na = 0;
+        for (int f = 0; f < nf; f++) memcpy(axes[na++], FN[f], sizeof(double) * 3);
+        double e0[3], e1[3], top[3];
+        for (int a = 0; a < 3; a++) { e0[a] = P[1][a] - P[0][a]; e1[a] = P[2][a] - P[0][a]; }
+        cross3(top, e0, e1);
+        if (top[2] < 0) for (int a = 0; a < 3; a++) top[a] = -top[a];
+        memcpy(axes[na++], top, sizeof(top));
+        axes[na][0] = 0; axes[na][1] = 0; axes[na][2] = -1; na++;
+        double pe[7][3];
+        for (int k = 0; k < 3; k++) {
+          const double* a0 = P[k]; const double* a1 = P[(k + 1) % 3];
+          double hz[3] = {a1[0] - a0[0], a1[1] - a0[1], 0.0}, side[3], up[3] = {0, 0, 1};
+          cross3(side, hz, up); /* horizontal normal of the side face */
+          memcpy(axes[na++], side, sizeof(side));
+          for (int a = 0; a < 3; a++) pe[k][a] = a1[a] - a0[a];
+          memcpy(pe[3 + k], hz, sizeof(hz));
+        }
+        pe[6][0] = 0; pe[6][1] = 0; pe[6][2] = 1;
+        for (int e = 0; e < ne; e++)
+          for (int k = 0; k < 7; k++) {
+            double u[3];
+            cross3(u, ED[e], pe[k]);
+            if (norm3(u) > 1e-9 * norm3(ED[e]) * norm3(pe[k])) memcpy(axes[na++], u, sizeof(u));
+          }
+        double best = 1e30, bu[3] = {0, 0, 1};
+        int sep = 0;
+        for (int i = 0; i < na && !sep; i++) {
+          double u[3], nn = norm3(axes[i]), ov, sgn;
+          for (int a = 0; a < 3; a++) u[a] = axes[i][a] / nn;
+          sat_axis(u, (const double(*)[3])V, nv, (const double(*)[3])P, 6, &ov, &sgn);
+          if (ov < 0) sep = 1;
+          else if (ov < best) { best = ov; for (int a = 0; a < 3; a++) bu[a] = sgn * u[a]; }
+        }
+        if (sep || n >= max) continue;
+        int kd = 0;
+        for (int k = 1; k < nv; k++)
+          if (dot3(V[k], bu) < dot3(V[kd], bu)) kd = k;
+        depth[n] = best;
+        mulmv3(normal + 3 * n, HR, bu);
+        double pw[3];
+        mulmv3(pw, HR, V[kd]);
+        for (int a = 0; a < 3; a++) point[3 * n + a] = pw[a] + hp[a];
+        n++;
+      }
+  return n;
+}
+
 /* convex hull (g1) vs convex hull (g2): separating-axis test over face normals and edge
  * pairs; on overlap, a 4-point manifold against the reference face (or one edge-edge
  * point). Declared simplification of mjx's convex-convex clipping. */

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""How far the build's height-field contact model (collide_hfield_convex: each hull vertex against the
+terrain triangle under it, MJX's 4-slot plane manifold) is from MuJoCo's prism decomposition
+(oracle_hfield_prisms: every grid triangle under the foot extruded to the base, exact SAT per prism).
+
+Both are evaluated by the oracle on the same states: the final substep of env-steps of the rough
+scenes with domain randomisation (C4: rough_terrain, C5's shard: rough_terrain_backlash), random
+U(-1,1) actions. Per foot and env-step: contact flag (any penetration) of each model, the deepest
+penetration of each, and the angle between their deepest contacts' normals. CPU only.
+
+usage: python tools/hfield_deviation.py [n_envs] [n_steps]   (prints one JSON line per scene)
+"""
+
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from open_duck_playground_amd import constants  # noqa: E402
+from open_duck_playground_amd.config import default_config, env_config_struct  # noqa: E402
+from open_duck_playground_amd.mjcf import Model  # noqa: E402
+from tests.oracle_ffi import OracleData, OracleEnv, OracleModel, lib  # noqa: E402
+
+
+def prisms(om, d, g_hf, g_foot, max_n=64):
+    dep, nrm, pt = np.zeros(max_n), np.zeros(3 * max_n), np.zeros(3 * max_n)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    n = lib().oracle_hfield_prisms(om.ptr, C.byref(d), g_hf, g_foot, max_n, dp(dep), dp(nrm), dp(pt))
+    return dep[:n], nrm[:3 * n].reshape(n, 3)
+
+
+def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
+    m = Model.load(constants.task_to_xml(task))
+    base = OracleModel(m)
+    cfg = env_config_struct(m, default_config(), False, domain_randomize=True)
+    floor = m.id("geom", "floor")
+    pairs = {}
+    for foot in constants.FEET_GEOMS:
+        g = m.id("geom", foot)
+        p = [k for k in range(m.npair) if {int(m.pair_geom1[k]), int(m.pair_geom2[k])} == {floor, g}][0]
+        pairs[g] = p
+    rng = np.random.default_rng(seed)
+    rows = []
+    for e in range(n_envs):
+        om = OracleModel(m, dr=base.dr_sample(seed + 1, e))
+        env = OracleEnv(om, cfg)
+        env.reset(seed=seed, env_id=e)
+        d = OracleData()
+        for t in range(n_steps):
+            env.step(rng.uniform(-1, 1, m.nu), d)
+            for g, p in pairs.items():
+                dist = d.arr("con_dist", 4 * m.npair)[4 * p:4 * p + 4]
+                frames = np.ctypeslib.as_array(d.con_frame)[4 * p:4 * p + 4]
+                dep, nrm = prisms(om, d, floor, g)
+                ours = -dist.min()
+                ref = dep.max() if len(dep) else -1.0
+                ang = np.nan
+                if ours > 0 and ref > 0:
+                    n1 = frames[int(np.argmin(dist))][:3]
+                    n2 = nrm[int(np.argmax(dep))]
+                    ang = float(np.degrees(np.arccos(np.clip(n1 @ n2, -1, 1))))
+                rows.append((ours > 0, ref > 0, max(ours, 0.0), max(ref, 0.0), ang))
+    a = np.array(rows, dtype=float)
+    flag_o, flag_r, dep_o, dep_r, ang = a.T
+    both = (flag_o > 0) & (flag_r > 0)
+    dd = np.abs(dep_o - dep_r)[both]
+    return {"scene": task, "foot_samples": len(a), "contact_ours": int(flag_o.sum()), "contact_prism": int(flag_r.sum()),
+            "flag_agreement": float((flag_o == flag_r).mean()),
+            "flag_disagree_max_depth_m": float(np.max(np.maximum(dep_o, dep_r)[flag_o != flag_r], initial=0.0)),
+            "depth_abs_diff_m": {"median": float(np.median(dd)), "p99": float(np.quantile(dd, 0.99)), "max": float(dd.max())},
+            "depth_prism_median_m": float(np.median(dep_r[both])),
+            "normal_angle_deg": {"median": float(np.nanmedian(ang)), "p99": float(np.nanquantile(ang, 0.99)),
+                                 "max": float(np.nanmax(ang))}}
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    for task in ("rough_terrain", "rough_terrain_backlash"):
+        print(json.dumps(measure(task, n, steps)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
