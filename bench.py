@@ -17,7 +17,7 @@ Extra JSON objects:
                   x envs per launch / average launch time from HIP events on the launch stream.
   issue_roofline  the same kernel against the FP32 VALU issue rate (its real bound: one wave per
                   SIMD on a dependent chain), from the SQ counters of the committed rocprofv3 run
-                  of this library (profiles/, checked against the library's sha1).
+                  of this library (profiles/, checked against the library's build id).
   cpu_baseline    the fp64 C oracle (oracle/, a restatement of the same step) over OpenMP on the
                   host cores this job may use (affinity, capped by the cgroup CPU quota), on a
                   bounded sample (rank 0, N=1 only), plus BASELINE configs[0] (C1): 1 env, 1 core.
@@ -93,10 +93,10 @@ def host_cores() -> int:
     return n
 
 
-def lib_sha1() -> str:
-    import hashlib
-    from open_duck_playground_amd.native import LIB_PATH
-    return hashlib.sha1(open(LIB_PATH, "rb").read()).hexdigest()
+def build_id() -> str:
+    """sha1 of the sources + flags libduck.so was built from (duck_build_id, native.build)."""
+    from open_duck_playground_amd.native import lib
+    return lib().duck_build_id().decode()
 
 
 def cpu_baseline_c1(task: str, use_imitation: bool, budget_s: float):
@@ -240,8 +240,8 @@ def main():
     traffic, issue_rf = None, None
     if os.path.exists(PMC_PROFILE) and args.config == "C2" and n == CONFIGS["C2"]["envs"]:
         prof = json.load(open(PMC_PROFILE))
-        current = prof.get("lib_sha1") == lib_sha1()
-        src = {"source": os.path.relpath(PMC_PROFILE, ROOT), "lib_sha1_matches": current}
+        current = prof.get("build_id") == build_id()
+        src = {"source": os.path.relpath(PMC_PROFILE, ROOT), "build_id_matches": current}
         if current:
             traffic = prof["hbm_bytes_per_launch"]
         valu = prof["SQ_INSTS_VALU"] * 64 / (kern_ms * 1e-3) / 1e12     # lane-instructions / s

@@ -40,6 +40,8 @@ enum { DUCK_OK = 0, DUCK_EINVAL = -1, DUCK_EUNSUPPORTED = -2, DUCK_EHIP = -3 };
 
 /* library version (major*10000 + minor*100 + patch) */
 int duck_version(void);
+/* sha1 of the sources, headers and compile flags this library was built from */
+const char* duck_build_id(void);
 /* message of the last failing call on this thread ("" if none) */
 const char* duck_last_error(void);
 /* per-env state layout for a model/config/task (same as duck_layout_make) */

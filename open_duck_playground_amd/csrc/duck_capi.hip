@@ -84,6 +84,11 @@ uint64_t duck_model_fingerprint(const duck_model_desc* m) {
 
 int duck_version(void) { return DUCK_VERSION; }
 
+#ifndef DUCK_BUILD_ID
+#define DUCK_BUILD_ID "unknown"
+#endif
+const char* duck_build_id(void) { return DUCK_BUILD_ID; }
+
 int duck_model_supported(const duck_model_desc* model) {
   if (!model) return 0;
   for (int i = 0; i < kNumVariants; i++)

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(HERE)
 
 BUILD = os.path.join(HERE, "build")  # libraries compiled for other models (model_library)
 
-EXPORTS = ["duck_version", "duck_last_error", "duck_layout_get", "duck_aux_size", "duck_create", "duck_destroy",
+EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get", "duck_aux_size", "duck_create", "duck_destroy",
            "duck_debug_stage_cycles", "duck_model_fingerprint", "duck_model_supported",
            "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae"]
 
@@ -59,6 +59,7 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no
         [os.path.abspath(__file__)]  # the compile flags live here
     if not defines and not extra_flags and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
+    import hashlib
     import tempfile
     # fp32 division and sqrt as v_rcp/v_sqrt (1-2 ulp) instead of the correctly rounded
     # multi-instruction sequences: the physics tolerances are fp32-vs-fp64 anyway; fp32
@@ -76,6 +77,13 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no
     # gated by tools/isa_exec_check.py, which rejects the register-allocation fault that once made
     # the rough + backlash physics_kernel compute a wrong Newton step.
     ilp = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+    # build id: sha1 of every source, header and flag that shapes the code (duck_build_id()); the
+    # .so itself is not byte-reproducible (object paths), so profiles are keyed by this instead
+    h = hashlib.sha1(" ".join(flags + ilp + sorted(no_ilp)).encode())
+    for d in sorted(set(deps) - {os.path.abspath(__file__)}):
+        h.update(os.path.relpath(d, ROOT).encode())
+        h.update(open(d, "rb").read())
+    flags = flags + [f'-DDUCK_BUILD_ID="{h.hexdigest()}"']
     with tempfile.TemporaryDirectory() as tmp:
         objs, procs = [], []
         for src in srcs:
@@ -154,6 +162,7 @@ def lib(path: str = None):
         L = C.CDLL(path)
         vp = C.c_void_p
         L.duck_version.restype = C.c_int
+        L.duck_build_id.restype = C.c_char_p
         L.duck_last_error.restype = C.c_char_p
         L.duck_layout_get.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(DuckLayout)]
         L.duck_aux_size.argtypes = [vp]

@@ -162,7 +162,7 @@ def test_dr_layout():
 
 def test_product_fails_loudly_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(native, "LIB_PATH", str(tmp_path / "missing.so"))
-    monkeypatch.setattr(native, "_lib", None)
+    monkeypatch.setattr(native, "_libs", {})
     with pytest.raises(native.DuckError):
         native.lib()
 

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarise a tools/gpu_pmc.sh run: step_kernel's average duration (kernel trace), FETCH_SIZE /
-WRITE_SIZE and SQ counters per dispatch, and the library they were measured on (sha1).
+WRITE_SIZE and SQ counters per dispatch, and the library they were measured on (duck_build_id).
 
 usage: pmc_summary.py OUT_DIR TAG CONFIG   -> OUT_DIR/<TAG>_pmc_<config>.json, _stats.csv
 """
@@ -8,7 +8,6 @@ usage: pmc_summary.py OUT_DIR TAG CONFIG   -> OUT_DIR/<TAG>_pmc_<config>.json, _
 import collections
 import csv
 import glob
-import hashlib
 import json
 import os
 import shutil
@@ -36,9 +35,10 @@ def main():
     c = {}
     for d in ("fetch", "write", "sq1", "sq2"):
         c.update(counters(f"{out}/{d}"))
-    lib = os.path.join(ROOT, "open_duck_playground_amd", "libduck.so")
+    sys.path.insert(0, ROOT)
+    from open_duck_playground_amd.native import lib
     res = {
-        "config": cfg, "kernel": "step_kernel", "lib_sha1": hashlib.sha1(open(lib, "rb").read()).hexdigest(),
+        "config": cfg, "kernel": "step_kernel", "build_id": lib().duck_build_id().decode(),
         "kernel_avg_ns": avg_ns,
         "fetch_kb": c["FETCH_SIZE"], "write_kb": c["WRITE_SIZE"],
         "hbm_bytes_per_launch": (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0,
