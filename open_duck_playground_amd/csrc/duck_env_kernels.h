@@ -45,63 +45,28 @@ struct KArgs {
   duck_dr_layout drl;
 };
 
-// Launch geometry. Team mode (default): 16 lanes per env, 16 envs (4 waves) per workgroup,
-// so 4096 envs are exactly one workgroup per CU. Single-lane mode (-DDUCK_TEAM=0): one env
-// per lane, WG envs per workgroup, EPW envs per wave.
-#ifndef DUCK_TEAM
-#define DUCK_TEAM 1
-#endif
-#if DUCK_TEAM
+// Launch geometry: 16 lanes per env (a team), 16 envs (4 waves) per workgroup, so 4096 envs are
+// exactly one workgroup per CU.
 constexpr int WG = 16;
 constexpr int EPW = 4;
 constexpr int TPB = WG * TEAM;
 constexpr int SW = 1;  // slice stride (contiguous per-env slices)
-#else
-#ifndef DUCK_WG
-#define DUCK_WG 16
-#endif
-#ifndef DUCK_EPW
-#define DUCK_EPW DUCK_WG
-#endif
-constexpr int WG = DUCK_WG;
-constexpr int EPW = DUCK_EPW;
-static_assert(WG % EPW == 0 && EPW <= 64, "EPW must divide WG");
-constexpr int TPB = EPW >= WG ? WG : (WG / EPW) * 64;  // threads per block
-constexpr int SW = WG;  // slice stride (interleaved per-lane slices)
-#endif
 
 // this lane's env within the workgroup (-1: idle lane) and its rank in the env's team
 DK int local_env(int& lane) {
-#if DUCK_TEAM
   lane = threadIdx.x % TEAM;
   return threadIdx.x / TEAM;
-#else
-  lane = 0;
-  if (EPW >= WG) return threadIdx.x;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  return l < EPW ? w * EPW + l : -1;
-#endif
 }
 
 template <class Md>
 DK Slice<SW> env_slice(float* lds, int t) {
-#if DUCK_TEAM
   return Slice<SW>{(lds_float*)(lds + t * TLay<Md>::STRIDE)};
-#else
-  return Slice<SW>{(lds_float*)(lds + t)};
-#endif
 }
 
 template <class Md>
 DK void phys_step(Slice<SW> L, int lane, bool integrate, bool want_out, float* aux, int aux_stride, float* scratch,
                   int sstride, const float* hfield) {
-#if DUCK_TEAM
   TPhys<Md>::step(L.p, lane, integrate, want_out, aux, aux_stride, scratch, sstride, hfield);
-#else
-  static_assert(Md::FLOOR_TYPE == 0, "the single-lane build supports plane floors only");
-  (void)hfield;
-  Phys<Md, WG>::step(L, integrate, want_out, aux, aux_stride, scratch, sstride);
-#endif
 }
 
 // the physics_kernel (mjx_env.step / mjx.forward parity entry) runs its substeps through one
@@ -197,7 +162,6 @@ DK void load_dyn(const KArgs& A, int e, Slice<WG> L) {
   }
 }
 
-#if DUCK_TEAM
 // load_dyn with the team's lanes: nominal block from the LDS model blob, then the env's DR record
 template <class Md>
 DK void load_dyn_team(const KArgs& A, int e, Slice<SW> L, int lane) {
@@ -221,7 +185,6 @@ DK void load_dyn_team(const KArgs& A, int e, Slice<SW> L, int lane) {
     }
   }
 }
-#endif
 
 // Joystick._get_obs (joystick.py:487-620) / Standing._get_obs (standing.py:462-575); reads the
 // last forward's outputs from the slice
@@ -334,7 +297,6 @@ DK void write_obs(const KArgs& A, int e, Slice<WG> L, const FA& F, const OS& out
   }
 }
 
-#if DUCK_TEAM
 // write_obs with the team's lanes splitting the rows (step_kernel): lane a < NU takes actuator
 // a's entries, lanes 0-2 the 3-vectors, lanes 0-1 the pairs; same values at the same offsets
 template <class Md, class FA, class OS, class RT>
@@ -407,17 +369,14 @@ DK void write_obs_team(const KArgs& A, int lane, Slice<SW> L, const FA& F, const
   if (Lo.imitation)
     for (int k = lane; k < 40; k += TEAM) out(PR + k, F[Lo.ref_motion + k]);
 }
-#endif
 
 template <class Md, int WG>
 __global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
   using Ly = Lay<Md>;
-#if DUCK_TEAM
   {
     extern __shared__ float lds_t[];
     load_model_tables<Md>(lds_t);
   }
-#endif
   int lane;
   const int t = local_env(lane);
   if (t < 0) return;
@@ -767,12 +726,10 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
 #ifdef DUCK_ANY_PROF
   const unsigned long long kstart = clock64();
 #endif
-#if DUCK_TEAM
   {
     extern __shared__ float lds_t[];
     load_model_tables<Md>(lds_t);
   }
-#endif
   STAGE_MARK(14);
   int lane;
   const int t = local_env(lane);
@@ -780,7 +737,6 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   const int e = blockIdx.x * WG + t;
   const int n = A.n;
   extern __shared__ float lds[];
-#if DUCK_TEAM
   using TL = TLay<Md>;
   if constexpr (TL::ES_LDS) {
     // hot state <-> LDS by the whole workgroup, field-major: a wave instruction moves 4 fields
@@ -819,17 +775,6 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
     r.ctr = (uint32_t)A.is[(size_t)Lo.rng_ctr * n + e];
     step_env<Md, Col<0>, true>(A, e, lane, L, G, G, r);
   }
-#else
-  if (e >= n) return;
-  const Slice<SW> L = env_slice<Md>(lds, t);
-  const Col<0> G{A.fs + e, n};
-  const duck_layout& Lo = A.lay;
-  Rng r;
-  r.k0 = (uint32_t)A.is[(size_t)Lo.rng_key * n + e];
-  r.k1 = (uint32_t)A.is[(size_t)(Lo.rng_key + 1) * n + e];
-  r.ctr = (uint32_t)A.is[(size_t)Lo.rng_ctr * n + e];
-  step_env<Md, Col<0>, false>(A, e, lane, L, G, G, r);
-#endif
   STAGE_MARK(15);
 #ifdef DUCK_ANY_PROF
   if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_stage_cycles[32 + 4 * blockIdx.x + threadIdx.x / 64] = clock64() - kstart;
@@ -840,12 +785,10 @@ template <class Md, int WG>
 __global__ void __launch_bounds__(TPB) physics_kernel(KArgs A, float* qpos_g, float* qvel_g, float* warm_g,
                                                      const float* ctrl_g, int nsub, float* aux) {
   using Ly = Lay<Md>;
-#if DUCK_TEAM
   {
     extern __shared__ float lds_t[];
     load_model_tables<Md>(lds_t);
   }
-#endif
   int lane;
   const int t = local_env(lane);
   if (t < 0) return;
@@ -908,12 +851,8 @@ static bool matches(const duck_model_desc* m) {
 
 template <class Md>
 static size_t lds_bytes() {
-#if DUCK_TEAM
   static_assert(WG == TEAM_WG, "team workgroup size");
   return (size_t)TLay<Md>::LDS_FLOATS * sizeof(float);
-#else
-  return (size_t)Lay<Md>::TOTAL * WG * sizeof(float);
-#endif
 }
 
 template <class Md>
@@ -952,9 +891,7 @@ static int launch_step(duck_sim* s, int n, float* fs, int32_t* is, const float* 
   KArgs A = make_args(s, n);
   A.fs = fs; A.is = is; A.dr = dr; A.action = action; A.obs = obs; A.priv = priv;
   A.reward = reward; A.done = done; A.scratch = scratch;
-#if DUCK_TEAM
   if (s->lay.first_qpos != TLay<Md>::HOT) return duck_fail(DUCK_EINVAL, "state layout does not match the kernel's hot-state size");
-#endif
   const dim3 grid((A.n + WG - 1) / WG), block(TPB);
   hipLaunchKernelGGL((step_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A);
   HIPCHECK(hipGetLastError());
