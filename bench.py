@@ -233,6 +233,7 @@ def main():
         thr = args.cpu_threads or host_cores()
         cpu = cpu_baseline(cfg["task"], cfg["imitation"], args.cpu_budget, thr)
         cpu["host_cores"] = host_cores()
+        cpu["affinity_cpus"] = len(os.sched_getaffinity(0))
         cpu["c1"] = cpu_baseline_c1(cfg["task"], cfg["imitation"], min(5.0, args.cpu_budget))
 
     # PMC numbers of the committed rocprofv3 run of this configuration (tools/gpu_pmc.sh); valid

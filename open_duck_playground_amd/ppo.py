@@ -34,7 +34,10 @@ import torch.nn.functional as F
 
 @dataclass
 class PPOConfig:
-    """brax_ppo_config("BerkeleyHumanoidJoystickFlatTerrain") as the reference runner uses it."""
+    """brax_ppo_config("BerkeleyHumanoidJoystickFlatTerrain") as the reference runner uses it
+    (common/runner.py:86-89; num_timesteps from open_duck_mini_v2/runner.py:44). The values come from
+    mujoco_playground's locomotion_params, an upstream dependency the reference does not vendor and
+    whose version is unpinned (pyproject.toml: playground>=0.0.3): restated, not pinned."""
     num_timesteps: int = 150_000_000     # open_duck_mini_v2/runner.py:44
     num_evals: int = 15
     reward_scaling: float = 1.0
