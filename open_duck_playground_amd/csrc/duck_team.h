@@ -100,6 +100,10 @@ DK int hmin8i(int v) {
   return v;
 }
 
+#ifndef DUCK_LS_DFLOOR
+#define DUCK_LS_DFLOOR 1e-6f
+#endif
+
 template <class Md>
 struct TLay {
   using Ly = Lay<Md>;
@@ -2072,19 +2076,23 @@ struct TPhys {
     Pt hi;
     if (lo.d0 < p0.d0) { hi = p0; } else { hi = lo; lo = p0; }
     bool swap = true;
+    // fp32 termination floor: a bracket end whose slope is below 1e-6 of the starting slope is at the
+    // minimum to fp32 resolution; MJX's gtol (tolerance * ls_tolerance * |search| ...) alone is far
+    // below fp32 noise, so fp32 iterations would keep swapping on rounding
+    const float gtol_ls = fmaxf(gtol, DUCK_LS_DFLOOR * fabsf(p0.d0));
 #ifdef DUCK_LS_NOBREAK
     bool stop = false;
 #pragma unroll
     for (int it = 0; it < Md::ls_iterations; it++) {
       bool done = stop || !swap;
-      done = done || ((lo.d0 < 0.0f) && (lo.d0 > -gtol));
-      done = done || ((hi.d0 > 0.0f) && (hi.d0 < gtol));
+      done = done || ((lo.d0 < 0.0f) && (lo.d0 > -gtol_ls));
+      done = done || ((hi.d0 > 0.0f) && (hi.d0 < gtol_ls));
       stop = done;
 #else
     for (int it = 0; it < Md::ls_iterations; it++) {
       bool done = !swap;
-      done = done || ((lo.d0 < 0.0f) && (lo.d0 > -gtol));
-      done = done || ((hi.d0 > 0.0f) && (hi.d0 < gtol));
+      done = done || ((lo.d0 < 0.0f) && (lo.d0 > -gtol_ls));
+      done = done || ((hi.d0 > 0.0f) && (hi.d0 < gtol_ls));
       if (done) break;
 #endif
       const float al = lo.alpha - lo.d0 / lo.d1, ah = hi.alpha - hi.d0 / hi.d1, am = 0.5f * (lo.alpha + hi.alpha);
