@@ -700,14 +700,43 @@ struct TPhys {
     for (int s = 0; s < NC; s++)
       if (TEAM * s < K) x[s] -= F.col[s][K] * xk;
   }
+  // lanes holding the ancestors of dof K (bit l: some column c = TEAM s + l is an ancestor of K): the
+  // only nonzeros of row K of the tree-sparse factor (the dense factor uses sol_fwd_dense)
+  static constexpr unsigned anc_lanes(int K) {
+    unsigned m = 0;
+    for (int j = Md::dof_parentid[K]; j >= 0; j = Md::dof_parentid[j]) m |= 1u << (j % TEAM);
+    return m;
+  }
+  // sum of v over the lanes in `lanes`, delivered (at least) to lane `dst`: one row broadcast for a
+  // single lane, a quad (2 steps) or 8-lane half (3 steps) when lanes and dst share it, else the team sum
+  template <unsigned LANES, int DST>
+  static DK float anc_sum(float v) {
+    constexpr unsigned all = LANES | (1u << DST);
+    if constexpr (LANES == 0) {
+      return 0.0f;
+    } else if constexpr ((LANES & (LANES - 1)) == 0) {
+      return bc<__builtin_ctz(LANES)>(v);
+    } else if constexpr ((all & ~(0xFu << (4 * (DST / 4)))) == 0) {
+      v += dppf<0xB1>(v);  // quad_perm [1,0,3,2]
+      v += dppf<0x4E>(v);  // quad_perm [2,3,0,1]
+      return v;
+    } else if constexpr ((all & ~(0xFFu << (8 * (DST / 8)))) == 0) {
+      return hsum8(v);
+    } else {
+      return tsum(v);
+    }
+  }
   template <int K>
   static DK void sol_fwd(const Fac& F, float* x, int lane) {
-    float p = 0.0f;
+    constexpr unsigned A = anc_lanes(K);
+    if constexpr (A != 0) {
+      float p = 0.0f;
 #pragma unroll
-    for (int s = 0; s < NC; s++)
-      if (TEAM * s < K) p += F.col[s][K] * x[s];
-    p = tsum(p);
-    if (lane == K % TEAM) x[K / TEAM] -= p;
+      for (int s = 0; s < NC; s++)
+        if (TEAM * s < K) p += F.col[s][K] * x[s];
+      p = anc_sum<A, K % TEAM>(p);
+      if (lane == K % TEAM) x[K / TEAM] -= p;
+    }
   }
   template <int... J>
   static DK void fac_all(Fac& F, int lane, std::integer_sequence<int, J...>) {
@@ -777,9 +806,19 @@ struct TPhys {
   static DK void back_all_dense(const Fac& F, float* x, std::integer_sequence<int, J...>) {
     (sol_back<NV - 1 - J>(F, x), ...);
   }
+  // the dense factor has a full lower triangle: every row's dot product needs the whole team sum
+  template <int K>
+  static DK void sol_fwd_dense(const Fac& F, float* x, int lane) {
+    float p = 0.0f;
+#pragma unroll
+    for (int s = 0; s < NC; s++)
+      if (TEAM * s < K) p += F.col[s][K] * x[s];
+    p = tsum(p);
+    if (lane == K % TEAM) x[K / TEAM] -= p;
+  }
   template <int... J>
   static DK void fwd_all_dense(const Fac& F, float* x, int lane, std::integer_sequence<int, J...>) {
-    (sol_fwd<J>(F, x, lane), ...);
+    (sol_fwd_dense<J>(F, x, lane), ...);
   }
   static DK void factor_solve_dense(Fac& F, float* x, int lane) {
 #pragma unroll

@@ -5,7 +5,7 @@ set -e
 REV=${1:-HEAD}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 TMP=$(mktemp -d)
-git -C "$ROOT" archive "$REV" open_duck_playground_amd include | tar -x -C "$TMP"
+git -C "$ROOT" archive "$REV" open_duck_playground_amd include tools | tar -x -C "$TMP"
 (cd "$TMP" && python -c "
 from open_duck_playground_amd import native
 native.build(out='$ROOT/open_duck_playground_amd/libduck_A.so')
