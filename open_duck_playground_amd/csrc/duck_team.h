@@ -1803,57 +1803,11 @@ struct TPhys {
     return q <= k ? (q * 6 - (q * (q - 1)) / 2 + (k - q)) : (k * 6 - (k * (k - 1)) / 2 + (q - k));
   }
 
-  struct Pt { float alpha, cost, d0, d1; };
+  // a line-search point: alpha, the team-summed linear and quadratic coefficients, the slope and
+  // curvature, and this lane's un-summed constant coefficient (the cost is only needed for the final
+  // bracket ends, so its team sum is deferred to them)
+  struct Pt { float alpha, q0p, q1, q2, d0, d1; };
 
-  // line-search rows held in registers: one friction row and up to RQ one-sided rows per lane
-  static constexpr int RQ = (NROW - R_LIM + TEAM - 1) / TEAM;
-  struct Rows {
-    float fD, fja, fv, ff;
-    float D[RQ], ja[RQ], v[RQ];
-  };
-
-  static DK void load_rows(LP L, int lane, Rows& R) {
-    const bool fr = lane < NFRIC;
-    R.fD = fr ? L[Ly::RD + lane] : 0.0f;
-    R.fja = fr ? L[Ly::JA + lane] : 0.0f;
-    R.fv = fr ? L[Ly::JV + lane] : 0.0f;
-    R.ff = fr ? L[Ly::DFRIC + fric_dof(lane)] : 0.0f;
-    for (int m = 0; m < RQ; m++) {
-      const int r = R_LIM + lane + TEAM * m;
-      const bool ok = r < NROW;
-      R.D[m] = ok ? L[Ly::RD + r] : 0.0f;
-      R.ja[m] = ok ? L[Ly::JA + r] : 0.0f;
-      R.v[m] = ok ? L[Ly::JV + r] : 0.0f;
-    }
-  }
-
-  // partial quadratic coefficients of this lane's rows at alpha
-  static DK void row_quad(const Rows& R, int lane, float alpha, float& q0, float& q1, float& q2) {
-    if (lane < NFRIC) {
-      const float D = R.fD, ja = R.fja, v = R.fv, f = R.ff;
-      const float rf = f / D, x = ja + alpha * v;
-      if (x <= -rf) { q0 += -0.5f * rf * f - f * ja; q1 += -f * v; }
-      else if (x >= rf) { q0 += -0.5f * rf * f + f * ja; q1 += f * v; }
-      else { q0 += 0.5f * D * ja * ja; q1 += D * v * ja; q2 += 0.5f * D * v * v; }
-    }
-    for (int m = 0; m < RQ; m++) {
-      const float D = R.D[m], ja = R.ja[m], v = R.v[m];
-      const float x = ja + alpha * v;
-      if (x < 0.0f) { q0 += 0.5f * D * ja * ja; q1 += D * v * ja; q2 += 0.5f * D * v * v; }
-    }
-  }
-
-  static DK Pt eval1(const Rows& R, int lane, float g0, float g1, float g2, float alpha) {
-    float q0 = 0.0f, q1 = 0.0f, q2 = 0.0f;
-    row_quad(R, lane, alpha, q0, q1, q2);
-    q0 = tsum(q0) + g0; q1 = tsum(q1) + g1; q2 = tsum(q2) + g2;
-    Pt p;
-    p.alpha = alpha;
-    p.cost = alpha * alpha * q2 + alpha * q1 + q0;
-    p.d0 = 2.0f * alpha * q2 + q1;
-    p.d1 = 2.0f * q2;
-    return p;
-  }
 
   // ---- fused solver passes ----
   // foot spatial motions of X (and X2) into TSP[0..11] (and TSP[12..23]); Y = M X (and Y2 = M X2)
@@ -2086,14 +2040,17 @@ struct TPhys {
     const float gtol = Md::tolerance * Md::ls_tolerance * sqrtf(sn) * Md::meaninertia * (float)(NV > 1 ? NV : 1);
     const float G0 = g0, G1 = sMa - sf, G2 = 0.5f * sMv;
     auto mk = [&](float alpha, float q0, float q1, float q2) {
-      q0 = tsum(q0) + G0; q1 = tsum(q1) + G1; q2 = tsum(q2) + G2;
+      q1 = tsum(q1) + G1; q2 = tsum(q2) + G2;
       Pt p;
       p.alpha = alpha;
-      p.cost = alpha * alpha * q2 + alpha * q1 + q0;
+      p.q0p = q0;
+      p.q1 = q1;
+      p.q2 = q2;
       p.d0 = 2.0f * alpha * q2 + q1;
       p.d1 = 2.0f * q2;
       return p;
     };
+    auto cost = [&](const Pt& p) { return p.alpha * p.alpha * p.q2 + p.alpha * p.q1 + (tsum(p.q0p) + G0); };
     Pt p0;
     {
       float q0 = 0, q1 = 0, q2 = 0;
@@ -2162,8 +2119,9 @@ struct TPhys {
       swap = s1 || s2 || s3 || s4;
 #endif
     }
-    const bool improved = (lo.cost < p0.cost) || (hi.cost < p0.cost);
-    const float alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+    const float lo_cost = cost(lo), hi_cost = cost(hi), p0_cost = cost(p0);
+    const bool improved = (lo_cost < p0_cost) || (hi_cost < p0_cost);
+    const float alpha = lo_cost < hi_cost ? lo.alpha : hi.alpha;
     if (improved)
       for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] += L[Ly::SRCH + i] * alpha;
     TSYNC();
@@ -2177,7 +2135,7 @@ struct TPhys {
       // change is below fp32 resolution)
       if (++newton_it >= Md::iterations) break;
       const float a = improved ? alpha : 0.0f;
-      const float cnew = improved ? (lo.cost < hi.cost ? lo.cost : hi.cost) : p0.cost;
+      const float cnew = improved ? (lo_cost < hi_cost ? lo_cost : hi_cost) : p0_cost;
       g0 = G0 + a * G1 + a * a * G2;  // gauss at the new point
       for (int i = lane; i < NV; i += TEAM) L[Ly::MA + i] += a * L[Ly::GRAD + i];  // GRAD = M.search
       if (lane < NFRIC) L[Ly::JA + lane] = R.fja + a * R.fv;
@@ -2190,7 +2148,7 @@ struct TPhys {
         for (int e = 0; e < 4; e++) L[Ly::JA + R_CON + 4 * lane + e] = R.ja[NLR + e] + a * R.v[NLR + e];
       TSYNC();
       const float scale = 1.0f / (Md::meaninertia * (float)(NV > 1 ? NV : 1));
-      if (scale * (p0.cost - cnew) < Md::tolerance) break;
+      if (scale * (p0_cost - cnew) < Md::tolerance) break;
     }
     }
   }
