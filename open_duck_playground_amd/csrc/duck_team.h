@@ -440,7 +440,8 @@ struct TPhys {
         for (int jj = 0; jj < MD; jj++) {
           const int i = dof[d][jj] >= 0 ? dof[d][jj] : 0;
           for (int k = 0; k < 6; k++) cd[d][jj][k] = L[Ly::CDOF + 6 * i + k];
-          qv[d][jj] = dof[d][jj] >= 0 ? L[Ly::QVEL + i] : 0.0f;
+          const float q = L[Ly::QVEL + i];  // unconditional load, then select (no masked load)
+          qv[d][jj] = dof[d][jj] >= 0 ? q : 0.0f;
         }
 #pragma unroll
       for (int d = 0; d < BL; d++) {
@@ -1639,165 +1640,6 @@ struct TPhys {
   }
 
   // ---------------- Newton solver pieces ----------------
-  // J.x for all rows -> DST (x at X); sub_aref: DST = J.x - aref
-  static DK void jmul(LP L, int lane, int X, int DST, bool sub_aref) {
-    // foot spatial motions: lanes 0-5 left, 6-11 right
-    if (lane < 12) {
-      const int b = lane < 6 ? Md::LFOOT_BODY : Md::RFOOT_BODY, k = lane < 6 ? lane : lane - 6;
-      const int cb = lane < 6 ? Md::B_CHAINL : Md::B_CHAINR;
-      float s = 0.0f;
-      for (int c = 0; c < Md::MAXCHAIN; c++) {
-        const int i = ti(cb + c);
-        const int ic = i >= 0 ? i : 0;
-        const float t = L[Ly::CDOF + 6 * ic + k] * L[X + ic];
-        s += i >= 0 ? t : 0.0f;
-      }
-      L[TL::TSP + lane] = s;
-    }
-    if (lane < NFRIC) {
-      const int r = lane;
-      L[DST + r] = L[X + fric_dof(r)] - (sub_aref ? L[Ly::AREF + r] : 0.0f);
-    }
-    for (int r = lane; r < NLIM; r += TEAM)
-      L[DST + R_LIM + r] = L[Ly::LSGN + r] * L[X + lim_dof(r)] -
-                           (sub_aref ? L[Ly::AREF + R_LIM + r] : 0.0f);
-    TSYNC();
-    if (lane < NCON) {
-      float SL[6], SR[6], v[4];
-      for (int k = 0; k < 6; k++) { SL[k] = L[TL::TSP + k]; SR[k] = L[TL::TSP + 6 + k]; }
-      contact_jx(L, lane >> 2, lane, SL, SR, v);
-      for (int e = 0; e < 4; e++) {
-        const int row = R_CON + 4 * lane + e;
-        L[DST + row] = v[e] - (sub_aref ? L[Ly::AREF + row] : 0.0f);
-      }
-    }
-    TSYNC();
-  }
-
-  // Y = M X (sparse symmetric)
-  static DK void mul_M(LP L, int lane, int X, int Y) {
-    for (int i = lane; i < NV; i += TEAM) {
-      float acc = 0.0f;
-      for (int j = 0; j < NV; j++) {
-        const int a = madr(i, j);
-        const float t = L[Ly::M + (a >= 0 ? a : 0)] * L[X + j];
-        acc += a >= 0 ? t : 0.0f;
-      }
-      L[Y + i] = acc;
-    }
-    TSYNC();
-  }
-
-  static DK float gauss(LP L, int lane, int X, int MX) {
-    float g = 0.0f;
-    for (int i = lane; i < NV; i += TEAM) g += 0.5f * (L[MX + i] - L[Ly::FSM + i]) * (L[X + i] - L[Ly::QSM + i]);
-    return tsum(g);
-  }
-
-  // constraint cost of all rows for Jaref at JA
-  static DK float cost_rows(LP L, int lane) {
-    float cost = 0.0f;
-    if (lane < NFRIC) {
-      const int r = lane;
-      const float D = L[Ly::RD + r], x = L[Ly::JA + r], f = L[Ly::DFRIC + fric_dof(r)];
-      const float rf = f * frcp(D);
-      cost += x <= -rf ? (-f * x - 0.5f * rf * f) : (x >= rf ? (f * x - 0.5f * rf * f) : 0.5f * D * x * x);
-    }
-    for (int r = R_LIM + lane; r < NROW; r += TEAM) {
-      const float D = L[Ly::RD + r], x = L[Ly::JA + r];
-      cost += x < 0.0f ? 0.5f * D * x * x : 0.0f;
-    }
-    return tsum(cost);
-  }
-
-  // gradient and H = M + J' D J at JA; SRCH = -H^-1 grad. Returns false when the
-  // foot/foot rows are active (the caller takes the single-lane dense path).
-  static DK bool newton_direction(LP L, int lane) {
-    for (int i = lane; i < NV; i += TEAM) L[Ly::GRAD + i] = L[Ly::MA + i] - L[Ly::FSM + i];
-    for (int k = lane; k < Md::NM; k += TEAM) L[Ly::H + k] = L[Ly::M + k];
-    TSYNC();
-    if (lane < NFRIC) {
-      const int r = lane, i = fric_dof(r);
-      const float D = L[Ly::RD + r], x = L[Ly::JA + r], f = L[Ly::DFRIC + i], rf = f / D;
-      const float force = x <= -rf ? f : (x >= rf ? -f : -D * x);
-      L[Ly::GRAD + i] -= force;
-      if (x > -rf && x < rf) L[Ly::H + diag_adr(i)] += D;
-    }
-    TSYNC();
-    for (int r = lane; r < NLIM; r += TEAM) {
-      const int i = lim_dof(r);
-      const float D = L[Ly::RD + R_LIM + r], x = L[Ly::JA + R_LIM + r];
-      if (x < 0.0f) {
-        L[Ly::GRAD + i] -= L[Ly::LSGN + r] * (-D * x);
-        L[Ly::H + diag_adr(i)] += D;
-      }
-    }
-    TSYNC();
-    // contact rows: lane = slot-in-pair * 4 + edge; pair p rows R_CON + 16p + lane
-    bool ff = false;
-    if (Md::FOOT_PAIR >= 0) {
-      const int row = R_CON + 16 * Md::FOOT_PAIR + lane;
-      const float act = (L[Ly::JA + row] < 0.0f && L[Ly::RD + row] != 0.0f) ? 1.0f : 0.0f;
-      ff = tsum(act) > 0.0f;
-    }
-    if (ff) return false;
-    for (int side = 0; side < 2; side++) {
-      const int p = Md::PLANE_PAIR[side];
-      const int foot = cgeom_slot<Md>(Md::pair_geom2[p]);  // 1 left, 2 right
-      const int b = foot == 1 ? Md::LFOOT_BODY : Md::RFOOT_BODY;
-      const float mu = Md::pair_friction[p][0];
-      const int slot = 4 * p + (lane >> 2), e = lane & 3, row = R_CON + 4 * slot + e;
-      const float D = L[Ly::RD + row], x = L[Ly::JA + row];
-      const float w = (x < 0.0f && D != 0.0f) ? D : 0.0f;
-      const float force = -w * x;
-      const int t = 1 + (e >> 1);
-      const float sg = (e & 1) ? -mu : mu;
-      float u[3], r[3], a[6];
-      for (int q = 0; q < 3; q++) {
-        u[q] = L[Ly::CFR + 9 * slot + q] + sg * L[Ly::CFR + 9 * slot + 3 * t + q];
-        r[q] = L[Ly::CR + 3 * slot + q];
-      }
-      cross3(a, r, u);
-      a[3] = u[0]; a[4] = u[1]; a[5] = u[2];
-      float K[21], F[6];
-      {
-        int o = 0;
-        for (int q = 0; q < 6; q++)
-          for (int kk = q; kk < 6; kk++) { K[o] = tsum(w * a[q] * a[kk]); o++; }
-        for (int q = 0; q < 6; q++) F[q] = tsum(force * a[q]);
-      }
-      // K.cdof_j and the gradient for the chain dofs (lane = chain position)
-      const int cb = foot == 1 ? Md::B_CHAINL : Md::B_CHAINR;
-      const int jl = lane < Md::MAXCHAIN ? ti(cb + lane) : -1;
-      if (jl >= 0) {
-        float cdj[6];
-        for (int k = 0; k < 6; k++) cdj[k] = L[Ly::CDOF + 6 * jl + k];
-        float g = 0.0f;
-        for (int q = 0; q < 6; q++) {
-          float s = 0.0f;
-          for (int k = 0; k < 6; k++) s += K[kidx(q, k)] * cdj[k];
-          L[TL::KC + 6 * lane + q] = s;
-          g += cdj[q] * F[q];
-        }
-        L[Ly::GRAD + jl] -= g;
-      }
-      TSYNC();
-      // H[i][j] += cdof_i . (K cdof_j) for chain pairs; lane = row position ci
-      if (jl >= 0) {
-        float cdi[6];
-        for (int k = 0; k < 6; k++) cdi[k] = L[Ly::CDOF + 6 * jl + k];
-        for (int cj = 0; cj <= lane; cj++) {
-          const int j = ti(cb + cj);
-          float s = 0.0f;
-          for (int k = 0; k < 6; k++) s += cdi[k] * L[TL::KC + 6 * cj + k];
-          L[Ly::H + madr(jl, j)] += s;
-        }
-      }
-      TSYNC();
-    }
-    return true;
-  }
-
   static DK constexpr int kidx(int q, int k) {
     // packed upper-triangular index of (min(q,k), max(q,k)) in a 6x6 symmetric block
     return q <= k ? (q * 6 - (q * (q - 1)) / 2 + (k - q)) : (k * 6 - (k * (k - 1)) / 2 + (q - k));
@@ -1808,54 +1650,33 @@ struct TPhys {
   // bracket ends, so its team sum is deferred to them)
   struct Pt { float alpha, q0p, q1, q2, d0, d1; };
 
-
   // ---- fused solver passes ----
-  // foot spatial motions of X (and X2) into TSP[0..11] (and TSP[12..23]); Y = M X (and Y2 = M X2)
   // foot spatial motions only (lanes 0-11): X into TSP[0..11], X2 (if >= 0) into TSP[12..23]
   static DK void spatial2(LP L, int lane, int X, int X2) {
     if (lane < 12) {
-      const int k = lane < 6 ? lane : lane - 6;
-      const int cb = lane < 6 ? Md::B_CHAINL : Md::B_CHAINR;
+      // the feet's dof chains are compile-time (Md::chain): at each chain position the lane only
+      // selects the left or right foot's dof, so no index words are loaded and the products of
+      // all positions issue back to back. The lane is made opaque here: otherwise those per-lane
+      // selects are hoisted out of the substep loop and held in registers for the whole kernel
+      // (+15 AGPRs, -1.6 % same-box)
+      int lo = lane;
+      asm volatile("" : "+v"(lo));
+      const bool left = lo < 6;
+      const int k = left ? lo : lo - 6;
       float s = 0.0f, s2 = 0.0f;
 #pragma unroll
       for (int c = 0; c < Md::MAXCHAIN; c++) {
-        const int i = ti(cb + c), ic = i >= 0 ? i : 0;
-        const float cd = i >= 0 ? L[Ly::CDOF + 6 * ic + k] : 0.0f;
+        const int iL = Md::chain[Md::LFOOT_BODY][c], iR = Md::chain[Md::RFOOT_BODY][c];
+        if (iL < 0 && iR < 0) continue;
+        const bool ok = left ? iL >= 0 : iR >= 0;
+        const int ic = left ? (iL >= 0 ? iL : 0) : (iR >= 0 ? iR : 0);
+        const float cv = L[Ly::CDOF + 6 * ic + k];
+        const float cd = ok ? cv : 0.0f;
         s += cd * L[X + ic];
         if (X2 >= 0) s2 += cd * L[X2 + ic];
       }
       L[TL::TSP + lane] = s;
       if (X2 >= 0) L[TL::TSP + 12 + lane] = s2;
-    }
-  }
-
-  static DK void spatial_and_M(LP L, int lane, int X, int Y, int X2, int Y2) {
-    if (lane < 12) {
-      const int b = lane < 6 ? Md::LFOOT_BODY : Md::RFOOT_BODY, k = lane < 6 ? lane : lane - 6;
-      const int cb = lane < 6 ? Md::B_CHAINL : Md::B_CHAINR;
-      float s = 0.0f, s2 = 0.0f;
-#pragma unroll
-      for (int c = 0; c < Md::MAXCHAIN; c++) {
-        const int i = ti(cb + c), ic = i >= 0 ? i : 0;
-        const float cd = i >= 0 ? L[Ly::CDOF + 6 * ic + k] : 0.0f;
-        s += cd * L[X + ic];
-        if (X2 >= 0) s2 += cd * L[X2 + ic];
-      }
-      L[TL::TSP + lane] = s;
-      if (X2 >= 0) L[TL::TSP + 12 + lane] = s2;
-    }
-    for (int i = lane; i < NV; i += TEAM) {
-      float acc = 0.0f, acc2 = 0.0f;
-#pragma unroll
-      for (int j = 0; j < NV; j++) {
-        const int a = madr(i, j);
-        const float mv = L[Ly::M + (a >= 0 ? a : 0)];
-        const float m = a >= 0 ? mv : 0.0f;
-        acc += m * L[X + j];
-        if (X2 >= 0) acc2 += m * L[X2 + j];
-      }
-      L[Y + i] = acc;
-      if (X2 >= 0) L[Y2 + i] = acc2;
     }
   }
 
@@ -1911,11 +1732,13 @@ struct TPhys {
     // M as full symmetric columns in registers for every M.x of the solver
     float Mc[NC][NV];
     load_cols(L, lane, Ly::M, Mc, false);
+    STAGE_MARK(20);
     // warm start vs smooth acceleration: J and M products of both in one pass
     // (M qacc_smooth = qfrc_smooth by definition: no product needed for the smooth start)
     spatial2(L, lane, Ly::WARM, Ly::QSM);
     mul_cols(L, lane, Mc, Ly::WARM, Ly::MA);
     TSYNC();
+    STAGE_MARK(25);
     float cwp = 0.0f, csp = 0.0f, gwp = 0.0f;
     {
       // branchless (no lane-divergent region: see TL::SINK)
@@ -2012,7 +1835,8 @@ struct TPhys {
       for (int e = 0; e < 4; e++) {
         const int row = R_CON + 4 * slot + e;
         const bool ok = lane < NCON;
-        set_row(R, NLR + e, ok ? L[Ly::RD + row] : 0.0f, ok ? L[Ly::JA + row] : 0.0f, ok ? v[e] : 0.0f);
+        const float D = L[Ly::RD + row], ja = L[Ly::JA + row];
+        set_row(R, NLR + e, ok ? D : 0.0f, ok ? ja : 0.0f, ok ? v[e] : 0.0f);
       }
     }
     float sn = 0.0f, sMa = 0.0f, sf = 0.0f, sMv = 0.0f;
