@@ -160,63 +160,13 @@ def pivot_order(m: Model):
 
 def team_tables(m: Model, rows, adr, pre: str, floor: int):
     """Index tables for the team (16 lanes per env) kernel: lanes pick their work items
-    (bodies of a tree level, mass-matrix entries, LDL updates) from these."""
+    (mass-matrix entries, limb bodies and dofs, constraint rows) from these; they are packed into
+    one blob that each launch copies into LDS."""
     nb, nv = m.nbody, m.nv
-    depth = np.zeros(nb, dtype=int)
-    for b in range(1, nb):
-        depth[b] = depth[m.body_parentid[b]] + 1
-    nlev = int(depth.max())
-    levels = [[b for b in range(1, nb) if depth[b] == lv + 1] for lv in range(nlev)]
-    levw = max(len(lv) for lv in levels)
-    assert levw <= 16
-    lev = np.full((nlev, levw), -1)
-    for i, lv in enumerate(levels):
-        lev[i, :len(lv)] = lv
-    children = [[c for c in range(1, nb) if m.body_parentid[c] == b] for b in range(nb)]
-    maxch = max(1, max(len(c) for c in children))
-    child = np.full((nb, maxch), -1)
-    for b, c in enumerate(children):
-        child[b, :len(c)] = c
     full = np.full((nv, nv), -1)
-    mi, mj = np.zeros(int(adr.max()) + 1, dtype=int), np.zeros(int(adr.max()) + 1, dtype=int)
     for i in range(nv):
         for j in rows[i]:
             full[i, j] = full[j, i] = adr[i, j]
-            mi[adr[i, j]], mj[adr[i, j]] = i, j
-    ldl, ldl_off = [], [0]
-    anc_dof, anc_adr, anc_off = [], [], [0]
-    for k in range(nv):
-        for i in _ancestors(m, k, False):
-            for j in _ancestors(m, i, True):
-                ldl.append((adr[i, j], adr[k, i], adr[k, j]))
-            anc_dof.append(i)
-            anc_adr.append(adr[k, i])
-        ldl_off.append(len(ldl))
-        anc_off.append(len(anc_dof))
-    # the same LDL'/solve work packed per (pivot, round of 16 lanes) for register-resident
-    # per-lane index words: ldl word = aij | aki << 10 | akj << 20, anc word = dof | adr << 10
-    assert int(adr.max()) < 1024 and nv < 1024
-    ldl_nr, ldl_rb, ldlp = [], [], []
-    anc_nr, anc_rb, ancp = [], [], []
-    for k in range(nv):
-        ent = [int(a) | int(b) << 10 | int(c) << 20 for (a, b, c) in ldl[ldl_off[k]:ldl_off[k + 1]]]
-        nr = (len(ent) + 15) // 16
-        ldl_rb.append(len(ldlp))
-        ldl_nr.append(nr)
-        for r in range(nr):
-            row = ent[16 * r:16 * r + 16]
-            ldlp.append(row + [-1] * (16 - len(row)))
-        ent = [int(d) | int(a) << 10 for d, a in zip(anc_dof[anc_off[k]:anc_off[k + 1]], anc_adr[anc_off[k]:anc_off[k + 1]])]
-        nr = (len(ent) + 15) // 16
-        anc_rb.append(len(ancp))
-        anc_nr.append(nr)
-        for r in range(nr):
-            row = ent[16 * r:16 * r + 16]
-            ancp.append(row + [-1] * (16 - len(row)))
-    if not ldlp:
-        ldlp = [[-1] * 16]
-    if not ancp:
-        ancp = [[-1] * 16]
     # register-resident LDL': lane l of column set s owns column c = 16 s + l; bit k of its
     # descendant mask is set when c is a strict ancestor of dof k
     assert nv <= 32
@@ -403,21 +353,11 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     extra_const = [f"  static constexpr int T_MAXSUB = {msub};\n"]
     T = lambda name, a, t: f"__device__ const {t} {pre}_{name}{''.join(f'[{d}]' for d in np.shape(a))} = " + \
         _arr("x", np.asarray(a), t).split("= ", 1)[1]
-    tabs = {"lev": (lev, "int"), "child": (child, "int"), "madr": (full, "int"), "mi": (mi, "int"), "mj": (mj, "int"),
-            "ldl": (np.array(ldl).reshape(-1, 3), "int"), "ldl_off": (ldl_off, "int"), "anc_dof": (anc_dof, "int"),
-            "anc_adr": (anc_adr, "int"), "anc_off": (anc_off, "int"),
-            "ldlp": (np.array(ldlp), "int"), "ancp": (np.array(ancp), "int"), "br": (br_arr, "int"), "brdof": (brdof, "int"),
-            "desc": (desc, "int"), "blob": (np.array(blob, dtype=np.int64), "int")}
+    # the lane-indexed tables live in the blob (copied to LDS per launch); it is the only device array
+    tabs = {"blob": (np.array(blob, dtype=np.int64), "int")}
     dev = [T(k, a, t) for k, (a, t) in tabs.items()]
-    acc = [f"  static constexpr int T_NLEV = {nlev}, T_LEVW = {levw}, T_MAXCH = {maxch};\n",
-           f"  static constexpr int T_MAXLDL = {max(ldl_off[k + 1] - ldl_off[k] for k in range(nv))}, "
-           f"T_MAXANC = {max(anc_off[k + 1] - anc_off[k] for k in range(nv))};\n",
-           f"  static constexpr int PLANE_PAIR[2] = {{{pplane[0]}, {pplane[1]}}};\n",
+    acc = [f"  static constexpr int PLANE_PAIR[2] = {{{pplane[0]}, {pplane[1]}}};\n",
            f"  static constexpr int FOOT_PAIR = {pfoot[0] if pfoot else -1};\n",
-           f"  static constexpr int T_LDL_NRT = {len(ldlp)}, T_ANC_NRT = {len(ancp)};\n",
-           _arr("T_LDL_NR", ldl_nr, "int"), _arr("T_LDL_RB", ldl_rb, "int"),
-           _arr("T_ANC_NR", anc_nr, "int"), _arr("T_ANC_RB", anc_rb, "int"),
-           _arr("T_DIAG", [adr[i, i] for i in range(nv)], "int"),
            _arr("T_PORD", pivot_order(m), "int"),
            f"  static constexpr int T_NROOT = {len(root)}, T_NBR = {len(branches)}, T_BRLEN = {brlen}, "
            f"T_BRMD = {int(max(m.body_dofnum[b] for br in branches for b in br))};\n",

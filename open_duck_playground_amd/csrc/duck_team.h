@@ -551,7 +551,9 @@ struct TPhys {
       for (int q = 0; q < MC; q++) {
         float v = 0.0f;
         for (int k = 0; k < 6; k++) v += cj[q][k] * F[k];
-        if (i < NV && jj[q] >= 0) L[Ly::M + rs + q] = v + (jj[q] == i ? arm : 0.0f);
+        // branchless store (a masked region per entry costs more than the select)
+        const bool ok = i < NV && jj[q] >= 0;
+        L[ok ? Ly::M + rs + q : TL::SINK + lane] = v + (jj[q] == i ? arm : 0.0f);
       }
     }
     TSYNC();
@@ -574,82 +576,6 @@ struct TPhys {
       L[Ly::FSM + dof] += g * f;
     }
     TSYNC();
-  }
-
-  // ---------------- sparse LDL' of H in place (mj_factorM): one pivot per pass ----------------
-  // Each lane holds its index words for every pass in registers (loaded once, fully
-  // unrolled over pivots), so a pass is LDS loads -> FMA -> LDS store with no table latency.
-  // Pass k updates the ancestors' block of pivot k and scales row k+1 (independent data).
-  static DK void factor_H(LP L, int lane) {
-    constexpr int NR = Md::T_LDL_NRT, NA = Md::T_ANC_NRT;
-    int w[NR], a[NA];
-#pragma unroll
-    for (int r = 0; r < NR; r++) w[r] = Md::t_ldlp()[r][lane];
-#pragma unroll
-    for (int r = 0; r < NA; r++) a[r] = Md::t_ancp()[r][lane];
-#pragma unroll
-    for (int k = NV - 1; k >= -1; k--) {
-      if (k >= 0) {
-        const float inv = 1.0f / L[Ly::H + Md::T_DIAG[k]];
-#pragma unroll
-        for (int m = 0; m < Md::T_LDL_NR[k]; m++) {
-          const int v = w[Md::T_LDL_RB[k] + m];
-          if (v >= 0) {
-            const int aij = v & 1023, aki = (v >> 10) & 1023, akj = v >> 20;
-            L[Ly::H + aij] -= L[Ly::H + aki] * inv * L[Ly::H + akj];
-          }
-        }
-      }
-      const int sr = k + 1;  // scale row sr (its pass is complete)
-      if (sr < NV) {
-        const float dinv = 1.0f / L[Ly::H + Md::T_DIAG[sr]];
-#pragma unroll
-        for (int m = 0; m < Md::T_ANC_NR[sr]; m++) {
-          const int v = a[Md::T_ANC_RB[sr] + m];
-          if (v >= 0) L[Ly::H + (v >> 10)] *= dinv;
-        }
-      }
-      TSYNC();
-    }
-  }
-
-  static DK int diag_adr(int i) { return madr(i, i); }
-
-  // DST = sign * H^-1 SRC with H factored in place (mj_solveLD)
-  static DK void solve_H(LP L, int lane, int SRC, int DST, float sign) {
-    constexpr int NA = Md::T_ANC_NRT;
-    int a[NA];
-#pragma unroll
-    for (int r = 0; r < NA; r++) a[r] = Md::t_ancp()[r][lane];
-    for (int i = lane; i < NV; i += TEAM) L[DST + i] = L[SRC + i];
-    TSYNC();
-#pragma unroll
-    for (int k = NV - 1; k >= 0; k--) {
-      if (Md::T_ANC_NR[k] == 0) continue;
-      const float xk = L[DST + k];
-#pragma unroll
-      for (int m = 0; m < Md::T_ANC_NR[k]; m++) {
-        const int v = a[Md::T_ANC_RB[k] + m];
-        if (v >= 0) L[DST + (v & 1023)] -= L[Ly::H + (v >> 10)] * xk;
-      }
-      TSYNC();
-    }
-    for (int i = lane; i < NV; i += TEAM) L[DST + i] = sign * (L[DST + i] / L[Ly::H + diag_adr(i)]);
-    TSYNC();
-    // forward substitution is linear, so the sign can be applied before it
-#pragma unroll
-    for (int k = 0; k < NV; k++) {
-      if (Md::T_ANC_NR[k] == 0) continue;
-      float s = 0.0f;
-#pragma unroll
-      for (int m = 0; m < Md::T_ANC_NR[k]; m++) {
-        const int v = a[Md::T_ANC_RB[k] + m];
-        if (v >= 0) s += L[Ly::H + (v >> 10)] * L[DST + (v & 1023)];
-      }
-      s = tsum(s);
-      if (lane == 0) L[DST + k] -= s;
-      TSYNC();
-    }
   }
 
   // ---------------- register-resident LDL' (mj_factorM + mj_solveLD) ----------------
@@ -1682,7 +1608,11 @@ struct TPhys {
 
   static DK float fric_cost(float D, float x, float f) {
     const float rf = f * frcp(D);
-    return x <= -rf ? (-f * x - 0.5f * rf * f) : (x >= rf ? (f * x - 0.5f * rf * f) : 0.5f * D * x * x);
+    // the three pieces computed unconditionally and selected (nested ?: on expressions compiles to
+    // branches)
+    const float lo = -f * x - 0.5f * rf * f, hi = f * x - 0.5f * rf * f, qd = 0.5f * D * x * x;
+    const float r = x >= rf ? hi : qd;
+    return x <= -rf ? lo : r;
   }
 
   // the lane's constraint rows for the line search: its friction row, limit rows, and the
