@@ -50,6 +50,7 @@ struct KArgs {
 constexpr int WG = 16;
 constexpr int EPW = 4;
 constexpr int TPB = WG * TEAM;
+static_assert(TPB == TPB_TEAM, "load_model_tables assumes the kernels' block size");
 constexpr int SW = 1;  // slice stride (contiguous per-env slices)
 
 // this lane's env within the workgroup (-1: idle lane) and its rank in the env's team
@@ -443,25 +444,52 @@ __global__ void __launch_bounds__(TPB) reset_kernel(KArgs A) {
   for (int k = 0; k < Lo.priv_size; k++) F[Lo.first_priv + k] = A.priv[(size_t)e * Lo.priv_size + k];
 }
 
+// the per-env values step_env reads from HBM besides the hot state: integer counters, the RNG
+// key, this lane's action. Loaded by one batch of independent loads issued together with the
+// hot-state loads, so the step waits for one memory round trip instead of three
+struct StepPre {
+  int32_t step, push_step, push_interval, ep_steps, imitation_i;
+  uint32_t k0, k1, ctr;
+  float act;
+};
+template <class Md>
+DK StepPre step_prefetch(const KArgs& A, int e, int lane) {
+  static_assert(Md::NU <= TEAM, "an actuator per lane");
+  const duck_layout& Lo = A.lay;
+  const int n = A.n, ec = e < n ? e : 0;
+  auto ig = [&](int k) { return A.is[(size_t)k * n + ec]; };
+  StepPre P;
+  P.step = ig(Lo.step);
+  P.push_step = ig(Lo.push_step);
+  P.push_interval = ig(Lo.push_interval);
+  P.ep_steps = ig(Lo.ep_steps);
+  P.imitation_i = ig(Lo.imitation_i);
+  P.k0 = (uint32_t)ig(Lo.rng_key);
+  P.k1 = (uint32_t)ig(Lo.rng_key + 1);
+  P.ctr = (uint32_t)ig(Lo.rng_ctr);
+  P.act = A.action[(size_t)ec * Md::NU + (lane < Md::NU ? lane : 0)];
+  return P;
+}
+
 // Joystick.step body for env e (joystick.py:323-481 + wrappers); F = the env's hot state
 // (LDS-staged or the global row), G = the global row (auto-reset snapshot)
 template <class Md, class FA, bool STAGE_OBS, class RT>
-DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, const Col<0>& G, const RT& r) {
+DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, const Col<0>& G, const RT& r,
+                 const StepPre& P) {
   using Ly = Lay<Md>;
   const duck_env_config& c = A.cfg;
   const duck_layout& Lo = A.lay;
   constexpr int NQ = Md::NQ, NV = Md::NV, NU = Md::NU;
   const int n = A.n;
   STAGE_T0();
-  auto iget = [&](int k) { return A.is[(size_t)k * n + e]; };
   auto iset = [&](int k, int32_t v) { A.is[(size_t)k * n + e] = v; };
   const float dt = c.ctrl_dt;
-  // every integer counter is read up front (a global load issued after the obs stores would
-  // wait for them: vmcnt counts stores too on CDNA)
-  const int step_prev = iget(Lo.step), push_step = iget(Lo.push_step), push_interval = iget(Lo.push_interval);
-  int ep_steps = iget(Lo.ep_steps);
+  // every integer counter was read up front (step_prefetch; a global load issued after the obs
+  // stores would wait for them: vmcnt counts stores too on CDNA)
+  const int step_prev = P.step, push_step = P.push_step, push_interval = P.push_interval;
+  int ep_steps = P.ep_steps;
   if (c.auto_reset && F[Lo.done] != 0.0f) ep_steps = 0;
-  int imitation_i = iget(Lo.imitation_i);
+  int imitation_i = P.imitation_i;
   if (Lo.imitation) {  // joystick.py:325-355
     const int nb = A.ref.nb;
     imitation_i = (imitation_i + 1) % nb;
@@ -478,7 +506,7 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   const int didx = r.randint(SLOT_ACTION_DELAY, c.action_min_delay, c.action_max_delay);
   float arate = 0.0f;
   for (int a = STAGE_OBS ? lane : 0; a < NU; a += STAGE_OBS ? TEAM : 1) {
-    const float act = A.action[(size_t)e * NU + a];
+    const float act = STAGE_OBS ? P.act : A.action[(size_t)e * NU + a];
     const float h1 = F[Lo.action_history + a], h2 = F[Lo.action_history + NU + a];
     F[Lo.action_history + a] = act;
     F[Lo.action_history + NU + a] = h1;
@@ -717,6 +745,7 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
     for (int k = lane; k < Lo.priv_size; k += TEAM) priv[k] = L[Ly::H + k];
     for (int k = lane; k < Lo.obs_size; k += TEAM) obs[k] = L[Ly::H + k];
   }
+  STAGE_MARK(34);
 }
 
 
@@ -726,6 +755,7 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
 #ifdef DUCK_ANY_PROF
   const unsigned long long kstart = clock64();
 #endif
+  using TL = TLay<Md>;
   {
     extern __shared__ float lds_t[];
     load_model_tables<Md>(lds_t);
@@ -737,29 +767,47 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   const int e = blockIdx.x * WG + t;
   const int n = A.n;
   extern __shared__ float lds[];
-  using TL = TLay<Md>;
   if constexpr (TL::ES_LDS) {
     // hot state <-> LDS by the whole workgroup, field-major: a wave instruction moves 4 fields
     // x 16 consecutive envs (four 64-B segments of the [field][env] rows) instead of 16 fields x
     // 4 envs; the step's 64 random draws are made by each team in parallel into the same region
     const int j = threadIdx.x % WG, ej = blockIdx.x * WG + j;
     lds_float* esj = (lds_float*)(lds + TL::ES + j * TL::ESTRIDE);
-    if (ej < n)
-      for (int k = threadIdx.x / WG; k < TL::HOT; k += TPB / WG) esj[k] = A.fs[(size_t)k * n + ej];
+    const StepPre P = step_prefetch<Md>(A, e, lane);
+    {
+      // compile-time trip count: all of the thread's loads are in flight before the first store
+      // waits (one memory round trip; a runtime-bounded loop costs one per unrolled group)
+      constexpr int NK = (TL::HOT + TPB / WG - 1) / (TPB / WG);
+      const int ejc = ej < n ? ej : 0;
+      float hv[NK];
+#pragma unroll
+      for (int kk = 0; kk < NK; kk++) {
+        const int k = (int)threadIdx.x / WG + (TPB / WG) * kk;
+        hv[kk] = A.fs[(size_t)(k < TL::HOT ? k : TL::HOT - 1) * n + ejc];
+      }
+#pragma unroll
+      for (int kk = 0; kk < NK; kk++) {
+        const int k = (int)threadIdx.x / WG + (TPB / WG) * kk;
+        if (ej < n && k < TL::HOT) esj[k] = hv[kk];
+      }
+    }
     __syncthreads();
+    STAGE_MARK(32);
     if (e < n) {
       const Slice<SW> L = env_slice<Md>(lds, t);
       const Col<0> G{A.fs + e, n};  // global row: the auto-reset snapshot (first_*) stays in HBM
       const duck_layout& Lo = A.lay;
       lds_float* esp = (lds_float*)(lds + TL::ES + t * TL::ESTRIDE);
       RngTab rt;
-      rt.k0 = (uint32_t)A.is[(size_t)Lo.rng_key * n + e];
-      rt.k1 = (uint32_t)A.is[(size_t)(Lo.rng_key + 1) * n + e];
-      rt.ctr = (uint32_t)A.is[(size_t)Lo.rng_ctr * n + e];
+      rt.k0 = P.k0;
+      rt.k1 = P.k1;
+      rt.ctr = P.ctr;
       rt.tab = esp + TL::HOT;
       rt.fill(esp + TL::HOT, lane);
       TSYNC();
-      step_env<Md, LCol, true>(A, e, lane, L, LCol{esp}, G, rt);
+      STAGE_MARK(33);
+      step_env<Md, LCol, true>(A, e, lane, L, LCol{esp}, G, rt, P);
+      STAGE_RESET();
     }
     __syncthreads();
     if (ej < n)
@@ -773,11 +821,11 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
     r.k0 = (uint32_t)A.is[(size_t)Lo.rng_key * n + e];
     r.k1 = (uint32_t)A.is[(size_t)(Lo.rng_key + 1) * n + e];
     r.ctr = (uint32_t)A.is[(size_t)Lo.rng_ctr * n + e];
-    step_env<Md, Col<0>, true>(A, e, lane, L, G, G, r);
+    step_env<Md, Col<0>, true>(A, e, lane, L, G, G, r, step_prefetch<Md>(A, e, lane));
   }
   STAGE_MARK(15);
 #ifdef DUCK_ANY_PROF
-  if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_stage_cycles[32 + 4 * blockIdx.x + threadIdx.x / 64] = clock64() - kstart;
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_stage_cycles[DUCK_NSTAGE + 4 * blockIdx.x + threadIdx.x / 64] = clock64() - kstart;
 #endif
 }
 
@@ -920,9 +968,9 @@ static int launch_physics(duck_sim* s, int n, float* qpos, float* qvel, float* w
 
 static int stage_cycles_of(unsigned long long* out, int reset) {
 #ifdef DUCK_ANY_PROF
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), sizeof(unsigned long long) * (32 + 1024));
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), sizeof(unsigned long long) * (DUCK_NSTAGE + 1024));
   if (e == hipSuccess && reset) {
-    static unsigned long long z[32 + 1024] = {0};
+    static unsigned long long z[DUCK_NSTAGE + 1024] = {0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, sizeof(z));
   }
   return e == hipSuccess ? 0 : DUCK_EHIP;

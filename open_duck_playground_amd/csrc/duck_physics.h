@@ -28,10 +28,11 @@ typedef __attribute__((address_space(3))) float lds_float;
 #define DUCK_ANY_PROF 1
 #endif
 #ifdef DUCK_ANY_PROF
-static __device__ unsigned long long g_stage_cycles[32 + 1024];
+#define DUCK_NSTAGE 48
+static __device__ unsigned long long g_stage_cycles[DUCK_NSTAGE + 1024];
 #endif
 #ifdef DUCK_STAGE_PROF
-// g_stage_cycles: [0, 32) stage counters; [32, 32 + 1024) cycles of each of the first 1024 waves
+// g_stage_cycles: [0, DUCK_NSTAGE) stage counters; [DUCK_NSTAGE, DUCK_NSTAGE + 1024) cycles of each of the first 1024 waves
 // of the last step_kernel launch (wave = 4 * workgroup + wave-in-workgroup), for the launch tail
 #define STAGE_T0() unsigned long long _t0 = wall_clock64(), _c0 = clock64()
 #define STAGE_RESET() (_c0 = clock64())

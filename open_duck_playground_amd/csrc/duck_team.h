@@ -18,6 +18,7 @@
 
 constexpr int TEAM = 16;
 constexpr int TEAM_WG = 16;  // envs (teams) per workgroup: 256 threads = 4 waves
+constexpr int TPB_TEAM = TEAM * TEAM_WG;
 typedef __attribute__((address_space(3))) int lds_int;
 
 // fp32 reciprocal as one v_rcp_f32 (1 ulp; operands here are never denormal or zero)
@@ -147,8 +148,21 @@ struct TLay {
 template <class Md>
 DK void load_model_tables(float* lds) {
   if constexpr (TLay<Md>::TAB_LDS) {
+    // a compile-time trip count: every load of the thread is issued before the first store waits
+    // (a runtime-bounded loop waits for each group of loads: one memory round trip per group)
     int* dst = (int*)(lds + TLay<Md>::TAB);
-    for (int i = threadIdx.x; i < Md::NBLOB; i += blockDim.x) dst[i] = Md::t_blob()[i];
+    constexpr int NK = (Md::NBLOB + TPB_TEAM - 1) / TPB_TEAM;
+    int w[NK];
+#pragma unroll
+    for (int kk = 0; kk < NK; kk++) {
+      const int i = (int)threadIdx.x + TPB_TEAM * kk;
+      w[kk] = Md::t_blob()[i < Md::NBLOB ? i : Md::NBLOB - 1];
+    }
+#pragma unroll
+    for (int kk = 0; kk < NK; kk++) {
+      const int i = (int)threadIdx.x + TPB_TEAM * kk;
+      if (i < Md::NBLOB) dst[i] = w[kk];
+    }
     __syncthreads();
   }
 }
