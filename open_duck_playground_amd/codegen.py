@@ -234,6 +234,17 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         blob.extend(int(w) for w in words)
 
     put("madr", full.reshape(-1))
+    # load_cols: per (column set s, row r, lane) the M entry of column 16 s + lane, or the zero word
+    # after M (Lay::MZERO = M + NM) where the tree pattern has none: one unmasked load per entry
+    nm_ = int(adr.max()) + 1
+    mcolz = np.full((nc, nv, 16), nm_)
+    for s_ in range(nc):
+        for r in range(nv):
+            for ln in range(16):
+                c = 16 * s_ + ln
+                if c < nv and full[r, c] >= 0:
+                    mcolz[s_, r, ln] = full[r, c]
+    put("mcolz", mcolz.reshape(-1))
     put("desc", desc.reshape(-1))
     fric = [i for i in range(nv) if m.dof_frictionloss[i] > 0]
     rec = []

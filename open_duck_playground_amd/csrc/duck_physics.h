@@ -80,7 +80,9 @@ struct Lay {
   static constexpr int CVEL = CIN + 10 * NB, COM = CVEL + 6 * NB;
   static constexpr int CDOF = COM + 3, CDD1 = CDOF + 6 * NV;
   // matrices
-  static constexpr int M = CDD1 + 18, H = M + Md::NM;
+  // M, then one word kept at zero (crb writes it with M): the register column
+  // loads of M read it for the entries outside the tree pattern (codegen mcolz table)
+  static constexpr int M = CDD1 + 18, MZERO = M + Md::NM, H = MZERO + 1;
   // RNE accumulators live in the H + row storage (dead until smooth()/make_rows())
   static constexpr int CACC = H, CFRC = CACC + 6 * NB;
   static_assert(12 * NB <= Md::NM + 4 * NROW, "RNE scratch must fit in H + rows");

@@ -541,6 +541,8 @@ struct TPhys {
     constexpr int BL = Md::T_BRLEN, MC = Md::MAXCHAIN;
     // (the composite inertias were summed in rne's subtree pass)
     STAGE_MARK(19);
+    L[lane == 0 ? Ly::MZERO : TL::SINK + lane] = 0.0f;  // the zero word load_cols reads (LDS is not
+                                                          // initialised by the launch)
     // M row i (lane i, i + 16): F_i = crb_{body(i)} cdof_i stays in registers;
     // M[i][j] = cdof_j . F_i over the ancestors j of i (the row is contiguous in M)
 #pragma unroll
@@ -713,7 +715,7 @@ struct TPhys {
   // out of line so the rare dense path does not share the hot path's code layout / registers
   static DNI void newton_dense(LP L, int lane) {
     float Mc[NC][NV];
-    load_cols(L, lane, Ly::M, Mc, false);
+    load_cols(L, lane, Mc, false);
     newton_fused<true>(L, lane, Mc);
   }
   // dense variant (a full lower triangle): pivots in natural order NV-1 .. 0, each updating every
@@ -782,27 +784,28 @@ struct TPhys {
       F.desc[s] = c < NV ? (unsigned)ti(Md::B_DESC + TEAM * s + lane) : 0u;
     }
   }
-  // columns of the symmetric tree-sparse matrix at HOFF: full (both triangles) or lower only
-  static DK void load_cols(LP L, int lane, int HOFF, float (*col)[NV], bool lower_only) {
+  // columns of the symmetric tree-sparse M: full (both triangles) or lower only. Entries outside
+  // the tree pattern (and columns past NV) read the zero word after M: one load per entry, no mask
+  static DK void load_cols(LP L, int lane, float (*col)[NV], bool lower_only) {
+    // lane opaque: the table words are per-lane constants, which the compiler would otherwise
+    // hoist out of the substep loop and keep in registers (+39 AGPRs)
+    asm volatile("" : "+v"(lane));
 #pragma unroll
     for (int s = 0; s < NC; s++) {
-      const int c = TEAM * s + lane, cc = c < NV ? c : 0;
 #pragma unroll
       for (int r = 0; r < NV; r++) {
-        const int a = madr(r, cc);
         if (lower_only && r < TEAM * s) { col[s][r] = 0.0f; continue; }  // above the diagonal
-        const float v = L[HOFF + (a >= 0 ? a : 0)];  // unconditional load: no branch per entry
         // (with lower_only the entries right of the diagonal may stay: the factorization's lower
         // triangle never reads them, and factor_solve drops them afterwards)
-        col[s][r] = (c < NV && a >= 0) ? v : 0.0f;
+        col[s][r] = L[Ly::M + ti(Md::B_MCOLZ + TEAM * (NV * s + r) + lane)];
       }
     }
   }
 
-  // DST = sign * A^-1 SRC for the tree-sparse SPD matrix A stored at HOFF (M_adr pattern)
-  static DK void solve_regs(LP L, int lane, int HOFF, int SRC, int DST, float sign) {
+  // DST = sign * M^-1 SRC (M tree-sparse SPD, M_adr pattern)
+  static DK void solve_regs(LP L, int lane, int SRC, int DST, float sign) {
     Fac F;
-    load_cols(L, lane, HOFF, F.col, true);
+    load_cols(L, lane, F.col, true);
     float x[NC];
 #pragma unroll
     for (int s = 0; s < NC; s++) {
@@ -1675,7 +1678,7 @@ struct TPhys {
     STAGE_T0();
     // M as full symmetric columns in registers for every M.x of the solver
     float Mc[NC][NV];
-    load_cols(L, lane, Ly::M, Mc, false);
+    load_cols(L, lane, Mc, false);
     STAGE_MARK(20);
     // warm start vs smooth acceleration: J and M products of both in one pass
     // (M qacc_smooth = qfrc_smooth by definition: no product needed for the smooth start)
@@ -2025,7 +2028,7 @@ struct TPhys {
     STAGE_MARK(3);
     smooth(L, lane);
     STAGE_MARK(28);
-    solve_regs(L, lane, Ly::M, Ly::FSM, Ly::QSM, 1.0f);
+    solve_regs(L, lane, Ly::FSM, Ly::QSM, 1.0f);
     STAGE_MARK(4);
     collision(L, lane, hf);
     STAGE_MARK(5);
