@@ -191,6 +191,10 @@ struct TPhys {
   static DK int lim_dof(int r) { return ti(Md::B_LIM + LIMW * r); }
   static DK int madr(int i, int j) { return ti(Md::B_MADR + NV * i + j); }
   // lane-indexed model constants live in the LDS blob (codegen.team_tables records)
+  // dofs 0-2 are the translational dofs of the trunk's free joint: their motion axes (cdof rows,
+  // com_pos) are the unit vectors e_3, e_4, e_5, so cdof_i . x = x[3 + i] exactly for i < 3 and the
+  // products that read those rows are skipped
+  static constexpr bool FREE0 = Md::jnt_type[0] == 0 && Md::body_dofadr[1] == 0 && Md::body_dofnum[1] == 6;
   static constexpr unsigned long long moving_mask() {
     unsigned long long msk = 0;
     for (int b = 0; b < Md::NB; b++)
@@ -396,10 +400,8 @@ struct TPhys {
   static DK void root_motion(LP L, int lane, int b, float* cv, float* ca) {
     const int da = Md::body_dofadr[b], nd = Md::body_dofnum[b];
     if (nd == 6) {
-      for (int i = 0; i < 3; i++) {
-        const float v = L[Ly::QVEL + da + i];
-        for (int k = 0; k < 6; k++) cv[k] += L[Ly::CDOF + 6 * (da + i) + k] * v;
-      }
+      // free joint: the translational cdof rows are the unit vectors e_3..e_5 (com_pos)
+      for (int i = 0; i < 3; i++) cv[3 + i] += L[Ly::QVEL + da + i];
       float cvt[6];
       for (int k = 0; k < 6; k++) cvt[k] = cv[k];
       for (int i = 3; i < 6; i++) {
@@ -557,6 +559,7 @@ struct TPhys {
 #pragma unroll
       for (int q = 0; q < MC; q++) {
         jj[q] = ti(Md::B_DCHAIN + MC * ic + q);
+        if (FREE0 && q < 3) continue;  // ancestors ascending: position q < 3 is dof q, cdof = e_{3+q}
         const int jc = jj[q] >= 0 ? jj[q] : 0;
         for (int k = 0; k < 6; k++) cj[q][k] = L[Ly::CDOF + 6 * jc + k];
       }
@@ -566,7 +569,10 @@ struct TPhys {
 #pragma unroll
       for (int q = 0; q < MC; q++) {
         float v = 0.0f;
-        for (int k = 0; k < 6; k++) v += cj[q][k] * F[k];
+        if (FREE0 && q < 3)
+          v = F[3 + q];  // cdof_q = e_{3+q}
+        else
+          for (int k = 0; k < 6; k++) v += cj[q][k] * F[k];
         // branchless store (a masked region per entry costs more than the select)
         const bool ok = i < NV && jj[q] >= 0;
         L[ok ? Ly::M + rs + q : TL::SINK + lane] = v + (jj[q] == i ? arm : 0.0f);
@@ -957,6 +963,7 @@ struct TPhys {
 #pragma unroll
         for (int r = 0; r < NV; r++) {
           if (!((msk >> r) & 1u) || r < TEAM * s) continue;  // compile-time: chain rows on or below the diagonal
+          if (FREE0 && r < 3) { F.col[s][r] += kc[3 + r]; continue; }  // cdof_r = e_{3+r}
           float h = 0.0f;
           for (int k = 0; k < 6; k++) h += L[Ly::CDOF + 6 * r + k] * kc[k];
           F.col[s][r] += h;  // (entries right of the diagonal are dropped after the factorization)
@@ -1613,6 +1620,15 @@ struct TPhys {
         if (iL < 0 && iR < 0) continue;
         const bool ok = left ? iL >= 0 : iR >= 0;
         const int ic = left ? (iL >= 0 ? iL : 0) : (iR >= 0 ? iR : 0);
+        if (FREE0 && iL == iR && iL >= 0 && iL < 3) {  // cdof = e_{3+i}: only lane k = 3 + i adds x
+          const float x = L[X + iL];
+          s += k == 3 + iL ? x : 0.0f;
+          if (X2 >= 0) {
+            const float x2 = L[X2 + iL];
+            s2 += k == 3 + iL ? x2 : 0.0f;
+          }
+          continue;
+        }
         const float cv = L[Ly::CDOF + 6 * ic + k];
         const float cd = ok ? cv : 0.0f;
         s += cd * L[X + ic];
