@@ -753,7 +753,7 @@ template <class Md, int WG>
 __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   STAGE_T0();
 #ifdef DUCK_ANY_PROF
-  const unsigned long long kstart = clock64();
+  const unsigned long long kstart = clock64(), kwall = wall_clock64();
 #endif
   using TL = TLay<Md>;
   {
@@ -825,7 +825,12 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
   }
   STAGE_MARK(15);
 #ifdef DUCK_ANY_PROF
-  if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_stage_cycles[DUCK_NSTAGE + 4 * blockIdx.x + threadIdx.x / 64] = clock64() - kstart;
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) {
+    const int w = 4 * blockIdx.x + threadIdx.x / 64;
+    g_stage_cycles[DUCK_NSTAGE + w] = clock64() - kstart;
+    g_stage_cycles[DUCK_NSTAGE + 1024 + w] = kwall;
+    g_stage_cycles[DUCK_NSTAGE + 2048 + w] = wall_clock64();
+  }
 #endif
 }
 
@@ -968,10 +973,15 @@ static int launch_physics(duck_sim* s, int n, float* qpos, float* qvel, float* w
 
 static int stage_cycles_of(unsigned long long* out, int reset) {
 #ifdef DUCK_ANY_PROF
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), sizeof(unsigned long long) * (DUCK_NSTAGE + 1024));
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), sizeof(unsigned long long) * (DUCK_NSTAGE + 3 * 1024));
+  static unsigned long long wg[DUCK_NSTAGE * 256];
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(wg, HIP_SYMBOL(g_stage_wg), sizeof(wg));
+  for (int k = 0; k < DUCK_NSTAGE && e == hipSuccess; k++)
+    for (int b = 0; b < 256; b++) out[k] += wg[k * 256 + b];
   if (e == hipSuccess && reset) {
-    static unsigned long long z[DUCK_NSTAGE + 1024] = {0};
+    static unsigned long long z[DUCK_NSTAGE + 3 * 1024] = {0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, sizeof(z));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_wg), z, sizeof(wg));
   }
   return e == hipSuccess ? 0 : DUCK_EHIP;
 #else

@@ -29,10 +29,16 @@ typedef __attribute__((address_space(3))) float lds_float;
 #endif
 #ifdef DUCK_ANY_PROF
 #define DUCK_NSTAGE 48
-static __device__ unsigned long long g_stage_cycles[DUCK_NSTAGE + 1024];
+static __device__ unsigned long long g_stage_cycles[DUCK_NSTAGE + 3 * 1024];
+// the stage counters themselves are kept per workgroup slot (summed by the host): one shared
+// counter per stage made every workgroup's atomics contend at one L2 channel, which slowed whole
+// XCDs by up to 30 % in profiled runs
+static __device__ unsigned long long g_stage_wg[DUCK_NSTAGE * 256];
+#define STAGE_ADD(k, v) atomicAdd(&g_stage_wg[(k) * 256 + (blockIdx.x & 255)], (v))
 #endif
 #ifdef DUCK_STAGE_PROF
-// g_stage_cycles: [0, DUCK_NSTAGE) stage counters; [DUCK_NSTAGE, DUCK_NSTAGE + 1024) cycles of each of the first 1024 waves
+// g_stage_cycles: [0, DUCK_NSTAGE) stage counters; then per wave of the first 1024: clock64 cycles,
+// wall-clock (s_memrealtime, 100 MHz) start, wall-clock end; [DUCK_NSTAGE, DUCK_NSTAGE + 1024) cycles of each of the first 1024 waves
 // of the last step_kernel launch (wave = 4 * workgroup + wave-in-workgroup), for the launch tail
 #define STAGE_T0() unsigned long long _t0 = wall_clock64(), _c0 = clock64()
 #define STAGE_RESET() (_c0 = clock64())
@@ -40,7 +46,7 @@ static __device__ unsigned long long g_stage_cycles[DUCK_NSTAGE + 1024];
   do {                                                                            \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                            \
     const unsigned long long _c1 = clock64();                                     \
-    if (threadIdx.x == 0) atomicAdd(&g_stage_cycles[k], _c1 - _c0);               \
+    if (threadIdx.x == 0) STAGE_ADD(k, _c1 - _c0);                                \
     _c0 = _c1;                                                                    \
     (void)_t0;                                                                    \
   } while (0)

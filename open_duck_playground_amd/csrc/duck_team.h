@@ -1516,7 +1516,7 @@ struct TPhys {
       } else {
         TSYNC();
 #ifdef DUCK_STAGE_PROF
-        if (lane == 0) atomicAdd(&g_stage_cycles[27], 1ull);  // how often the SAT path runs
+        if (lane == 0) STAGE_ADD(27, 1ull);  // how often the SAT path runs
 #endif
 #ifndef DUCK_DIAG_NO_RARE_CALLS
         collide_hulls_rare(L, lane);  // rare: the boxes overlap
@@ -1764,7 +1764,7 @@ struct TPhys {
     } else {
       TSYNC();
 #ifdef DUCK_STAGE_PROF
-      if (lane == 0) atomicAdd(&g_stage_cycles[23], 1ull);  // dense Newton fallbacks
+      if (lane == 0) STAGE_ADD(23, 1ull);  // dense Newton fallbacks
 #endif
 #ifndef DUCK_DIAG_NO_RARE_CALLS
       newton_dense(L, lane);  // rare: foot/foot contact rows active (dense H)

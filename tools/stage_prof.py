@@ -40,7 +40,7 @@ def main():
     for i in range(20):
         env.step(st, pool[i % len(pool)])
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * (NSTAGE + 1024))()
+    buf = (C.c_ulonglong * (NSTAGE + 3 * 1024))()
     lib = native.lib()
     lib.duck_debug_stage_cycles(env._sim, buf, 1)
     steps = 5
@@ -69,7 +69,17 @@ def main():
             print("  per-workgroup max/min spread: mean %.3f" % (wg.max(1) / wg.min(1)).mean())
             print("  per-XCD (blockIdx % 8) mean wave cycles:", [int(wg[x::8].mean()) for x in range(8)])
             print("  per wave-in-workgroup mean:", [int(wg[:, k].mean()) for k in range(4)])
-            print("  slowest workgroups:", list(np.argsort(wg.max(1))[-8:]))
+            print("  slowest workgroups:", [int(x) for x in np.argsort(wg.max(1))[-8:]])
+            t0 = np.array([buf[NSTAGE + 1024 + i] for i in range(4 * nwg)], dtype=np.float64).reshape(-1, 4)
+            t1 = np.array([buf[NSTAGE + 2048 + i] for i in range(4 * nwg)], dtype=np.float64).reshape(-1, 4)
+            base = t0.min()
+            us = lambda a: (a - base) / 100.0  # s_memrealtime: 100 MHz
+            print("  wall clock per XCD (us from the first wave's start): start mean/max, end mean/max")
+            for x in range(8):
+                print(f"    XCD {x}: start {us(t0[x::8]).mean():7.1f} {us(t0[x::8]).max():7.1f}  "
+                      f"end {us(t1[x::8]).mean():7.1f} {us(t1[x::8]).max():7.1f}  "
+                      f"duration mean {((t1[x::8] - t0[x::8]) / 100).mean():7.1f}")
+            print(f"  launch span (first start to last end): {us(t1).max():.1f} us")
     print(f"{'dense Newton fallbacks':28s} {buf[23] / steps:10.1f} per env-step (all {n} envs)")
     print(f"{'foot/foot SAT runs':28s} {buf[27] / steps:10.1f} per env-step (all {n} envs)")
     outside = per(14) + sum(per(k) for k in ENV)
