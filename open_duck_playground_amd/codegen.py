@@ -167,15 +167,8 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     for i in range(nv):
         for j in rows[i]:
             full[i, j] = full[j, i] = adr[i, j]
-    # register-resident LDL': lane l of column set s owns column c = 16 s + l; bit k of its
-    # descendant mask is set when c is a strict ancestor of dof k
     assert nv <= 32
     nc = (nv + 15) // 16
-    desc = np.zeros((nc, 16), dtype=np.int64)
-    for k in range(nv):
-        for i in _ancestors(m, k, False):
-            desc[i // 16, i % 16] |= 1 << k
-    desc = np.where(desc >= 2 ** 31, desc - 2 ** 32, desc)
     pplane = [p for p in range(m.npair) if m.pair_geom1[p] == floor]
     pfoot = [p for p in range(m.npair) if m.pair_geom1[p] != floor]
     assert len(pplane) == 2 and len(pfoot) <= 1
@@ -245,7 +238,6 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
                 if c < nv and full[r, c] >= 0:
                     mcolz[s_, r, ln] = full[r, c]
     put("mcolz", mcolz.reshape(-1))
-    put("desc", desc.reshape(-1))
     fric = [i for i in range(nv) if m.dof_frictionloss[i] > 0]
     rec = []
     for i in fric:

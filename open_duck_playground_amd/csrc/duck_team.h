@@ -604,12 +604,11 @@ struct TPhys {
   // Lane l holds column c = 16 s + l of the matrix densely in registers (col[s][row]); a pivot
   // reads H[K][I] from the lane owning column I with a DPP row broadcast (row_newbcast), so
   // a pass is a handful of broadcasts and FMAs with no memory traffic. Entries above the
-  // diagonal may collect garbage; they are never read unmasked (descendant masks).
+  // diagonal may collect garbage; factor_solve zeroes them before the triangular solves.
   static constexpr int NC = (NV + TEAM - 1) / TEAM;
   struct Fac {
     float col[NC][NV];
     float dg[NC];
-    unsigned desc[NC];
   };
   template <int SRC>
   static DK float bc(float v) { return dppf<0x150 + SRC>(v); }
@@ -637,7 +636,7 @@ struct TPhys {
     const float inv = __builtin_amdgcn_rcpf(dk);
     fac_anc<K, Md::dof_parentid[K]>(F, inv);
     // scale row K of every column; the diagonal entry (lane kl) becomes 1, never read again
-    // (D is kept in dg; the solves read strictly-below-diagonal entries via descendant masks)
+    // (D is kept in dg; the solves read only the strictly lower triangle)
 #pragma unroll
     for (int s = 0; s < NC; s++)
       if (TEAM * s <= K) F.col[s][K] *= inv;
@@ -783,13 +782,6 @@ struct TPhys {
     fwd_all_dense(F, x, lane, std::make_integer_sequence<int, NV>{});
   }
 
-  static DK void set_desc(Fac& F, int lane) {
-#pragma unroll
-    for (int s = 0; s < NC; s++) {
-      const int c = TEAM * s + lane;
-      F.desc[s] = c < NV ? (unsigned)ti(Md::B_DESC + TEAM * s + lane) : 0u;
-    }
-  }
   // columns of the symmetric tree-sparse M: full (both triangles) or lower only. Entries outside
   // the tree pattern (and columns past NV) read the zero word after M: one load per entry, no mask
   static DK void load_cols(LP L, int lane, float (*col)[NV], bool lower_only) {
