@@ -506,8 +506,11 @@ struct TPhys {
         }
       }
     }
-    for (int k = 0; k < 6; k++) S[k] = tsum(S[k]);
-    for (int k = 0; k < 10; k++) SI[k] = tsum(SI[k]);
+    // only the limb lanes hold sums and only lane 0 uses the total (root stores below): the
+    // reduction over the limb lanes (a quad for <= 4 limbs) is exact against the team sum, whose
+    // other lanes add zeros
+    for (int k = 0; k < 6; k++) S[k] = anc_sum<(1u << Md::T_NBR) - 1u, 0>(S[k]);
+    for (int k = 0; k < 10; k++) SI[k] = anc_sum<(1u << Md::T_NBR) - 1u, 0>(SI[k]);
     {
       float fr[NR][6], Rr[NR][10];
 #pragma unroll
