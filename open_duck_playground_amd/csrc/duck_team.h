@@ -788,17 +788,34 @@ struct TPhys {
   // columns of the symmetric tree-sparse M: full (both triangles) or lower only. Entries outside
   // the tree pattern (and columns past NV) read the zero word after M: one load per entry, no mask
   static DK void load_cols(LP L, int lane, float (*col)[NV], bool lower_only) {
-    // lane opaque: the table words are per-lane constants, which the compiler would otherwise
-    // hoist out of the substep loop and keep in registers (+39 AGPRs)
-    asm volatile("" : "+v"(lane));
+    if constexpr (TL::TAB_LDS) {
+      // lane opaque: the table words are per-lane constants, which the compiler would otherwise
+      // hoist out of the substep loop and keep in registers (+39 AGPRs)
+      asm volatile("" : "+v"(lane));
 #pragma unroll
-    for (int s = 0; s < NC; s++) {
+      for (int s = 0; s < NC; s++) {
 #pragma unroll
-      for (int r = 0; r < NV; r++) {
-        if (lower_only && r < TEAM * s) { col[s][r] = 0.0f; continue; }  // above the diagonal
-        // (with lower_only the entries right of the diagonal may stay: the factorization's lower
-        // triangle never reads them, and factor_solve drops them afterwards)
-        col[s][r] = L[Ly::M + ti(Md::B_MCOLZ + TEAM * (NV * s + r) + lane)];
+        for (int r = 0; r < NV; r++) {
+          if (lower_only && r < TEAM * s) { col[s][r] = 0.0f; continue; }  // above the diagonal
+          // (with lower_only the entries right of the diagonal may stay: the factorization's lower
+          // triangle never reads them, and factor_solve drops them afterwards)
+          col[s][r] = L[Ly::M + ti(Md::B_MCOLZ + TEAM * (NV * s + r) + lane)];
+        }
+      }
+    } else {
+      // model tables in global memory (models whose env slices leave no LDS for them): the M
+      // addresses of the pattern are loop-invariant index words the compiler keeps in registers
+      // across the substeps, so the masked form without the per-launch table reads is faster
+#pragma unroll
+      for (int s = 0; s < NC; s++) {
+        const int c = TEAM * s + lane, cc = c < NV ? c : 0;
+#pragma unroll
+        for (int r = 0; r < NV; r++) {
+          const int a = madr(r, cc);
+          if (lower_only && r < TEAM * s) { col[s][r] = 0.0f; continue; }
+          const float v = L[Ly::M + (a >= 0 ? a : 0)];  // unconditional load: no branch per entry
+          col[s][r] = (c < NV && a >= 0) ? v : 0.0f;
+        }
       }
     }
   }
