@@ -742,8 +742,26 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
     TSYNC();
     float* priv = A.priv + (size_t)e * Lo.priv_size;
     float* obs = A.obs + (size_t)e * Lo.obs_size;
-    for (int k = lane; k < Lo.priv_size; k += TEAM) priv[k] = L[Ly::H + k];
-    for (int k = lane; k < Lo.obs_size; k += TEAM) obs[k] = L[Ly::H + k];
+    // the staged row is read in one batch (compile-time trip count over the largest row), then
+    // stored: one LDS round trip instead of one per element group; obs is the row's prefix
+    constexpr int PMAX = DUCK_OBS_SIZE(NU) + 15 + 3 * NU + 1 + 2 + 6 + 2 + 40 + 1 + 2;
+    constexpr int NKP = (PMAX + TEAM - 1) / TEAM, NKO = (DUCK_OBS_SIZE(NU) + TEAM - 1) / TEAM;
+    float pv[NKP];
+#pragma unroll
+    for (int kk = 0; kk < NKP; kk++) {
+      const int k = lane + TEAM * kk;
+      pv[kk] = L[Ly::H + (k < PMAX ? k : PMAX - 1)];
+    }
+#pragma unroll
+    for (int kk = 0; kk < NKP; kk++) {
+      const int k = lane + TEAM * kk;
+      if (k < Lo.priv_size) priv[k] = pv[kk];
+    }
+#pragma unroll
+    for (int kk = 0; kk < NKO; kk++) {
+      const int k = lane + TEAM * kk;
+      if (k < Lo.obs_size) obs[k] = pv[kk];
+    }
   }
   STAGE_MARK(34);
 }
@@ -810,8 +828,20 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
       STAGE_RESET();
     }
     __syncthreads();
-    if (ej < n)
-      for (int k = threadIdx.x / WG; k < TL::HOT; k += TPB / WG) A.fs[(size_t)k * n + ej] = esj[k];
+    {
+      constexpr int NK = (TL::HOT + TPB / WG - 1) / (TPB / WG);
+      float hv[NK];
+#pragma unroll
+      for (int kk = 0; kk < NK; kk++) {
+        const int k = (int)threadIdx.x / WG + (TPB / WG) * kk;
+        hv[kk] = esj[k < TL::HOT ? k : TL::HOT - 1];
+      }
+#pragma unroll
+      for (int kk = 0; kk < NK; kk++) {
+        const int k = (int)threadIdx.x / WG + (TPB / WG) * kk;
+        if (ej < n && k < TL::HOT) A.fs[(size_t)k * n + ej] = hv[kk];
+      }
+    }
   } else {
     if (e >= n) return;
     const Slice<SW> L = env_slice<Md>(lds, t);
