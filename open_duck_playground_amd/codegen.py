@@ -365,6 +365,7 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
            f"  static constexpr int T_NROOT = {len(root)}, T_NBR = {len(branches)}, T_BRLEN = {brlen}, "
            f"T_BRMD = {int(max(m.body_dofnum[b] for br in branches for b in br))};\n",
            _arr("T_ROOT", root, "int"),
+           _arr("T_BRB", br_arr, "int"),  # [T_NBR][T_BRLEN] limb bodies, -1 past a limb's end
            f"  static constexpr int NBLOB = {len(blob)};\n"] + extra_const + [
            "".join(f"  static constexpr int B_{k.upper()} = {v};\n" for k, v in boff.items())]
     for k, (a, t) in tabs.items():

@@ -488,48 +488,41 @@ struct TPhys {
     TSYNC();
     STAGE_MARK(22);
     // (C) subtree sums of the body forces (rne) and of the body inertias (mj_crb's composite
-    // inertias, which overwrite CIN: phase B has read the body inertias), in one pass
-    float S[6] = {0, 0, 0, 0, 0, 0}, SI[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // inertias, which overwrite CIN: phase B has read the body inertias), a component per lane:
+    // lane k < 6 sums force component k, lane 6 + j inertia component j, down every limb from its
+    // tip (the limb bodies are compile-time, Md::T_BRB), then the limb totals, then the root path.
+    // Each component's additions run in the same order as a limb-per-lane pass.
+    static_assert(TEAM == 6 + 10, "a force or inertia component per lane");
     {
-      float fb[BL][6], C[BL][10];
+      int lk = lane;
+      asm volatile("" : "+v"(lk));  // else the per-lane address selects are hoisted out of the substep
+                                    // loop into registers (+19 AGPRs, -6 % measured)
+      const bool fk = lk < 6;
+      const int src = fk ? RFB + lk : Ly::CIN + (lk - 6), dst = fk ? Ly::CFRC + lk : Ly::CIN + (lk - 6);
+      const int st = fk ? 6 : 10;
+      float tot = 0.0f;
 #pragma unroll
-      for (int d = 0; d < BL; d++) {
-        const int bc = bb[d] >= 0 ? bb[d] : 1;
-        for (int k = 0; k < 6; k++) fb[d][k] = L[RFB + 6 * bc + k];
-        for (int k = 0; k < 10; k++) C[d][k] = L[Ly::CIN + 10 * bc + k];
-      }
+      for (int m = 0; m < Md::T_NBR; m++) {
+        float acc = 0.0f;
 #pragma unroll
-      for (int d = BL - 1; d >= 0; d--) {
-        if (limb && bb[d] >= 0) {
-          for (int k = 0; k < 6; k++) { S[k] += fb[d][k]; L[Ly::CFRC + 6 * bb[d] + k] = S[k]; }
-          for (int k = 0; k < 10; k++) { SI[k] += C[d][k]; L[Ly::CIN + 10 * bb[d] + k] = SI[k]; }
+        for (int d = BL - 1; d >= 0; d--) {
+          const int b = Md::T_BRB[m][d];
+          if (b < 0) continue;
+          acc += L[src + st * b];
+          L[dst + st * b] = acc;
         }
+        tot = m == 0 ? acc : tot + acc;
       }
-    }
-    // only the limb lanes hold sums and only lane 0 uses the total (root stores below): the
-    // reduction over the limb lanes (a quad for <= 4 limbs) is exact against the team sum, whose
-    // other lanes add zeros
-    for (int k = 0; k < 6; k++) S[k] = anc_sum<(1u << Md::T_NBR) - 1u, 0>(S[k]);
-    for (int k = 0; k < 10; k++) SI[k] = anc_sum<(1u << Md::T_NBR) - 1u, 0>(SI[k]);
-    {
-      float fr[NR][6], Rr[NR][10];
-#pragma unroll
-      for (int r = 0; r < NR; r++) {
-        for (int k = 0; k < 6; k++) fr[r][k] = L[RFB + 6 * Md::T_ROOT[r] + k];
-        for (int k = 0; k < 10; k++) Rr[r][k] = L[Ly::CIN + 10 * Md::T_ROOT[r] + k];
-      }
-      TSYNC();
+      STAGE_MARK(35);
 #pragma unroll
       for (int r = NR - 1; r >= 0; r--) {
-        for (int k = 0; k < 6; k++) S[k] += fr[r][k];
-        for (int k = 0; k < 10; k++) SI[k] += Rr[r][k];
-        if (lane == 0) {
-          for (int k = 0; k < 6; k++) L[Ly::CFRC + 6 * Md::T_ROOT[r] + k] = S[k];
-          for (int k = 0; k < 10; k++) L[Ly::CIN + 10 * Md::T_ROOT[r] + k] = SI[k];
-        }
+        const int b = Md::T_ROOT[r];
+        tot += L[src + st * b];
+        L[dst + st * b] = tot;
       }
     }
     TSYNC();
+    STAGE_MARK(36);
     for (int i = lane; i < NV; i += TEAM) {
       const int b = dof_body(i);
       float s = 0.0f;

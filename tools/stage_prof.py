@@ -18,7 +18,7 @@ from open_duck_playground_amd.joystick import Joystick, wrap_for_brax_training  
 
 TOP = {0: "kinematics", 1: "com_pos", 2: "rne", 3: "crb", 28: "smooth (actuation, damping)",
        4: "qacc_smooth solve", 5: "collision", 6: "make_rows", 7: "solve", 8: "sensors+euler"}
-SUB = {24: "kinematics:local", 21: "rne:A vel/acc", 22: "rne:A+B forces", 19: "crb:inertia sums",
+SUB = {24: "kinematics:local", 21: "rne:A vel/acc", 22: "rne:A+B forces", 35: "rne:C limb sums", 36: "rne:C root sums", 19: "crb:inertia sums",
        26: "collision:floor", 20: "solve:load M cols", 25: "solve:warm J,M products", 9: "solve:warm costs+select", 10: "solve:newton_dir", 16: "  newton:grad+diag",
        17: "  newton:+J'DJ", 18: "  newton:+factor_solve", 11: "solve:(dense fallback)", 12: "solve:jmul+mulM",
        13: "solve:linesearch"}
