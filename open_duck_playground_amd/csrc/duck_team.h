@@ -543,8 +543,13 @@ struct TPhys {
                                                           // initialised by the launch)
     // M row i (lane i, i + 16): F_i = crb_{body(i)} cdof_i stays in registers;
     // M[i][j] = cdof_j . F_i over the ancestors j of i (the row is contiguous in M)
+    // a last column set of at most 4 rows takes 4 lanes per row, each lane a quarter of the row's
+    // entries (otherwise 4 lanes do the whole set's work while 12 idle)
+    constexpr int RT = NV - TEAM * (NC - 1);
+    constexpr bool SPLIT = NC >= 2 && RT <= 4;
+    constexpr int NS = SPLIT ? NC - 1 : NC;
 #pragma unroll
-    for (int s = 0; s < NC; s++) {
+    for (int s = 0; s < NS; s++) {
       const int i = TEAM * s + lane, ic = i < NV ? i : 0;
       float cd[6], F[6], I[10];
       for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * ic + k];
@@ -572,6 +577,34 @@ struct TPhys {
         // branchless store (a masked region per entry costs more than the select)
         const bool ok = i < NV && jj[q] >= 0;
         L[ok ? Ly::M + rs + q : TL::SINK + lane] = v + (jj[q] == i ? arm : 0.0f);
+      }
+    }
+    if constexpr (SPLIT) {
+      int lr = lane;
+      asm volatile("" : "+v"(lr));  // the per-lane row/entry split stays inside the substep
+      const int i = TEAM * (NC - 1) + (lr >> 2), sub = lr & 3;
+      const bool okr = i < NV;
+      const int ic = okr ? i : 0;
+      float cd[6], F[6], I[10];
+      for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * ic + k];
+      const int bi = dof_body(ic);
+      for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * bi + k];
+      const float arm = L[Ly::DARM + ic];
+      const int rs = ti(Md::B_MROW + ic);
+      mul_inert_vec(F, I, cd);
+#pragma unroll
+      for (int t = 0; t < (MC + 3) / 4; t++) {
+        const int q = sub + 4 * t;
+        const bool okq = q < MC;
+        const int qc = okq ? q : 0;
+        const int j = ti(Md::B_DCHAIN + MC * ic + qc), jc = j >= 0 ? j : 0;
+        float cj[6];
+        for (int k = 0; k < 6; k++) cj[k] = L[Ly::CDOF + 6 * jc + k];
+        float v = 0.0f;
+        for (int k = 0; k < 6; k++) v += cj[k] * F[k];
+        if (FREE0) v = qc < 3 ? (qc == 0 ? F[3] : (qc == 1 ? F[4] : F[5])) : v;  // cdof_q = e_{3+q}
+        const bool ok = okr && okq && j >= 0;
+        L[ok ? Ly::M + rs + qc : TL::SINK + lr] = v + (j == i ? arm : 0.0f);
       }
     }
     TSYNC();
