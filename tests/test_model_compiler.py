@@ -90,3 +90,42 @@ def test_edited_scenes_are_reproducible_from_the_xml():
     with tempfile.TemporaryDirectory() as td:
         m = compile_mjcf(B.edited_scene(td, [], []), timestep=0.002)
     assert model_fingerprint(m) == model_fingerprint(Model.load(constants.task_to_xml("flat_terrain")))
+
+
+def _header_tables(variant):
+    """The blob and the scalar constants of a generated model header (codegen.model_header)."""
+    import re
+    txt = open(os.path.join(native.CSRC, "generated", f"duck_model_{variant}.h")).read()
+    blob = np.array([int(x) for x in re.search(r"_blob\[\d+\] = \{([^}]*)\}", txt).group(1).split(",")])
+    const = {k: int(v) for k, v in re.findall(r"\b([A-Z][A-Z0-9_]*) = (-?\d+)", txt)}
+    brb = re.search(r"T_BRB\[(\d+)\]\[(\d+)\] = \{(.*?)\};", txt)
+    nbr, brlen = int(brb.group(1)), int(brb.group(2))
+    t_brb = np.array([int(x) for x in re.findall(r"-?\d+", brb.group(3))]).reshape(nbr, brlen)
+    return blob, const, t_brb
+
+
+@pytest.mark.parametrize("variant", ["flat", "backlash", "rough", "rough_backlash"])
+def test_register_column_table_points_outside_entries_at_the_zero_word(variant):
+    """load_cols' per-lane table (codegen mcolz): entry (s, r, lane) is M's address of (row r,
+    column 16 s + lane) where the tree pattern has one, else NM, the zero word after M."""
+    blob, c, _ = _header_tables(variant)
+    nv, nm = c["NV"], c["NM"]
+    nc = (nv + 15) // 16
+    madr = blob[c["B_MADR"]:c["B_MADR"] + nv * nv].reshape(nv, nv)
+    mcolz = blob[c["B_MCOLZ"]:c["B_MCOLZ"] + nc * nv * 16].reshape(nc, nv, 16)
+    for s in range(nc):
+        for r in range(nv):
+            for ln in range(16):
+                col = 16 * s + ln
+                want = madr[r, col] if col < nv and madr[r, col] >= 0 else nm
+                assert mcolz[s, r, ln] == want, (s, r, ln)
+    assert sorted(set(madr[madr >= 0].tolist())) == list(range(nm))  # every M entry addressed once per pair
+
+
+@pytest.mark.parametrize("variant", ["flat", "backlash", "rough", "rough_backlash"])
+def test_compile_time_limb_bodies_match_the_blob(variant):
+    """rne's component-per-lane subtree sums walk Md::T_BRB; the other passes read the blob's copy."""
+    blob, c, t_brb = _header_tables(variant)
+    nbr, brlen = t_brb.shape
+    assert nbr == c["T_NBR"] and brlen == c["T_BRLEN"]
+    assert (blob[c["B_BR"]:c["B_BR"] + nbr * brlen].reshape(nbr, brlen) == t_brb).all()
