@@ -318,26 +318,14 @@ struct TPhys {
   // ---------------- mj_comPos: subtree com (team reduction), cinert, cdof ----------------
   static DK void com_pos(LP L, int lane) {
 #pragma clang fp reassociate(on)
-    float ms = 0.0f, cx = 0.0f, cy = 0.0f, cz = 0.0f;
-    for (int b = 1 + lane; b < NB; b += TEAM) {
-      if (!moving(b)) continue;
-      float R[9], t[3], ip[3];
-      for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
-      for (int k = 0; k < 3; k++) ip[k] = (b == 1) ? L[Ly::DIPOS + k] : tf(Md::B_BINERT + 17 * b + k);
-      mulmv3(t, R, ip);
-      const float m = L[Ly::DMASS + b];
-      ms += m;
-      cx += m * (L[Ly::XPOS + 3 * b] + t[0]);
-      cy += m * (L[Ly::XPOS + 3 * b + 1] + t[1]);
-      cz += m * (L[Ly::XPOS + 3 * b + 2] + t[2]);
-    }
-    ms = tsum(ms);
-    const float inv = frcp(ms);
-    const float com[3] = {tsum(cx) * inv, tsum(cy) * inv, tsum(cz) * inv};
-    if (lane == 0)
-      for (int k = 0; k < 3; k++) L[Ly::COM + k] = com[k];
-    for (int b = 1 + lane; b < NB; b += TEAM) {
-      if (!moving(b)) continue;
+    // every moving body fits the team (a body per lane): its inertial frame (xipos, the rotated
+    // inertia) is formed once, held across the subtree-com reduction, and only the offset from the
+    // com is applied after it
+    static_assert((moving_mask() >> (1 + TEAM)) == 0, "a moving body per lane");
+    float xi[3] = {0, 0, 0}, rot[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, m = 0.0f;
+    const int b = 1 + lane;
+    const bool mv = b < NB && moving(b);
+    if (mv) {
       const int ob = Md::B_BINERT + 17 * b;
       float R[9], t[3], ip[3], Ri[9], Bi[9];
       for (int k = 0; k < 9; k++) R[k] = L[Ly::XMAT + 9 * b + k];
@@ -346,13 +334,20 @@ struct TPhys {
       mulmv3(t, R, ip);
       mulmm3(Ri, R, Bi);
       const float I[3] = {tf(ob + 12), tf(ob + 13), tf(ob + 14)};
-      float rot[9];
       for (int a = 0; a < 3; a++)
         for (int c = 0; c < 3; c++)
           rot[3 * a + c] = Ri[3 * a] * I[0] * Ri[3 * c] + Ri[3 * a + 1] * I[1] * Ri[3 * c + 1] + Ri[3 * a + 2] * I[2] * Ri[3 * c + 2];
-      const float d[3] = {L[Ly::XPOS + 3 * b] + t[0] - com[0], L[Ly::XPOS + 3 * b + 1] + t[1] - com[1],
-                          L[Ly::XPOS + 3 * b + 2] + t[2] - com[2]};
-      const float m = L[Ly::DMASS + b], dd = dot3(d, d);
+      for (int k = 0; k < 3; k++) xi[k] = L[Ly::XPOS + 3 * b + k] + t[k];
+      m = L[Ly::DMASS + b];
+    }
+    const float ms = tsum(m);
+    const float inv = frcp(ms);
+    const float com[3] = {tsum(m * xi[0]) * inv, tsum(m * xi[1]) * inv, tsum(m * xi[2]) * inv};
+    if (lane == 0)
+      for (int k = 0; k < 3; k++) L[Ly::COM + k] = com[k];
+    if (mv) {
+      const float d[3] = {xi[0] - com[0], xi[1] - com[1], xi[2] - com[2]};
+      const float dd = dot3(d, d);
       const int o = Ly::CIN + 10 * b;
       L[o + 0] = rot[0] + m * (dd - d[0] * d[0]);
       L[o + 1] = rot[4] + m * (dd - d[1] * d[1]);
