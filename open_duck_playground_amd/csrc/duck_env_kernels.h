@@ -1009,8 +1009,8 @@ static int stage_cycles_of(unsigned long long* out, int reset) {
   for (int k = 0; k < DUCK_NSTAGE && e == hipSuccess; k++)
     for (int b = 0; b < 256; b++) out[k] += wg[k * 256 + b];
   if (e == hipSuccess && reset) {
-    static unsigned long long z[DUCK_NSTAGE + 3 * 1024] = {0};
-    e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, sizeof(z));
+    static unsigned long long z[DUCK_NSTAGE * 256 > DUCK_NSTAGE + 3 * 1024 ? DUCK_NSTAGE * 256 : DUCK_NSTAGE + 3 * 1024] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, sizeof(unsigned long long) * (DUCK_NSTAGE + 3 * 1024));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_wg), z, sizeof(wg));
   }
   return e == hipSuccess ? 0 : DUCK_EHIP;
