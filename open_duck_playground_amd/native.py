@@ -38,6 +38,31 @@ class DuckLayout(C.Structure):
         "rng_key", "rng_ctr", "step", "push_step", "push_interval", "imitation_i", "ep_steps", "nint")]
 
 
+# the machine scheduler's max-ILP strategy: the step kernel runs one wave per SIMD, so
+# occupancy-driven scheduling buys nothing and latency hiding must come from the wave's own
+# instruction stream (same-box A/B: +3 % env-steps/s). Every unit uses it; the build is
+# gated by tools/isa_exec_check.py, which rejects the register-allocation fault that once made
+# the rough + backlash physics_kernel compute a wrong Newton step.
+ILP_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+
+
+def _base_flags(inc: str) -> list:
+    # fp32 division and sqrt as v_rcp/v_sqrt (1-2 ulp) instead of the correctly rounded
+    # multi-instruction sequences: the physics tolerances are fp32-vs-fp64 anyway; fp32
+    # denormals flushed (no frexp/ldexp range scaling around v_rcp/v_sqrt/sincos); x/y as
+    # x*rcp(y) and signed zeros ignored (+0.8 % same-box, parity unchanged) -- NaN/Inf stay
+    # honoured: the termination check and the auto-reset NaN guard depend on them
+    return ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-hip-fp32-correctly-rounded-divide-sqrt",
+            "-fgpu-flush-denormals-to-zero", "-fno-slp-vectorize",
+            "-fno-signed-zeros", "-fno-trapping-math", "-fno-math-errno", "-freciprocal-math", "-I" + CSRC,
+            "-I" + inc]
+
+
+def compile_flags() -> list:
+    """The hipcc flags of the shipped scene units (tools: occupancy_probe.sh, ISA studies)."""
+    return _base_flags(os.path.join(CSRC, "generated")) + ILP_FLAGS
+
+
 def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no_ilp=(), isa_check: bool = True,
           gen_dir: str = None) -> str:
     """Compile libduck.so for gfx950 with hipcc (in-tree, so it travels with the repo).
@@ -61,22 +86,8 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no
         return out
     import hashlib
     import tempfile
-    # fp32 division and sqrt as v_rcp/v_sqrt (1-2 ulp) instead of the correctly rounded
-    # multi-instruction sequences: the physics tolerances are fp32-vs-fp64 anyway; fp32
-    # denormals flushed (no frexp/ldexp range scaling around v_rcp/v_sqrt/sincos); x/y as
-    # x*rcp(y) and signed zeros ignored (+0.8 % same-box, parity unchanged) -- NaN/Inf stay
-    # honoured: the termination check and the auto-reset NaN guard depend on them
-    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-hip-fp32-correctly-rounded-divide-sqrt",
-             "-fgpu-flush-denormals-to-zero", "-fno-slp-vectorize",
-             "-fno-signed-zeros", "-fno-trapping-math", "-fno-math-errno", "-freciprocal-math", "-I" + CSRC,
-             "-I" + inc] + \
-        [f"-D{d}" for d in defines] + list(extra_flags)
-    # the machine scheduler's max-ILP strategy: the step kernel runs one wave per SIMD, so
-    # occupancy-driven scheduling buys nothing and latency hiding must come from the wave's own
-    # instruction stream (same-box A/B: +3 % env-steps/s). Every unit uses it; the build is
-    # gated by tools/isa_exec_check.py, which rejects the register-allocation fault that once made
-    # the rough + backlash physics_kernel compute a wrong Newton step.
-    ilp = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+    flags = _base_flags(inc) + [f"-D{d}" for d in defines] + list(extra_flags)
+    ilp = ILP_FLAGS
     # build id: sha1 of every source, header and flag that shapes the code (duck_build_id()); the
     # .so itself is not byte-reproducible (object paths), so profiles are keyed by this instead
     h = hashlib.sha1(" ".join(flags + ilp + sorted(no_ilp)).encode())
