@@ -841,22 +841,27 @@ struct TPhys {
     }
   }
 
-  // DST = sign * M^-1 SRC (M tree-sparse SPD, M_adr pattern)
-  static DK void solve_regs(LP L, int lane, int SRC, int DST, float sign) {
+  // qacc_smooth = M^-1 qfrc_smooth (mj_solveM) from the solver's register columns of M: the factor
+  // works on a copy (it reads only the lower triangle) and Mc stays for every M.x of the solver,
+  // so M is loaded from LDS once per substep
+  static DK void smooth_acc(LP L, int lane, const float (*Mc)[NV]) {
     Fac F;
-    load_cols(L, lane, F.col, true);
+#pragma unroll
+    for (int s = 0; s < NC; s++)
+#pragma unroll
+      for (int r = 0; r < NV; r++) F.col[s][r] = Mc[s][r];
     float x[NC];
 #pragma unroll
     for (int s = 0; s < NC; s++) {
       const int c = TEAM * s + lane;
-      const float v = L[SRC + (c < NV ? c : 0)];
+      const float v = L[Ly::FSM + (c < NV ? c : 0)];
       x[s] = c < NV ? v : 0.0f;
     }
     factor_solve(F, x, lane);
 #pragma unroll
     for (int s = 0; s < NC; s++) {
       const int c = TEAM * s + lane;
-      if (c < NV) L[DST + c] = sign * x[s];
+      if (c < NV) L[Ly::QSM + c] = x[s];
     }
     TSYNC();
   }
@@ -1723,12 +1728,9 @@ struct TPhys {
 
   // mjx solver.solve: warm-start choice, then Md::iterations Newton steps (the Open Duck scenes
   // use 1; a model compiled with more iterates to the MJX stopping rule on the cost improvement)
-  static DK void solve(LP L, int lane, float* scratch, int stride) {
+  // Mc: M as full symmetric columns in registers for every M.x of the solver
+  static DK void solve(LP L, int lane, float* scratch, int stride, const float (*Mc)[NV]) {
     STAGE_T0();
-    // M as full symmetric columns in registers for every M.x of the solver
-    float Mc[NC][NV];
-    load_cols(L, lane, Mc, false);
-    STAGE_MARK(20);
     // warm start vs smooth acceleration: J and M products of both in one pass
     // (M qacc_smooth = qfrc_smooth by definition: no product needed for the smooth start)
     spatial2(L, lane, Ly::WARM, Ly::QSM);
@@ -2077,13 +2079,20 @@ struct TPhys {
     STAGE_MARK(3);
     smooth(L, lane);
     STAGE_MARK(28);
-    solve_regs(L, lane, Ly::FSM, Ly::QSM, 1.0f);
-    STAGE_MARK(4);
+    // collision and the constraint rows depend on the kinematics only: they run before the
+    // smooth acceleration so that M is loaded into registers once for both solves
     collision(L, lane, hf);
     STAGE_MARK(5);
     make_rows(L, lane);
     STAGE_MARK(6);
-    solve(L, lane, scratch, sstride);
+    {
+      float Mc[NC][NV];
+      load_cols(L, lane, Mc, false);
+      STAGE_MARK(20);
+      smooth_acc(L, lane, Mc);
+      STAGE_MARK(4);
+      solve(L, lane, scratch, sstride, Mc);
+    }
     STAGE_MARK(7);
     if (want_out) {
       sensors(L, lane);
