@@ -109,8 +109,7 @@ template <class Md>
 struct TLay {
   using Ly = Lay<Md>;
   static constexpr int KC = Ly::TOTAL;                 // K.cdof per chain dof (6 x MAXCHAIN)
-  static constexpr int TSP = KC + 6 * Md::MAXCHAIN;    // foot spatial motions (2 x 12)
-  static constexpr int USED = TSP + 24;
+  static constexpr int USED = KC + 6 * Md::MAXCHAIN;
   static constexpr int STRIDE = ((USED + 15) / 32) * 32 + 16;  // = 16 (mod 32), >= USED
   static_assert(STRIDE >= USED && STRIDE % 32 == 16, "stride");
   static constexpr int FTMP = Ly::JA;                  // crb: F_i = I_b cdof_i (dead row storage)
@@ -890,6 +889,26 @@ struct TPhys {
     return msk;
   }
 
+  // H[r][c] += kc_r . cdof_c for the chain rows r on or below the diagonal block of each column set
+  // (kc_r read from lane r % TEAM of set r / TEAM); kc_r = 0 off the chain
+  template <int R>
+  static DK void jdj_row(Fac& F, const float (*kc)[6], const float (*cdc)[6], const bool* in, unsigned msk) {
+    if (!((msk >> R) & 1u)) return;  // compile-time after unrolling (msk is the side's constant)
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      if (R < TEAM * s) continue;
+      if (FREE0 && R < 3) { F.col[s][R] += kc[s][3 + R]; continue; }  // cdof_r = e_{3+r}
+      float h = 0.0f;
+      for (int k = 0; k < 6; k++) h += bc<R % TEAM>(kc[R / TEAM][k]) * cdc[s][k];
+      F.col[s][R] += in[s] ? h : 0.0f;  // (entries right of the diagonal are dropped after the factorization)
+    }
+  }
+  template <int... R>
+  static DK void jdj_rows(Fac& F, const float (*kc)[6], const float (*cdc)[6], const bool* in, unsigned msk,
+                          std::integer_sequence<int, R...>) {
+    (jdj_row<R>(F, kc, cdc, in, msk), ...);
+  }
+
   // Newton direction at (QACC, JA, MA) with H = M + J'DJ assembled directly into register
   // columns (mjx _update_gradient + the Cholesky solve): SRCH = -H^-1 grad. Returns false
   // (nothing written) when foot/foot contact rows are active.
@@ -983,30 +1002,26 @@ struct TPhys {
       for (int k = 0; k < 6; k++) Fv[k] = side == 0 ? bc<0>(Fh[k]) : bc<8>(Fh[k]);
       constexpr unsigned MASKL = chain_mask(Md::LFOOT_BODY), MASKR = chain_mask(Md::RFOOT_BODY);
       const unsigned msk = foot == 1 ? MASKL : MASKR;
+      // kc_c = K cdof_c for both column sets first: H[r][c] += cdof_r . K cdof_c = kc_r . cdof_c
+      // (K symmetric) takes kc_r from lane r by a DPP row broadcast folded into the FMA, instead of
+      // reloading cdof_r from LDS in every lane
+      float cdc[NC][6], kc[NC][6];
+      bool in[NC];
 #pragma unroll
       for (int s = 0; s < NC; s++) {
         const int c = TEAM * s + lane, cc = c < NV ? c : 0;
-        const bool in = c < NV && ((msk >> cc) & 1u);
-        float cdc[6], kc[6];
-        for (int k = 0; k < 6; k++) cdc[k] = L[Ly::CDOF + 6 * cc + k];
+        in[s] = c < NV && ((msk >> cc) & 1u);
+        for (int k = 0; k < 6; k++) cdc[s][k] = L[Ly::CDOF + 6 * cc + k];
         float gf = 0.0f;
         for (int q = 0; q < 6; q++) {
           float sacc = 0.0f;
-          for (int k = 0; k < 6; k++) sacc += K[kidx(q, k)] * cdc[k];
-          kc[q] = in ? sacc : 0.0f;
-          gf += cdc[q] * Fv[q];
+          for (int k = 0; k < 6; k++) sacc += K[kidx(q, k)] * cdc[s][k];
+          kc[s][q] = in[s] ? sacc : 0.0f;
+          gf += cdc[s][q] * Fv[q];
         }
-        g[s] -= in ? gf : 0.0f;
-        // H[r][c] += cdof_r . K cdof_c for chain rows r >= c (kc = 0 off the chain)
-#pragma unroll
-        for (int r = 0; r < NV; r++) {
-          if (!((msk >> r) & 1u) || r < TEAM * s) continue;  // compile-time: chain rows on or below the diagonal
-          if (FREE0 && r < 3) { F.col[s][r] += kc[3 + r]; continue; }  // cdof_r = e_{3+r}
-          float h = 0.0f;
-          for (int k = 0; k < 6; k++) h += L[Ly::CDOF + 6 * r + k] * kc[k];
-          F.col[s][r] += h;  // (entries right of the diagonal are dropped after the factorization)
-        }
+        g[s] -= in[s] ? gf : 0.0f;
       }
+      jdj_rows(F, kc, cdc, in, msk, std::make_integer_sequence<int, NV>{});
     }
     if constexpr (FF) {
       if constexpr (Md::FOOT_PAIR >= 0) {
@@ -1639,8 +1654,11 @@ struct TPhys {
   struct Pt { float alpha, q0p, q1, q2, d0, d1; };
 
   // ---- fused solver passes ----
-  // foot spatial motions only (lanes 0-11): X into TSP[0..11], X2 (if >= 0) into TSP[12..23]
-  static DK void spatial2(LP L, int lane, int X, int X2) {
+  // foot spatial motions only: component lane of X (lanes 0-11: left foot 0-5, right foot 6-11)
+  // into so, of X2 (if >= 0) into so2; consumers take them by DPP row broadcasts (no LDS round trip)
+  static DK void spatial2(LP L, int lane, int X, int X2, float& so, float& so2) {
+    so = 0.0f;
+    so2 = 0.0f;
     if (lane < 12) {
       // the feet's dof chains are compile-time (Md::chain): at each chain position the lane only
       // selects the left or right foot's dof, so no index words are loaded and the products of
@@ -1672,9 +1690,15 @@ struct TPhys {
         s += cd * L[X + ic];
         if (X2 >= 0) s2 += cd * L[X2 + ic];
       }
-      L[TL::TSP + lane] = s;
-      if (X2 >= 0) L[TL::TSP + 12 + lane] = s2;
+      so = s;
+      so2 = s2;
     }
+  }
+
+  // SL[k] = component k of the left foot's motion (lane k), SR[k] the right foot's (lane 6 + k)
+  static DK void sp_bcast(float v, float* SL, float* SR) {
+    SL[0] = bc<0>(v); SL[1] = bc<1>(v); SL[2] = bc<2>(v); SL[3] = bc<3>(v); SL[4] = bc<4>(v); SL[5] = bc<5>(v);
+    SR[0] = bc<6>(v); SR[1] = bc<7>(v); SR[2] = bc<8>(v); SR[3] = bc<9>(v); SR[4] = bc<10>(v); SR[5] = bc<11>(v);
   }
 
   static DK float fric_cost(float D, float x, float f) {
@@ -1733,9 +1757,14 @@ struct TPhys {
     STAGE_T0();
     // warm start vs smooth acceleration: J and M products of both in one pass
     // (M qacc_smooth = qfrc_smooth by definition: no product needed for the smooth start)
-    spatial2(L, lane, Ly::WARM, Ly::QSM);
+    float sw, ss;
+    spatial2(L, lane, Ly::WARM, Ly::QSM, sw, ss);
     mul_cols(L, lane, Mc, Ly::WARM, Ly::MA);
     TSYNC();
+    // the feet's spatial motions, broadcast with the full team active (before any lane region)
+    float SL[6], SR[6], SL2[6], SR2[6];
+    sp_bcast(sw, SL, SR);
+    sp_bcast(ss, SL2, SR2);
     STAGE_MARK(25);
     float cwp = 0.0f, csp = 0.0f, gwp = 0.0f;
     {
@@ -1759,11 +1788,7 @@ struct TPhys {
       L[Ly::JV + row] = js;
     }
     if (lane < NCON) {
-      float SL[6], SR[6], SL2[6], SR2[6], vw[4], vs[4];
-      for (int k = 0; k < 6; k++) {
-        SL[k] = L[TL::TSP + k]; SR[k] = L[TL::TSP + 6 + k];
-        SL2[k] = L[TL::TSP + 12 + k]; SR2[k] = L[TL::TSP + 18 + k];
-      }
+      float vw[4], vs[4];
       contact_jx(L, lane >> 2, lane, SL, SR, vw);
       contact_jx(L, lane >> 2, lane, SL2, SR2, vs);
       for (int e = 0; e < 4; e++) {
@@ -1807,7 +1832,8 @@ struct TPhys {
       TSYNC();
     }
     // J.search and M.search in one pass; rows go straight to registers
-    spatial2(L, lane, Ly::SRCH, -1);
+    float sv, sv2;
+    spatial2(L, lane, Ly::SRCH, -1, sv, sv2);
     mul_cols(L, lane, Mc, Ly::SRCH, Ly::GRAD);
     TSYNC();
     Rows2 R;
@@ -1828,7 +1854,7 @@ struct TPhys {
     {
       float SL[6], SR[6], v[4];
       const int slot = lane < NCON ? lane : 0;
-      for (int k = 0; k < 6; k++) { SL[k] = L[TL::TSP + k]; SR[k] = L[TL::TSP + 6 + k]; }
+      sp_bcast(sv, SL, SR);
       contact_jx(L, slot >> 2, slot, SL, SR, v);
       for (int e = 0; e < 4; e++) {
         const int row = R_CON + 4 * slot + e;
