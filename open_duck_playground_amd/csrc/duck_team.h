@@ -865,21 +865,30 @@ struct TPhys {
     TSYNC();
   }
 
-  // y = M x for the lane's columns (M held as full columns, x read by broadcast); Y[c] = y
-  static DK void mul_cols(LP L, int lane, const float (*Mc)[NV], int X, int Y) {
+  // y = M x for the lane's columns (M held as full columns); Y[c] = y. x[s] holds x_c of the lane's
+  // columns c = TEAM s + lane; x_r reaches every lane by a DPP row broadcast folded into the FMA
+  template <int... R>
+  static DK void mul_acc(const float (*Mc)[NV], const float* x, float* y, std::integer_sequence<int, R...>) {
+#pragma unroll
+    for (int s = 0; s < NC; s++) ((y[s] += Mc[s][R] * bc<R % TEAM>(x[R / TEAM])), ...);
+  }
+  static DK void mul_cols(LP L, int lane, const float (*Mc)[NV], const float* x, int Y) {
     float y[NC];
 #pragma unroll
     for (int s = 0; s < NC; s++) y[s] = 0.0f;
-#pragma unroll
-    for (int r = 0; r < NV; r++) {
-      const float xr = L[X + r];
-#pragma unroll
-      for (int s = 0; s < NC; s++) y[s] += Mc[s][r] * xr;
-    }
+    mul_acc(Mc, x, y, std::make_integer_sequence<int, NV>{});
 #pragma unroll
     for (int s = 0; s < NC; s++) {
       const int c = TEAM * s + lane;
       if (c < NV) L[Y + c] = y[s];
+    }
+  }
+  // the lane's entries x[s] = X[TEAM s + lane] of an LDS vector
+  static DK void lane_vec(LP L, int lane, int X, float* x) {
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane;
+      x[s] = L[X + (c < NV ? c : 0)];
     }
   }
 
@@ -1759,7 +1768,11 @@ struct TPhys {
     // (M qacc_smooth = qfrc_smooth by definition: no product needed for the smooth start)
     float sw, ss;
     spatial2(L, lane, Ly::WARM, Ly::QSM, sw, ss);
-    mul_cols(L, lane, Mc, Ly::WARM, Ly::MA);
+    {
+      float xw[NC];
+      lane_vec(L, lane, Ly::WARM, xw);
+      mul_cols(L, lane, Mc, xw, Ly::MA);
+    }
     TSYNC();
     // the feet's spatial motions, broadcast with the full team active (before any lane region)
     float SL[6], SR[6], SL2[6], SR2[6];
@@ -1834,7 +1847,11 @@ struct TPhys {
     // J.search and M.search in one pass; rows go straight to registers
     float sv, sv2;
     spatial2(L, lane, Ly::SRCH, -1, sv, sv2);
-    mul_cols(L, lane, Mc, Ly::SRCH, Ly::GRAD);
+    {
+      float xs[NC];
+      lane_vec(L, lane, Ly::SRCH, xs);
+      mul_cols(L, lane, Mc, xs, Ly::GRAD);
+    }
     TSYNC();
     Rows2 R;
     {
