@@ -2,7 +2,7 @@
 """Per-stage cycle breakdown of step_kernel (needs a -DDUCK_STAGE_PROF build in DUCK_LIB).
 
 Counters are wave-0 clock64 deltas summed over workgroups; printed per substep per wave.
-Top-level stages (they partition a substep): 0-8 and 28. Sub-stage counters measure from
+Top-level stages (they partition a substep): 0-8, 20 and 28. Sub-stage counters measure from
 the start of their parent stage: 9-13 solve, 16-18 newton direction, 19 crb limb/root
 sums, 21/22 rne passes A/B, 24 kinematics local transforms, 26 floor collision.
 """
@@ -17,9 +17,10 @@ from open_duck_playground_amd import native  # noqa: E402
 from open_duck_playground_amd.joystick import Joystick, wrap_for_brax_training  # noqa: E402
 
 TOP = {0: "kinematics", 1: "com_pos", 2: "rne", 3: "crb", 28: "smooth (actuation, damping)",
-       4: "qacc_smooth solve", 5: "collision", 6: "make_rows", 7: "solve", 8: "sensors+euler"}
+       5: "collision", 6: "make_rows", 20: "M columns -> registers", 4: "qacc_smooth solve", 7: "solve",
+       8: "sensors+euler"}
 SUB = {24: "kinematics:local", 21: "rne:A vel/acc", 22: "rne:A+B forces", 35: "rne:C limb sums", 36: "rne:C root sums", 19: "crb:inertia sums",
-       26: "collision:floor", 20: "solve:load M cols", 25: "solve:warm J,M products", 9: "solve:warm costs+select", 10: "solve:newton_dir", 16: "  newton:grad+diag",
+       26: "collision:floor", 25: "solve:warm J,M products", 9: "solve:warm costs+select", 10: "solve:newton_dir", 16: "  newton:grad+diag",
        17: "  newton:+J'DJ", 18: "  newton:+factor_solve", 11: "solve:(dense fallback)", 12: "solve:jmul+mulM",
        13: "solve:linesearch"}
 NSTAGE = 48  # DUCK_NSTAGE
