@@ -276,6 +276,13 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         d2l[m.jnt_dofadr[j]] = r
     put("dof2fric", d2f)
     put("dof2lim", d2l)
+    # when the friction / limit rows cover consecutive dofs (the Open Duck scenes: the 14 hinges), the
+    # row <-> dof maps are affine and the kernels compute them instead of loading index words (widths,
+    # not offsets: B_FRIC0 / B_LIM0 = the first dof, or -1 for the table form)
+    lim_dofs = [int(m.jnt_dofadr[j]) for j in lim]
+    affine = lambda d: d[0] if d and d == list(range(d[0], d[0] + len(d))) else -1
+    boff["fric0"] = affine([int(i) for i in fric])
+    boff["lim0"] = affine(lim_dofs)
     # flattened tree recursions: per body its dof chain and its subtree, per body the local
     # kinematics record, per dof its body / parent body / first dof of its body / free flag
     mc = maxchain_of(m)

@@ -186,8 +186,24 @@ struct TPhys {
   }
   static DK float tf(int off) { return __int_as_float(ti(off)); }
   static constexpr int LIMW = 13, PAIRW = 13;
-  static DK int fric_dof(int r) { return ti(Md::B_FRIC + 3 * r); }
-  static DK int lim_dof(int r) { return ti(Md::B_LIM + LIMW * r); }
+  // row -> dof and dof -> row maps of the friction and limit rows: affine when the rows cover
+  // consecutive dofs (codegen B_FRIC0 / B_LIM0 >= 0), else index words of the model blob
+  static DK int fric_dof(int r) {
+    if constexpr (Md::B_FRIC0 >= 0) return Md::B_FRIC0 + r;
+    else return ti(Md::B_FRIC + 3 * r);
+  }
+  static DK int lim_dof(int r) {
+    if constexpr (Md::B_LIM0 >= 0) return Md::B_LIM0 + r;
+    else return ti(Md::B_LIM + LIMW * r);
+  }
+  static DK int dof_fric(int c) {
+    if constexpr (Md::B_FRIC0 >= 0) return (c >= Md::B_FRIC0 && c < Md::B_FRIC0 + NFRIC) ? c - Md::B_FRIC0 : -1;
+    else return ti(Md::B_DOF2FRIC + c);
+  }
+  static DK int dof_lim(int c) {
+    if constexpr (Md::B_LIM0 >= 0) return (c >= Md::B_LIM0 && c < Md::B_LIM0 + NLIM) ? c - Md::B_LIM0 : -1;
+    else return ti(Md::B_DOF2LIM + c);
+  }
   static DK int madr(int i, int j) { return ti(Md::B_MADR + NV * i + j); }
   // lane-indexed model constants live in the LDS blob (codegen.team_tables records)
   // dofs 0-2 are the translational dofs of the trunk's free joint: their motion axes (cdof rows,
@@ -942,7 +958,7 @@ struct TPhys {
       const bool valid = c < NV;
       float gr = L[Ly::MA + cc] - L[Ly::FSM + cc], diag = 0.0f;
       // friction row of dof c (Huber cost): force and quadratic-zone curvature
-      const int fr = ti(Md::B_DOF2FRIC + cc), frc = fr >= 0 ? fr : 0;
+      const int fr = dof_fric(cc), frc = fr >= 0 ? fr : 0;
       {
         const float D = L[Ly::RD + frc], x = L[Ly::JA + frc], f = L[Ly::DFRIC + cc], rf = f * frcp(D);
         const float force = x <= -rf ? f : (x >= rf ? -f : -D * x);
@@ -951,7 +967,7 @@ struct TPhys {
         diag += (fr >= 0 && quad) ? D : 0.0f;
       }
       // joint-limit row of dof c (one-sided)
-      const int lr = ti(Md::B_DOF2LIM + cc), lrc = lr >= 0 ? lr : 0;
+      const int lr = dof_lim(cc), lrc = lr >= 0 ? lr : 0;
       {
         const float D = L[Ly::RD + R_LIM + lrc], x = L[Ly::JA + R_LIM + lrc], sg = L[Ly::LSGN + lrc];
         const bool act = lr >= 0 && x < 0.0f;
