@@ -245,6 +245,8 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         R = max(float(m.dof_invweight0[i]) * (1 - imp) / imp, 1e-15)
         rec += [i, f2i(1.0 / R), f2i(b_)]
     put("fric", rec)  # stride 3: dof, D, b
+    # d[0] when the list is d[0], d[0] + 1, ... (an affine map from its index), else -1
+    affine = lambda d: d[0] if d and d == list(range(d[0], d[0] + len(d))) else -1
     lim = [j for j in range(m.njnt) if m.jnt_limited[j]]
     rec = []
     for j in lim:
@@ -280,7 +282,6 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     # row <-> dof maps are affine and the kernels compute them instead of loading index words (widths,
     # not offsets: B_FRIC0 / B_LIM0 = the first dof, or -1 for the table form)
     lim_dofs = [int(m.jnt_dofadr[j]) for j in lim]
-    affine = lambda d: d[0] if d and d == list(range(d[0], d[0] + len(d))) else -1
     boff["fric0"] = affine([int(i) for i in fric])
     boff["lim0"] = affine(lim_dofs)
     # flattened tree recursions: per body its dof chain and its subtree, per body the local
@@ -337,6 +338,19 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
                 int(m.actuator_forcelimited[a]), f2i(m.actuator_forcerange[a][0]), f2i(m.actuator_forcerange[a][1]),
                 0, 0]
     put("act", rec)  # stride 12: ctrllimited, ctrlrange2, gear, qadr, dof, kv, forcelimited, forcerange2, pad2
+    # affine index maps (see B_FRIC0): actuator -> dof / qpos address, limit row -> qpos address, and
+    # dof -> body (the first B_DBN dofs on body B_DB0, then body = dof + B_DBD; B_DBD = -1000: table)
+    act_j = [int(m.actuator_trnid[a]) for a in range(m.nu)]
+    boff["actd0"] = affine([int(m.jnt_dofadr[j]) for j in act_j])
+    boff["actq0"] = affine([int(m.jnt_qposadr[j]) for j in act_j])
+    boff["limq0"] = affine([int(m.jnt_qposadr[j]) for j in lim])
+    db = [int(x) for x in m.dof_bodyid]
+    nfr = 6 if (m.njnt > 0 and m.jnt_type[0] == 0 and m.jnt_dofadr[0] == 0) else 0
+    ok = nv > nfr and all(db[i] == db[0] for i in range(nfr)) and \
+        all(db[i] == i + (db[nfr] - nfr) for i in range(nfr, nv))
+    boff["dbn"] = nfr
+    boff["db0"] = db[0] if nfr else 0
+    boff["dbd"] = (db[nfr] - nfr) if ok else -1000
     rec = []
     for g in (floor, m.id("geom", "left_foot_bottom_tpu"), m.id("geom", "right_foot_bottom_tpu")):
         rec += [int(m.geom_bodyid[g])] + [f2i(x) for x in m.geom_pos[g]] + \

@@ -219,7 +219,22 @@ struct TPhys {
   static DK bool moving(int b) { return (moving_mask() >> b) & 1ull; }
   static DK int limb_body(int lane, int d) { return ti(Md::B_BR + Md::T_BRLEN * (lane < Md::T_NBR ? lane : 0) + d); }
   static DK int limb_dof(int lane, int k) { return ti(Md::B_BRDOF + 2 * Md::T_BRLEN * (lane < Md::T_NBR ? lane : 0) + k); }
-  static DK int dof_body(int i) { return ti(Md::B_DOFREC + 4 * i); }
+  static DK int dof_body(int i) {
+    if constexpr (Md::B_DBD > -1000) return i < Md::B_DBN ? Md::B_DB0 : i + Md::B_DBD;
+    else return ti(Md::B_DOFREC + 4 * i);
+  }
+  static DK int act_dof(int a) {
+    if constexpr (Md::B_ACTD0 >= 0) return Md::B_ACTD0 + a;
+    else return ti(Md::B_ACT + 12 * a + 5);
+  }
+  static DK int act_qadr(int a) {
+    if constexpr (Md::B_ACTQ0 >= 0) return Md::B_ACTQ0 + a;
+    else return ti(Md::B_ACT + 12 * a + 4);
+  }
+  static DK int lim_qadr(int r) {
+    if constexpr (Md::B_LIMQ0 >= 0) return Md::B_LIMQ0 + r;
+    else return ti(Md::B_LIM + LIMW * r + 1);
+  }
 
   static_assert(NFRIC <= TEAM, "one friction row per lane");
   static_assert(NCON <= TEAM, "one contact slot per lane");
@@ -626,11 +641,11 @@ struct TPhys {
     TSYNC();
     if (lane < NU) {
       const int a = lane, o = Md::B_ACT + 12 * a;
-      const int dof = ti(o + 5);
+      const int dof = act_dof(a);
       float c = L[Ly::CTRL + a];
       if (ti(o)) c = fminf(fmaxf(c, tf(o + 1)), tf(o + 2));
       const float g = tf(o + 3), kp = L[Ly::DKP + a];
-      const float len = g * L[Ly::QPOS + ti(o + 4)], vel = g * L[Ly::QVEL + dof];
+      const float len = g * L[Ly::QPOS + act_qadr(a)], vel = g * L[Ly::QVEL + dof];
       float f = kp * c + (-kp * len - tf(o + 6) * vel);
       if (ti(o + 7)) f = fminf(fmaxf(f, tf(o + 8)), tf(o + 9));
       L[Ly::AF + a] = f;
@@ -1613,7 +1628,7 @@ struct TPhys {
     }
     for (int r = lane; r < NLIM; r += TEAM) {
       const int o = Md::B_LIM + LIMW * r;
-      const int i = ti(o), qa = ti(o + 1);
+      const int i = lim_dof(r), qa = lim_qadr(r);
       const float q = L[Ly::QPOS + qa];
       const float dlo = q - tf(o + 2), dhi = tf(o + 3) - q;
       const float pos = fminf(dlo, dhi) - tf(o + 4);
