@@ -351,6 +351,16 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     boff["dbn"] = nfr
     boff["db0"] = db[0] if nfr else 0
     boff["dbd"] = (db[nfr] - nfr) if ok else -1000
+    # joints after a leading free joint: all hinges with body / dof / qpos address = j + const
+    # (B_JAFF = 1; com_pos and Euler then compute them instead of loading the joint records)
+    j0 = 1 if (m.njnt > 0 and m.jnt_type[0] == 0) else 0
+    js = range(j0, m.njnt)
+    jb, jd, jq = ([int(a[j]) - j for j in js] for a in (m.jnt_bodyid, m.jnt_dofadr, m.jnt_qposadr))
+    jaff = len(js) > 0 and all(int(m.jnt_type[j]) == 3 for j in js) and len(set(jb)) == 1 and \
+        len(set(jd)) == 1 and len(set(jq)) == 1
+    boff["jaff"] = 1 if jaff else 0
+    boff["jn0"] = j0
+    boff["jbd"], boff["jdd"], boff["jqd"] = (jb[0], jd[0], jq[0]) if jaff else (0, 0, 0)
     rec = []
     for g in (floor, m.id("geom", "left_foot_bottom_tpu"), m.id("geom", "right_foot_bottom_tpu")):
         rec += [int(m.geom_bodyid[g])] + [f2i(x) for x in m.geom_pos[g]] + \

@@ -389,9 +389,12 @@ struct TPhys {
       L[o + 9] = m;
     }
     for (int j = lane; j < NJ; j += TEAM) {
-      const int oj = Md::B_JREC + 9 * j, b = ti(oj), da = ti(oj + 1);
+      const int oj = Md::B_JREC + 9 * j;
+      // affine joint maps (codegen B_JAFF): hinge j >= B_JN0 sits on body j + B_JBD with dof j + B_JDD
+      const bool jh = Md::B_JAFF && j >= Md::B_JN0;
+      const int b = jh ? j + Md::B_JBD : ti(oj), da = jh ? j + Md::B_JDD : ti(oj + 1);
       const float off[3] = {com[0] - L[Ly::XPOS + 3 * b], com[1] - L[Ly::XPOS + 3 * b + 1], com[2] - L[Ly::XPOS + 3 * b + 2]};
-      if (ti(oj + 3) == 0) {
+      if (!jh && ti(oj + 3) == 0) {
         for (int k = 0; k < 3; k++)
           for (int q = 0; q < 6; q++) L[Ly::CDOF + 6 * (da + k) + q] = (q == 3 + k) ? 1.0f : 0.0f;
         for (int k = 0; k < 3; k++) {
@@ -2135,7 +2138,9 @@ struct TPhys {
     }
     for (int j = 1 + lane; j < NJ; j += TEAM) {
       const int oj = Md::B_JREC + 9 * j;
-      L[Ly::QPOS + ti(oj + 2)] += dt * L[Ly::QVEL + ti(oj + 1)];
+      const bool jh = Md::B_JAFF && j >= Md::B_JN0;
+      const int qa = jh ? j + Md::B_JQD : ti(oj + 2), da = jh ? j + Md::B_JDD : ti(oj + 1);
+      L[Ly::QPOS + qa] += dt * L[Ly::QVEL + da];
     }
     TSYNC();
   }
