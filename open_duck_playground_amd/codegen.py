@@ -383,6 +383,20 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         c = sorted(_ancestors(m, i, True))
         dch[i, :len(c)] = c
     put("dchain", dch.reshape(-1))  # ancestors of dof i incl. itself, ascending (= M row order)
+    # the same chains as "free-joint dofs, then a run of consecutive limb dofs up to i" (B_DCHAFF = 1):
+    # crb computes them from the run starts T_DLST instead of loading index words
+    nfd = 6 if (m.njnt > 0 and m.jnt_type[0] == 0 and m.jnt_dofadr[0] == 0) else 0
+    dlst = [i for i in range(nfd, nv) if i == nfd or (mc > nfd and dch[i, nfd] == i)]
+
+    def chain_model(i):
+        if i < nfd:
+            return list(range(i + 1))
+        st = max(x for x in dlst if x <= i)
+        return list(range(nfd)) + list(range(st, i + 1))
+    dchaff = nfd > 0 and len(dlst) > 0 and all(
+        [int(x) for x in dch[i] if x >= 0] == chain_model(i) for i in range(nv))
+    boff["dchaff"] = 1 if dchaff else 0
+    boff["dchn"] = nfd
     put("mrow", [adr[i, min(_ancestors(m, i, True))] for i in range(nv)])  # adr of row i's first entry
     extra_const = [f"  static constexpr int T_MAXSUB = {msub};\n"]
     T = lambda name, a, t: f"__device__ const {t} {pre}_{name}{''.join(f'[{d}]' for d in np.shape(a))} = " + \
@@ -397,6 +411,8 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
            f"T_BRMD = {int(max(m.body_dofnum[b] for br in branches for b in br))};\n",
            _arr("T_ROOT", root, "int"),
            _arr("T_BRB", br_arr, "int"),  # [T_NBR][T_BRLEN] limb bodies, -1 past a limb's end
+           _arr("T_DLST", dlst if dlst else [0], "int"),  # starts of the consecutive limb-dof runs (B_DCHAFF)
+           f"  static constexpr int T_NDLST = {len(dlst)};\n",
            f"  static constexpr int NBLOB = {len(blob)};\n"] + extra_const + [
            "".join(f"  static constexpr int B_{k.upper()} = {v};\n" for k, v in boff.items())]
     for k, (a, t) in tabs.items():

@@ -585,9 +585,20 @@ struct TPhys {
       for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * bi + k];
       int jj[MC];
       float cj[MC][6];
+      // with B_DCHAFF the chain is the B_DCHN free-joint dofs, then the run of limb dofs from the
+      // run start at or below i up to i (codegen T_DLST): no index words to load
+      int st = Md::T_DLST[0];
+#pragma unroll
+      for (int k = 1; k < Md::T_NDLST; k++) st = ic >= Md::T_DLST[k] ? Md::T_DLST[k] : st;
 #pragma unroll
       for (int q = 0; q < MC; q++) {
-        jj[q] = ti(Md::B_DCHAIN + MC * ic + q);
+        if constexpr (Md::B_DCHAFF) {
+          constexpr int NF = Md::B_DCHN;
+          const int jq = q < NF ? q : st + (q - NF);
+          jj[q] = (q < NF ? (ic < NF ? q <= ic : true) : (ic >= NF && jq <= ic)) ? jq : -1;
+        } else {
+          jj[q] = ti(Md::B_DCHAIN + MC * ic + q);
+        }
         if (FREE0 && q < 3) continue;  // ancestors ascending: position q < 3 is dof q, cdof = e_{3+q}
         const int jc = jj[q] >= 0 ? jj[q] : 0;
         for (int k = 0; k < 6; k++) cj[q][k] = L[Ly::CDOF + 6 * jc + k];
