@@ -522,11 +522,13 @@ static int argmax_tol(const double* v, int n, double tol) {
 }
 #define MANIFOLD_TOL 2e-8
 
-/* mjx collision_convex._manifold_points: 4 points of approximately maximal area */
-static void manifold_points(const double (*poly)[3], const int* mask, int n, const double* nrm, int idx[4]) {
-  double dm[DUCK_MAXHULLV] = {0}, s[2 * DUCK_MAXHULLV];
+/* mjx collision_convex._manifold_points: 4 points of approximately maximal area; the first is
+ * point a (mjx: the first masked point; the height field's prism contacts start from the deepest) */
+#define MANIFOLD_MAXN 128
+static void manifold_points_from(const double (*poly)[3], const int* mask, int n, const double* nrm, int a, int idx[4]) {
+  if (n > MANIFOLD_MAXN) abort(); /* fixed-capacity scratch */
+  double dm[MANIFOLD_MAXN] = {0}, s[2 * MANIFOLD_MAXN];
   for (int k = 0; k < n; k++) dm[k] = mask[k] ? 0.0 : -1e6;
-  int a = argmax_tol(dm, n, 0.0);
   for (int k = 0; k < n; k++) {
     double dx = poly[a][0] - poly[k][0], dy = poly[a][1] - poly[k][1], dz = poly[a][2] - poly[k][2];
     s[k] = dx * dx + dy * dy + dz * dz + dm[k];
@@ -552,6 +554,12 @@ static void manifold_points(const double (*poly)[3], const int* mask, int n, con
   }
   int dd = argmax_tol(s, 2 * n, MANIFOLD_TOL) % n;
   idx[0] = a; idx[1] = b; idx[2] = c; idx[3] = dd;
+}
+static void manifold_points(const double (*poly)[3], const int* mask, int n, const double* nrm, int idx[4]) {
+  if (n > MANIFOLD_MAXN) abort();
+  double dm[MANIFOLD_MAXN] = {0};
+  for (int k = 0; k < n; k++) dm[k] = mask[k] ? 0.0 : -1e6;
+  manifold_points_from(poly, mask, n, nrm, argmax_tol(dm, n, 0.0), idx);
 }
 
 /* mjx math.make_frame: rows (normal, t1, t2) */
@@ -620,189 +628,356 @@ static void collide_plane_convex(const oracle_model* m, oracle_data* d, int g1, 
   }
 }
 
-/* height field: elevation of MuJoCo's triangulated grid at (x, y) in the hfield frame (each
- * cell split along its (0,0)-(1,1) diagonal; outside the grid the border cells extend) and
- * the unit normal of that triangle. Row r <-> y, column c <-> x. */
-static double hfield_point(const oracle_model* m, double x, double y, double nrm[3]) {
-  const int nr = m->hfield_nrow, nc = m->hfield_ncol;
-  const double sx = m->hfield_size[0], sy = m->hfield_size[1], sz = m->hfield_size[2];
-  const double dx = 2.0 * sx / (nc - 1), dy = 2.0 * sy / (nr - 1);
-  const double fx = (x + sx) / dx, fy = (y + sy) / dy;
-  int c = (int)floor(fx), r = (int)floor(fy);
-  if (!(fx == fx)) c = 0;
-  if (!(fy == fy)) r = 0;
-  c = c < 0 ? 0 : (c > nc - 2 ? nc - 2 : c);
-  r = r < 0 ? 0 : (r > nr - 2 ? nr - 2 : r);
-  double u = fx - c, w = fy - r;
-  u = u < 0 ? 0 : (u > 1 ? 1 : u);
-  w = w < 0 ? 0 : (w > 1 ? 1 : w);
-  const double* h = m->hfield_data;
-  const double z00 = sz * h[r * nc + c], z10 = sz * h[r * nc + c + 1];
-  const double z01 = sz * h[(r + 1) * nc + c], z11 = sz * h[(r + 1) * nc + c + 1];
-  double z;
-  if (u >= w) {
-    z = z00 + u * (z10 - z00) + w * (z11 - z10);
-    nrm[0] = -(z10 - z00) * dy; nrm[1] = dx * (z10 - z11); nrm[2] = dx * dy;
+/* ------------------------------------------------------------------------------------ */
+/* height field vs convex hull: MuJoCo's prism decomposition                             */
+/* ------------------------------------------------------------------------------------ */
+/* MuJoCo mjc_ConvexHField (engine_collision_convex.c), which MJX's hfield collision follows:
+ *  - the hull's bounding box in the height field's frame (its extreme vertices along +-x, +-y,
+ *    +-z) is tested against the field's box [-sx, sx] x [-sy, sy] x [-size[3], size[2]];
+ *  - the sub-grid: vertex columns cmin = floor((xmin + sx) / (2 sx) (ncol - 1)), cmax = ceil(..)
+ *    clamped to [0, ncol - 1]; rows rmin / rmax likewise;
+ *  - each row r in [rmin, rmax) is walked as a triangle strip over the vertices (c, r), (c, r + 1),
+ *    c = cmin .. cmax (addVert): every three consecutive vertices are the top of a prism whose
+ *    bottom is at z = -size[3]; cell (c, r) thus holds the triangles
+ *    A = {(c, r), (c, r + 1), (c + 1, r)} and B = {(c, r + 1), (c + 1, r), (c + 1, r + 1)}
+ *    (the cell's (c, r + 1)-(c + 1, r) diagonal);
+ *  - the prism height test: a prism whose three top vertices are all below the hull's lowest
+ *    point is skipped;
+ *  - every other prism is collided with the hull as a convex-convex pair, one contact per prism.
+ * Restated with an exact penetration depth in place of libccd's MPR estimate: the minimum over
+ * the faces of the Minkowski difference P - H of its support function (separating-axis test over
+ * the prism's 5 face normals, the hull's face normals and the edge pairs whose Gauss-map arcs
+ * cross -- Gregorius, GDC 2013), and MJX's fixed DUCK_CON_PER_PAIR slots per pair, filled from the
+ * prism contacts by MJX's _manifold_points starting at the deepest. Declared choices (DESIGN.md
+ * §5 item 6): near-equal axes resolve to the first in the priority order (prism top, sides,
+ * bottom, hull faces, edge pairs) within HF_SAT_TIE of the minimum; the contact point of a prism
+ * is the penetration-weighted centroid of the vertices of each shape inside the other, or, when
+ * none is (crossing edges), the midpoint of the two shapes' support features (the centroid of each
+ * shape's vertices within HF_WITNESS_BAND of its support plane along the normal, weighted 1 at the
+ * plane to 0 at the band edge; the prism's top vertices only). */
+#define HF_SAT_TIE 1e-6      /* m; = codegen.HF_SAT_TIE */
+#define HF_WITNESS_BAND 1e-3 /* m; = codegen.HF_WITNESS_BAND */
+#define HF_MAXPRISM 128      /* prisms under one hull (the sub-grid of a 0.11 m foot: <= 18) */
+
+/* the hull in the local frame (the height field's axes, origin at the hull's frame) */
+typedef struct {
+  int nv, nf, ne;
+  double V[DUCK_MAXHULLV][3], FN[DUCK_MAXHULLF][3];
+} hf_hull;
+
+/* support values over a point set */
+static double pts_min(const double* u, const double (*P)[3], int n) {
+  double v = 1e300;
+  for (int i = 0; i < n; i++) v = fmin(v, dot3(u, P[i]));
+  return v;
+}
+static double pts_max(const double* u, const double (*P)[3], int n) {
+  double v = -1e300;
+  for (int i = 0; i < n; i++) v = fmax(v, dot3(u, P[i]));
+  return v;
+}
+
+/* the prism's outward face normals: top nt (z > 0), side k through top edge T_k -> T_{k+1} */
+static void prism_normals(const double T[3][3], double nt[3], double s[3][3]) {
+  double e0[3], e1[3];
+  for (int a = 0; a < 3; a++) { e0[a] = T[1][a] - T[0][a]; e1[a] = T[2][a] - T[0][a]; }
+  cross3(nt, e0, e1);
+  const double nn = norm3(nt), sg = nt[2] < 0 ? -1.0 : 1.0;
+  for (int a = 0; a < 3; a++) nt[a] *= sg / nn;
+  for (int k = 0; k < 3; k++) {
+    const double* p = T[k];
+    const double* q = T[(k + 1) % 3];
+    const double* o = T[(k + 2) % 3];
+    double sx = q[1] - p[1], sy = -(q[0] - p[0]);
+    const double l = sqrt(sx * sx + sy * sy);
+    sx /= l; sy /= l;
+    if (sx * (o[0] - p[0]) + sy * (o[1] - p[1]) > 0) { sx = -sx; sy = -sy; }
+    s[k][0] = sx; s[k][1] = sy; s[k][2] = 0.0;
+  }
+}
+
+/* Gregorius' Minkowski-face test: do the Gauss-map arcs (A, B) of one polytope's edge and
+ * (C, D) of the other's negated edge cross? */
+static int minkowski_face(const double* A, const double* B, const double* C, const double* D) {
+  double BxA[3], DxC[3];
+  cross3(BxA, B, A);
+  cross3(DxC, D, C);
+  const double CBA = dot3(C, BxA), DBA = dot3(D, BxA), ADC = dot3(A, DxC), BDC = dot3(B, DxC);
+  return CBA * DBA < 0 && ADC * BDC < 0 && CBA * BDC > 0;
+}
+
+/* one prism (top vertices T, bottom at z = base, local frame) against the hull: exact
+ * penetration depth, contact normal u (pushes the hull out of the prism) and point. Returns 0
+ * when the shapes do not overlap. */
+static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const double T[3][3], double base, double* depth,
+                            double u_out[3], double pos[3]) {
+  double P[6][3], nt[3], s[3][3];
+  for (int k = 0; k < 3; k++) {
+    memcpy(P[k], T[k], sizeof(double) * 3);
+    P[k + 3][0] = T[k][0]; P[k + 3][1] = T[k][1]; P[k + 3][2] = base;
+  }
+  prism_normals(T, nt, s);
+  /* candidate axes in priority order */
+  enum { NAX = 5 + DUCK_MAXHULLF + 9 * DUCK_MAXHULLE };
+  double ax[NAX][3], ov[NAX];
+  int na = 0;
+  memcpy(ax[na++], nt, sizeof(nt));
+  for (int k = 0; k < 3; k++) memcpy(ax[na++], s[k], sizeof(double) * 3);
+  ax[na][0] = 0; ax[na][1] = 0; ax[na][2] = -1; na++;
+  for (int f = 0; f < H->nf; f++)
+    for (int a = 0; a < 3; a++) ax[na + f][a] = -H->FN[f][a];
+  na += H->nf;
+  /* prism edges: top k (T_k, T_k+1; faces nt, s_k), vertical k (at vertex k; faces s_k-1, s_k),
+   * bottom k (faces -z, s_k) */
+  const double mz[3] = {0, 0, -1};
+  for (int e = 0; e < H->ne; e++) {
+    const int v0 = m->hull_edge[e][0], v1 = m->hull_edge[e][1];
+    const double *nA = H->FN[m->hull_edge_face[e][0]], *nB = H->FN[m->hull_edge_face[e][1]];
+    const double C[3] = {-nA[0], -nA[1], -nA[2]}, D[3] = {-nB[0], -nB[1], -nB[2]};
+    double eh[3];
+    for (int a = 0; a < 3; a++) eh[a] = H->V[v1][a] - H->V[v0][a];
+    for (int q = 0; q < 9; q++) {
+      const int k = q % 3, kind = q / 3;
+      const double *fa, *fb;
+      double ep[3];
+      if (kind == 0) {
+        fa = nt; fb = s[k];
+        for (int a = 0; a < 3; a++) ep[a] = T[(k + 1) % 3][a] - T[k][a];
+      } else if (kind == 1) {
+        fa = s[(k + 2) % 3]; fb = s[k];
+        ep[0] = 0; ep[1] = 0; ep[2] = 1;
+      } else {
+        fa = mz; fb = s[k];
+        for (int a = 0; a < 2; a++) ep[a] = T[(k + 1) % 3][a] - T[k][a];
+        ep[2] = 0;
+      }
+      if (!minkowski_face(fa, fb, C, D)) continue;
+      double u[3];
+      cross3(u, eh, ep);
+      const double un = norm3(u);
+      if (un < 1e-9 * norm3(eh) * norm3(ep)) continue;
+      const double sg = (dot3(u, fa) + dot3(u, fb)) < 0 ? -1.0 : 1.0;
+      for (int a = 0; a < 3; a++) ax[na][a] = sg * u[a] / un;
+      na++;
+    }
+  }
+  double mn = 1e300;
+  for (int i = 0; i < na; i++) {
+    ov[i] = pts_max(ax[i], (const double(*)[3])P, 6) - pts_min(ax[i], (const double(*)[3])H->V, H->nv);
+    mn = fmin(mn, ov[i]);
+  }
+  if (!(mn > 0)) return 0;
+  int w = 0;
+  while (ov[w] > mn + HF_SAT_TIE) w++;
+  const double* u = ax[w];
+  /* the contact point: the centroid of the vertices of each shape inside the other (hull
+   * vertices inside the prism, prism top vertices inside the hull), each weighted by its
+   * penetration (distance to the nearest face of the other shape); when no vertex is inside
+   * (crossing edges), the midpoint of the two shapes' support features along u */
+  double wsum = 0, c[3] = {0, 0, 0};
+  const double ptop = dot3(nt, T[0]);
+  for (int k = 0; k < H->nv; k++) {
+    const double* v = H->V[k];
+    double pen = fmin(ptop - dot3(nt, v), v[2] - base);
+    for (int j = 0; j < 3; j++) pen = fmin(pen, s[j][0] * (T[j][0] - v[0]) + s[j][1] * (T[j][1] - v[1]));
+    if (pen > 0) { wsum += pen; for (int a = 0; a < 3; a++) c[a] += pen * v[a]; }
+  }
+  for (int j = 0; j < 3; j++) {
+    double pen = 1e300;
+    for (int f = 0; f < H->nf; f++) pen = fmin(pen, m->hull_face_offset[f] - dot3(H->FN[f], T[j]));
+    if (pen > 0) { wsum += pen; for (int a = 0; a < 3; a++) c[a] += pen * T[j][a]; }
+  }
+  if (wsum > 0) {
+    for (int a = 0; a < 3; a++) pos[a] = c[a] / wsum;
   } else {
-    z = z00 + w * (z01 - z00) + u * (z11 - z01);
-    nrm[0] = dy * (z01 - z11); nrm[1] = -dx * (z01 - z00); nrm[2] = dx * dy;
+    const double hmin = pts_min(u, (const double(*)[3])H->V, H->nv), pmax = pts_max(u, T, 3);
+    double wh = 0, wp = 0, ch[3] = {0, 0, 0}, cp[3] = {0, 0, 0};
+    for (int k = 0; k < H->nv; k++) {
+      const double wk = fmax(0.0, 1.0 - (dot3(u, H->V[k]) - hmin) / HF_WITNESS_BAND);
+      wh += wk;
+      for (int a = 0; a < 3; a++) ch[a] += wk * H->V[k][a];
+    }
+    for (int k = 0; k < 3; k++) {
+      const double wk = fmax(0.0, 1.0 - (pmax - dot3(u, T[k])) / HF_WITNESS_BAND);
+      wp += wk;
+      for (int a = 0; a < 3; a++) cp[a] += wk * T[k][a];
+    }
+    for (int a = 0; a < 3; a++) pos[a] = 0.5 * (ch[a] / wh + cp[a] / wp);
   }
-  const double nn = norm3(nrm);
-  nrm[0] /= nn; nrm[1] /= nn; nrm[2] /= nn;
-  return z;
+  memcpy(u_out, u, sizeof(double) * 3);
+  *depth = ov[w];
+  return 1;
 }
 
-/* signed distance of world point vw to the terrain triangle plane under it; world normal */
-static double hfield_dist(const oracle_model* m, const double* hp, const double* HR, const double* vw, double nw[3]) {
-  double d[3] = {vw[0] - hp[0], vw[1] - hp[1], vw[2] - hp[2]}, pl[3], nl[3];
-  mulmtv3(pl, HR, d);
-  const double z = hfield_point(m, pl[0], pl[1], nl);
-  mulmv3(nw, HR, nl);
-  return (pl[2] - z) * nl[2];
-}
+/* the hull in the height field's local frame; its bounding box in the hfield frame; the
+ * sub-grid. Returns 0 when the box misses the field. */
+typedef struct {
+  double R[9], t[3];  /* hull frame -> hfield frame: x_hf = R v + t */
+  double zmin;
+  int cmin, cmax, rmin, rmax;
+} hf_frame;
 
-/* height field (g1) vs convex hull (g2). Every hull vertex is measured against the terrain
- * triangle under it; the 4 contacts are the plane-convex manifold (same masks and argmax
- * rules) taken with the terrain normal under the deepest vertex, each contact carrying its
- * own vertex's distance and triangle normal. Declared stand-in for mjx's prism
- * decomposition; on a flat field it equals collide_plane_convex. */
-static void collide_hfield_convex(const oracle_model* m, oracle_data* d, int g1, int g2, int slot0) {
-  const double* hp = d->geom_xpos[g1];
-  const double* HR = d->geom_xmat[g1];
-  const double* cp = d->geom_xpos[g2];
-  const double* CR = d->geom_xmat[g2];
-  int nv = m->hull_nvert;
-  double support[DUCK_MAXHULLV], vw[DUCK_MAXHULLV][3], nw[DUCK_MAXHULLV][3];
-  double smax = -1e30;
-  for (int k = 0; k < nv; k++) {
-    mulmv3(vw[k], CR, m->hull_vert[k]);
-    for (int a = 0; a < 3; a++) vw[k][a] += cp[a];
-    support[k] = -hfield_dist(m, hp, HR, vw[k], nw[k]);
-    if (support[k] > smax) smax = support[k];
-  }
-  double thr = smax - 1e-3 > 0 ? smax - 1e-3 : 0;
-  int mask[DUCK_MAXHULLV];
-  for (int k = 0; k < nv; k++) mask[k] = support[k] > thr;
-  const int kd = argmax_tol(support, nv, 0.0);
-  double n_local[3];
-  mulmtv3(n_local, CR, nw[kd]);
-  int idx[4];
-  manifold_points((const double(*)[3])m->hull_vert, mask, nv, n_local, idx);
-  for (int c = 0; c < 4; c++) {
-    int k = idx[c], unique = 1;
-    for (int e = 0; e < c; e++)
-      if (idx[e] == k) unique = 0;
-    double dist = unique ? -support[k] : 1.0;
-    int s = slot0 + c;
-    for (int a = 0; a < 3; a++) d->con_pos[s][a] = vw[k][a] - 0.5 * dist * nw[k][a];
-    d->con_dist[s] = dist;
-    make_frame(d->con_frame[s], nw[k]);
-    d->con_geom1[s] = g1; d->con_geom2[s] = g2;
-  }
-}
-
-/* Prism reference for the height field (measurement aid for DESIGN.md §5, tools/hfield_deviation.py;
- * not used by oracle_forward). MuJoCo's height-field collision decomposes the field under a convex
- * geom into triangular prisms (each grid cell's two triangles extruded down to the field's base,
- * -size[3]) and collides every prism with the geom as a convex-convex pair. This restates that with
- * an exact separating-axis test per prism (the hull's 30 face normals, the prism's 5, and every hull
- * edge x prism edge direction), writing for each penetrating prism its depth, the unit normal that
- * pushes the hull out (world frame) and the deepest hull vertex. Returns the number written. */
-static void sat_axis(const double* u, const double (*A)[3], int na, const double (*B)[3], int nb, double* ov,
-                     double* sgn) {
-  double amin = 1e30, amax = -1e30, bmin = 1e30, bmax = -1e30;
-  for (int i = 0; i < na; i++) { double t = dot3(u, A[i]); amin = fmin(amin, t); amax = fmax(amax, t); }
-  for (int i = 0; i < nb; i++) { double t = dot3(u, B[i]); bmin = fmin(bmin, t); bmax = fmax(bmax, t); }
-  double o1 = bmax - amin, o2 = amax - bmin; /* push A (hull) along +u by o1, or along -u by o2 */
-  if (o1 < o2) { *ov = o1; *sgn = 1; } else { *ov = o2; *sgn = -1; }
-}
-
-int oracle_hfield_prisms(const oracle_model* m, const oracle_data* d, int g_hf, int g_cvx, int max, double* depth,
-                         double* normal, double* point) {
-  if (!m->hfield_data) return 0;
+static int hf_setup(const oracle_model* m, const oracle_data* d, int g_hf, int g_cvx, hf_hull* H, hf_frame* F) {
   const double *hp = d->geom_xpos[g_hf], *HR = d->geom_xmat[g_hf], *cp = d->geom_xpos[g_cvx], *CR = d->geom_xmat[g_cvx];
-  const int nv = m->hull_nvert, nf = m->hull_nface, ne = m->hull_nedge;
-  const int nr = m->hfield_nrow, nc = m->hfield_ncol;
-  const double sx = m->hfield_size[0], sy = m->hfield_size[1], sz = m->hfield_size[2], base = -m->hfield_size[3];
-  const double dx = 2.0 * sx / (nc - 1), dy = 2.0 * sy / (nr - 1);
-  /* hull in the height field's frame */
-  double V[DUCK_MAXHULLV][3], FN[DUCK_MAXHULLF][3], ED[DUCK_MAXHULLE][3], R[9];
   for (int a = 0; a < 3; a++)
-    for (int b = 0; b < 3; b++) R[3 * a + b] = HR[0 * 3 + a] * CR[0 * 3 + b] + HR[1 * 3 + a] * CR[1 * 3 + b] + HR[2 * 3 + a] * CR[2 * 3 + b];
-  double off[3] = {cp[0] - hp[0], cp[1] - hp[1], cp[2] - hp[2]}, ol[3];
-  mulmtv3(ol, HR, off);
-  double xmin = 1e30, xmax = -1e30, ymin = 1e30, ymax = -1e30;
-  for (int k = 0; k < nv; k++) {
-    mulmv3(V[k], R, m->hull_vert[k]);
-    for (int a = 0; a < 3; a++) V[k][a] += ol[a];
-    xmin = fmin(xmin, V[k][0]); xmax = fmax(xmax, V[k][0]); ymin = fmin(ymin, V[k][1]); ymax = fmax(ymax, V[k][1]);
+    for (int b = 0; b < 3; b++) F->R[3 * a + b] = HR[a] * CR[b] + HR[3 + a] * CR[3 + b] + HR[6 + a] * CR[6 + b];
+  const double off[3] = {cp[0] - hp[0], cp[1] - hp[1], cp[2] - hp[2]};
+  mulmtv3(F->t, HR, off);
+  H->nv = m->hull_nvert; H->nf = m->hull_nface; H->ne = m->hull_nedge;
+  double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+  for (int k = 0; k < H->nv; k++) {
+    mulmv3(H->V[k], F->R, m->hull_vert[k]);
+    for (int a = 0; a < 3; a++) {
+      lo[a] = fmin(lo[a], H->V[k][a] + F->t[a]);
+      hi[a] = fmax(hi[a], H->V[k][a] + F->t[a]);
+    }
   }
-  for (int f = 0; f < nf; f++) mulmv3(FN[f], R, m->hull_face_normal[f]);
-  for (int e = 0; e < ne; e++) {
-    double t[3];
-    for (int a = 0; a < 3; a++) t[a] = m->hull_vert[m->hull_edge[e][1]][a] - m->hull_vert[m->hull_edge[e][0]][a];
-    mulmv3(ED[e], R, t);
+  for (int f = 0; f < H->nf; f++) mulmv3(H->FN[f], F->R, m->hull_face_normal[f]);
+  const double *sz = m->hfield_size;
+  const int nr = m->hfield_nrow, nc = m->hfield_ncol;
+  F->zmin = lo[2];
+  if (hi[0] < -sz[0] || lo[0] > sz[0] || hi[1] < -sz[1] || lo[1] > sz[1] || lo[2] > sz[2] || hi[2] < -sz[3])
+    return 0;
+  F->cmin = (int)floor((lo[0] + sz[0]) / (2 * sz[0]) * (nc - 1));
+  F->cmax = (int)ceil((hi[0] + sz[0]) / (2 * sz[0]) * (nc - 1));
+  F->rmin = (int)floor((lo[1] + sz[1]) / (2 * sz[1]) * (nr - 1));
+  F->rmax = (int)ceil((hi[1] + sz[1]) / (2 * sz[1]) * (nr - 1));
+  F->cmin = F->cmin < 0 ? 0 : F->cmin;
+  F->cmax = F->cmax > nc - 1 ? nc - 1 : F->cmax;
+  F->rmin = F->rmin < 0 ? 0 : F->rmin;
+  F->rmax = F->rmax > nr - 1 ? nr - 1 : F->rmax;
+  return 1;
+}
+
+/* top vertices of strip prism (r, c, tri) in the local frame; returns 0 when the prism height
+ * test skips it */
+static int hf_prism_top(const oracle_model* m, const hf_frame* F, int r, int c, int tri, double T[3][3]) {
+  static const int cc[2][3][2] = {{{0, 0}, {0, 1}, {1, 0}}, {{0, 1}, {1, 0}, {1, 1}}}; /* (dc, dr) */
+  const double* sz = m->hfield_size;
+  const int nr = m->hfield_nrow, nc = m->hfield_ncol;
+  int below = 0;
+  for (int k = 0; k < 3; k++) {
+    const int ci = c + cc[tri][k][0], ri = r + cc[tri][k][1];
+    const double x = sz[0] * (2.0 * ci / (nc - 1) - 1.0), y = sz[1] * (2.0 * ri / (nr - 1) - 1.0);
+    const double z = sz[2] * m->hfield_data[ri * nc + ci];
+    below += z < F->zmin;
+    T[k][0] = x - F->t[0]; T[k][1] = y - F->t[1]; T[k][2] = z - F->t[2];
   }
-  int c0 = (int)floor((xmin + sx) / dx), c1 = (int)floor((xmax + sx) / dx);
-  int r0 = (int)floor((ymin + sy) / dy), r1 = (int)floor((ymax + sy) / dy);
-  c0 = c0 < 0 ? 0 : c0; r0 = r0 < 0 ? 0 : r0; c1 = c1 > nc - 2 ? nc - 2 : c1; r1 = r1 > nr - 2 ? nr - 2 : r1;
+  return below < 3;
+}
+
+/* height field (g1) vs convex hull (g2): the DUCK_CON_PER_PAIR deepest prism contacts */
+static void collide_hfield_convex(const oracle_model* m, oracle_data* d, int g1, int g2, int slot0) {
+  for (int c = 0; c < DUCK_CON_PER_PAIR; c++) set_inactive(d, slot0 + c, g1, g2);
+  hf_hull H;
+  hf_frame F;
+  if (!hf_setup(m, d, g1, g2, &H, &F)) return;
+  double dep[HF_MAXPRISM], nrm[HF_MAXPRISM][3], pt[HF_MAXPRISM][3];
   int n = 0;
-  for (int r = r0; r <= r1; r++)
-    for (int c = c0; c <= c1; c++)
+  const double base = -m->hfield_size[3] - F.t[2];
+  for (int r = F.rmin; r < F.rmax; r++)
+    for (int c = F.cmin; c < F.cmax; c++)
       for (int tri = 0; tri < 2; tri++) {
-        /* the cell's triangles as hfield_point splits it: (00,10,11) where u >= w, (00,11,01) */
-        const int cc[2][3][2] = {{{0, 0}, {1, 0}, {1, 1}}, {{0, 0}, {1, 1}, {0, 1}}};
-        double P[6][3];
+        double T[3][3];
+        if (!hf_prism_top(m, &F, r, c, tri, T)) continue;
+        if (n >= HF_MAXPRISM) abort(); /* the fixed-capacity list: never reached by a foot-sized hull */
+        if (hf_prism_contact(m, &H, (const double(*)[3])T, base, &dep[n], nrm[n], pt[n])) n++;
+      }
+  if (n == 0) return;
+  /* 4 of the prism contacts by mjx's _manifold_points over their points, from the deepest (first
+   * in strip order among equal depths), areas taken in the plane of its normal; repeats stay
+   * inactive (plane_convex's rule) */
+  int a = 0;
+  for (int i = 1; i < n; i++)
+    if (dep[i] > dep[a]) a = i;
+  int mask[HF_MAXPRISM], idx[4];
+  for (int i = 0; i < n; i++) mask[i] = 1;
+  manifold_points_from((const double(*)[3])pt, mask, n, nrm[a], a, idx);
+  const double *hp = d->geom_xpos[g1], *HR = d->geom_xmat[g1];
+  for (int s = 0; s < DUCK_CON_PER_PAIR; s++) {
+    const int b = idx[s];
+    int unique = 1;
+    for (int e = 0; e < s; e++)
+      if (idx[e] == b) unique = 0;
+    double pl[3], nw[3];
+    for (int q = 0; q < 3; q++) pl[q] = pt[b][q] + F.t[q];
+    mulmv3(d->con_pos[slot0 + s], HR, pl);
+    for (int q = 0; q < 3; q++) d->con_pos[slot0 + s][q] += hp[q];
+    mulmv3(nw, HR, nrm[b]);
+    make_frame(d->con_frame[slot0 + s], nw);
+    d->con_dist[slot0 + s] = unique ? -dep[b] : 1.0;
+  }
+}
+
+/* Brute-force reference for the prism decomposition (tools/hfield_deviation.py, tests): the same
+ * sub-grid, strip and height test, and for every prism the separating-axis minimum over ALL
+ * axes -- the 5 prism faces, every hull face, every hull edge x prism edge direction, no
+ * Minkowski-face filter and no tie rule -- with its unit normal (pushes the hull out, world
+ * frame), the deepest hull vertex along it (world) and the prism's strip index. Returns the
+ * number of penetrating prisms written (at most max). */
+int oracle_hfield_prisms(const oracle_model* m, const oracle_data* d, int g_hf, int g_cvx, int max, double* depth,
+                         double* normal, double* point, int* index) {
+  if (!m->hfield_data) return 0;
+  hf_hull H;
+  hf_frame F;
+  if (!hf_setup(m, d, g_hf, g_cvx, &H, &F)) return 0;
+  const double *hp = d->geom_xpos[g_hf], *HR = d->geom_xmat[g_hf];
+  const double base = -m->hfield_size[3] - F.t[2];
+  int n = 0, idx = 0;
+  for (int r = F.rmin; r < F.rmax; r++)
+    for (int c = F.cmin; c < F.cmax; c++)
+      for (int tri = 0; tri < 2; tri++, idx++) {
+        double T[3][3], P[6][3], nt[3], s[3][3];
+        if (!hf_prism_top(m, &F, r, c, tri, T)) continue;
         for (int k = 0; k < 3; k++) {
-          const int ci = c + cc[tri][k][0], ri = r + cc[tri][k][1];
-          P[k][0] = P[k + 3][0] = -sx + ci * dx;
-          P[k][1] = P[k + 3][1] = -sy + ri * dy;
-          P[k][2] = sz * m->hfield_data[ri * nc + ci];
-          P[k + 3][2] = base;
+          memcpy(P[k], T[k], sizeof(double) * 3);
+          P[k + 3][0] = T[k][0]; P[k + 3][1] = T[k][1]; P[k + 3][2] = base;
         }
-        double axes[3 + DUCK_MAXHULLF + 5 + DUCK_MAXHULLE * 7][3];
-        int na = 0;
-        for (int f = 0; f < nf; f++) memcpy(axes[na++], FN[f], sizeof(double) * 3);
-        double e0[3], e1[3], top[3];
-        for (int a = 0; a < 3; a++) { e0[a] = P[1][a] - P[0][a]; e1[a] = P[2][a] - P[0][a]; }
-        cross3(top, e0, e1);
-        if (top[2] < 0) for (int a = 0; a < 3; a++) top[a] = -top[a];
-        memcpy(axes[na++], top, sizeof(top));
-        axes[na][0] = 0; axes[na][1] = 0; axes[na][2] = -1; na++;
-        double pe[7][3];
+        prism_normals((const double(*)[3])T, nt, s);
+        double pe[9][3];
         for (int k = 0; k < 3; k++) {
-          const double* a0 = P[k]; const double* a1 = P[(k + 1) % 3];
-          double hz[3] = {a1[0] - a0[0], a1[1] - a0[1], 0.0}, side[3], up[3] = {0, 0, 1};
-          cross3(side, hz, up); /* horizontal normal of the side face */
-          memcpy(axes[na++], side, sizeof(side));
-          for (int a = 0; a < 3; a++) pe[k][a] = a1[a] - a0[a];
-          memcpy(pe[3 + k], hz, sizeof(hz));
+          for (int a = 0; a < 3; a++) pe[k][a] = T[(k + 1) % 3][a] - T[k][a];
+          pe[3 + k][0] = 0; pe[3 + k][1] = 0; pe[3 + k][2] = 1;
+          pe[6 + k][0] = pe[k][0]; pe[6 + k][1] = pe[k][1]; pe[6 + k][2] = 0;
         }
-        pe[6][0] = 0; pe[6][1] = 0; pe[6][2] = 1;
-        for (int e = 0; e < ne; e++)
-          for (int k = 0; k < 7; k++) {
-            double u[3];
-            cross3(u, ED[e], pe[k]);
-            if (norm3(u) > 1e-9 * norm3(ED[e]) * norm3(pe[k])) memcpy(axes[na++], u, sizeof(u));
-          }
-        double best = 1e30, bu[3] = {0, 0, 1};
+        double best = 1e300, bu[3] = {0, 0, 1};
         int sep = 0;
-        for (int i = 0; i < na && !sep; i++) {
-          double u[3], nn = norm3(axes[i]), ov, sgn;
-          for (int a = 0; a < 3; a++) u[a] = axes[i][a] / nn;
-          sat_axis(u, (const double(*)[3])V, nv, (const double(*)[3])P, 6, &ov, &sgn);
-          if (ov < 0) sep = 1;
-          else if (ov < best) { best = ov; for (int a = 0; a < 3; a++) bu[a] = sgn * u[a]; }
+        const int naxes = 5 + H.nf + 9 * H.ne;
+        for (int i = 0; i < naxes && !sep; i++) {
+          double u[3];
+          if (i == 0) memcpy(u, nt, sizeof(u));
+          else if (i < 4) memcpy(u, s[i - 1], sizeof(u));
+          else if (i == 4) { u[0] = 0; u[1] = 0; u[2] = -1; }
+          else if (i < 5 + H.nf) for (int a = 0; a < 3; a++) u[a] = -H.FN[i - 5][a];
+          else {
+            const int q = i - 5 - H.nf, e = q / 9, k = q % 9;
+            double eh[3];
+            for (int a = 0; a < 3; a++) eh[a] = H.V[m->hull_edge[e][1]][a] - H.V[m->hull_edge[e][0]][a];
+            cross3(u, eh, pe[k]);
+            const double un = norm3(u);
+            if (un < 1e-9 * norm3(eh) * norm3(pe[k])) continue;
+            for (int a = 0; a < 3; a++) u[a] /= un;
+          }
+          /* both directions of an edge axis; faces are outward already */
+          for (int sgn = 0; sgn < (i >= 5 + H.nf ? 2 : 1); sgn++) {
+            if (sgn) for (int a = 0; a < 3; a++) u[a] = -u[a];
+            const double o = pts_max(u, (const double(*)[3])P, 6) - pts_min(u, (const double(*)[3])H.V, H.nv);
+            if (o <= 0) { sep = 1; break; }
+            if (o < best) { best = o; memcpy(bu, u, sizeof(bu)); }
+          }
         }
-        if (sep || n >= max) continue;
+        if (sep) continue;
+        if (n >= max) return n;
         int kd = 0;
-        for (int k = 1; k < nv; k++)
-          if (dot3(V[k], bu) < dot3(V[kd], bu)) kd = k;
+        for (int k = 1; k < H.nv; k++)
+          if (dot3(H.V[k], bu) < dot3(H.V[kd], bu)) kd = k;
         depth[n] = best;
         mulmv3(normal + 3 * n, HR, bu);
-        double pw[3];
-        mulmv3(pw, HR, V[kd]);
-        for (int a = 0; a < 3; a++) point[3 * n + a] = pw[a] + hp[a];
+        double pl[3];
+        for (int a = 0; a < 3; a++) pl[a] = H.V[kd][a] + F.t[a];
+        mulmv3(point + 3 * n, HR, pl);
+        for (int a = 0; a < 3; a++) point[3 * n + a] += hp[a];
+        index[n] = idx;
         n++;
       }
   return n;

@@ -68,9 +68,10 @@ void oracle_threefry2x32(const uint32_t key[2], const uint32_t ctr[2], uint32_t 
 /* Joystick env on one env: fstate/istate are this env's columns (stride 1). */
 int oracle_env_reset(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref,
                      uint64_t seed, int64_t env_id, double* fstate, int32_t* istate, double* obs, double* priv);
-/* measurement aid: MuJoCo-style prism decomposition of the height field vs a convex geom */
+/* brute-force check of the height-field prism decomposition: every penetrating prism's exact
+ * separating-axis depth, normal, deepest hull vertex and strip index */
 int oracle_hfield_prisms(const oracle_model* m, const oracle_data* d, int g_hf, int g_cvx, int max, double* depth,
-                         double* normal, double* point);
+                         double* normal, double* point, int* index);
 void oracle_set_trace(double* buf); /* test aid: record substep inputs of oracle_env_step */
 int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref,
                     double* fstate, int32_t* istate, const double* action, double* obs, double* priv,

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""How far the build's height-field contact model (collide_hfield_convex: each hull vertex against the
-terrain triangle under it, MJX's 4-slot plane manifold) is from MuJoCo's prism decomposition
-(oracle_hfield_prisms: every grid triangle under the foot extruded to the base, exact SAT per prism).
+"""The oracle's height-field contacts (collide_hfield_convex: MuJoCo's prism decomposition with the
+Minkowski-face axis set, the tie rule and MJX's 4 slots) against the brute-force prism reference
+(oracle_hfield_prisms: the same prisms, every separating axis, no filter, no tie rule).
 
 Both are evaluated by the oracle on the same states: the final substep of env-steps of the rough
 scenes with domain randomisation (C4: rough_terrain, C5's shard: rough_terrain_backlash), random
-U(-1,1) actions. Per foot and env-step: contact flag (any penetration) of each model, the deepest
-penetration of each, and the angle between their deepest contacts' normals. CPU only.
+U(-1,1) actions. Per foot and env-step: contact flag (any penetration) of each, the deepest
+penetration of each, the angle between their deepest contacts' normals, and whether the 4 slots
+hold the 4 deepest prisms' depths. CPU only.
 
 usage: python tools/hfield_deviation.py [n_envs] [n_steps]   (prints one JSON line per scene)
 """
@@ -29,8 +30,10 @@ from tests.oracle_ffi import OracleData, OracleEnv, OracleModel, lib  # noqa: E4
 
 def prisms(om, d, g_hf, g_foot, max_n=64):
     dep, nrm, pt = np.zeros(max_n), np.zeros(3 * max_n), np.zeros(3 * max_n)
+    idx = np.zeros(max_n, dtype=np.int32)
     dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
-    n = lib().oracle_hfield_prisms(om.ptr, C.byref(d), g_hf, g_foot, max_n, dp(dep), dp(nrm), dp(pt))
+    n = lib().oracle_hfield_prisms(om.ptr, C.byref(d), g_hf, g_foot, max_n, dp(dep), dp(nrm), dp(pt),
+                                   idx.ctypes.data_as(C.POINTER(C.c_int32)))
     return dep[:n], nrm[:3 * n].reshape(n, 3)
 
 
@@ -64,9 +67,12 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
                     n1 = frames[int(np.argmin(dist))][:3]
                     n2 = nrm[int(np.argmax(dep))]
                     ang = float(np.degrees(np.arccos(np.clip(n1 @ n2, -1, 1))))
-                rows.append((ours > 0, ref > 0, max(ours, 0.0), max(ref, 0.0), ang))
+                top = np.sort(dep)[::-1][:4]
+                mine = np.sort(-dist[dist < 0])[::-1]
+                slots = float(np.abs(top - mine).max(initial=0.0)) if len(top) == len(mine) else np.inf
+                rows.append((ours > 0, ref > 0, max(ours, 0.0), max(ref, 0.0), ang, slots, len(dep)))
     a = np.array(rows, dtype=float)
-    flag_o, flag_r, dep_o, dep_r, ang = a.T
+    flag_o, flag_r, dep_o, dep_r, ang, slots, nprism = a.T
     both = (flag_o > 0) & (flag_r > 0)
     dd = np.abs(dep_o - dep_r)[both]
     return {"scene": task, "foot_samples": len(a), "contact_ours": int(flag_o.sum()), "contact_prism": int(flag_r.sum()),
@@ -75,7 +81,9 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
             "depth_abs_diff_m": {"median": float(np.median(dd)), "p99": float(np.quantile(dd, 0.99)), "max": float(dd.max())},
             "depth_prism_median_m": float(np.median(dep_r[both])),
             "normal_angle_deg": {"median": float(np.nanmedian(ang)), "p99": float(np.nanquantile(ang, 0.99)),
-                                 "max": float(np.nanmax(ang))}}
+                                 "max": float(np.nanmax(ang))},
+            "slots_hold_4_deepest_max_abs_diff_m": float(slots.max()),
+            "penetrating_prisms_per_foot": {"mean": float(nprism[flag_r > 0].mean()), "max": int(nprism.max())}}
 
 
 def main():
