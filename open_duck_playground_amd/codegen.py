@@ -271,6 +271,19 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         c = chain_of(m, m.geom_bodyid[m.id("geom", g)])
         put(name, c + [-1] * (maxchain_of(m) - len(c)))
     put("hull", [f2i(x) for x in np.asarray(m.hulls[0].vert, dtype=np.float64).reshape(-1)])
+    # height-field prism SAT (TPhys::collide_hfield): per hull face its outward normal and offset,
+    # per hull edge the Gauss-map arc of the negated hull (C = -n_A, D = -n_B), D x C, the edge
+    # vector and its first vertex (mesh frame)
+    hull = m.hulls[0]
+    put("hface", [f2i(x) for f in range(len(hull.face_normal))
+                  for x in list(hull.face_normal[f]) + [hull.face_offset[f]]])  # stride 4
+    hef = hull_edge_faces(hull)
+    rec = []
+    for e, (a, b) in enumerate(hull.edge):
+        C_, D_ = -np.asarray(hull.face_normal[hef[e][0]]), -np.asarray(hull.face_normal[hef[e][1]])
+        v0, v1 = np.asarray(hull.vert[a]), np.asarray(hull.vert[b])
+        rec += [f2i(x) for x in np.concatenate([C_, D_, np.cross(D_, C_), v1 - v0, v0, [0.0]])]
+    put("hedge", rec)  # stride 16: C3, D3, DxC3, edge3, v0 3, pad
     d2f, d2l = [-1] * nv, [-1] * nv
     for r, i in enumerate(fric):
         d2f[i] = r
@@ -473,6 +486,14 @@ def model_header(m: Model, variant: str) -> str:
     hc = hull.vert.mean(axis=0)
     hr = float(np.max(np.linalg.norm(hull.vert - hc, axis=1)))
     hef = hull_edge_faces(hull)
+    # height field: the most grid cells the hull's bounding box can span along x / y in any
+    # orientation, floor(diameter / cell) + 2 (the prism loop's static bound)
+    diam = float(np.max(np.linalg.norm(hull.vert[:, None, :] - hull.vert[None, :, :], axis=2)))
+    if int(m.hfield_nrow) > 1 and int(m.hfield_ncol) > 1:
+        cell = (2 * float(m.hfield_size[0]) / (int(m.hfield_ncol) - 1), 2 * float(m.hfield_size[1]) / (int(m.hfield_nrow) - 1))
+        hf_cells = tuple(min(int(diam // c) + 2, n - 1) for c, n in zip(cell, (int(m.hfield_ncol), int(m.hfield_nrow))))
+    else:
+        hf_cells = (1, 1)
     pre = f"DuckModel_{variant}"
     dev = [f"__device__ const float {pre}_hull_vert_d[{len(hull.vert)}][3] = {_arr('x', hull.vert, 'float').split('= ', 1)[1]}",
            f"__device__ const float {pre}_hull_face_normal_d[{len(hull.face_normal)}][3] = {_arr('x', hull.face_normal, 'float').split('= ', 1)[1]}",
@@ -497,6 +518,7 @@ def model_header(m: Model, variant: str) -> str:
            f"  static constexpr int FLOOR_TYPE = {m.geom_type[floor]};\n",
            f"  static constexpr int HF_NROW = {int(m.hfield_nrow)}, HF_NCOL = {int(m.hfield_ncol)};\n",
            f"  static constexpr float HF_SIZE[4] = {{{', '.join(_f(x) for x in m.hfield_size)}}};\n",
+           f"  static constexpr int HF_MAXCX = {hf_cells[0]}, HF_MAXCY = {hf_cells[1]};  // cells a hull's box spans\n",
            f"  static constexpr float timestep = {_f(m.opt_timestep)}, impratio = {_f(m.opt_impratio)};\n",
            f"  static constexpr float tolerance = {_f(m.opt_tolerance)}, ls_tolerance = {_f(m.opt_ls_tolerance)};\n",
            f"  static constexpr float meaninertia = {_f(m.stat_meaninertia)};\n",

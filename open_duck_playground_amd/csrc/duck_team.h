@@ -9,8 +9,9 @@
 // issue order).
 //
 // The env slice is contiguous (element k of env t at lds[t*STRIDE + k]); STRIDE = 16 mod 32
-// so the two teams of a 32-lane half hit disjoint banks. Rare paths (foot/foot contact)
-// fall back to the single-lane code of duck_physics.h executed identically by all 16 lanes.
+// so the two teams of a 32-lane half hit disjoint banks. The rare foot/foot contact runs its
+// hull/hull SAT and dense Newton direction team-parallel too, out of line (collide_hulls_rare,
+// newton_dense).
 #pragma once
 #include <utility>
 
@@ -100,6 +101,12 @@ DK int hmin8i(int v) {
   v = min(v, dppi<0x141>(v));
   return v;
 }
+
+// the height field's contact point when no vertex of either shape is inside the other: the
+// support features' vertices within this band (m) of the support plane (oracle HF_WITNESS_BAND)
+constexpr float HF_WITNESS_BAND = 1e-3f;
+// depths within this (m) of the deepest prism contact count as equal (oracle HF_DEPTH_TIE)
+constexpr float HF_DEPTH_TIE = 1e-6f;
 
 #ifndef DUCK_LS_DFLOOR
 #define DUCK_LS_DFLOOR 1e-6f
@@ -1145,40 +1152,6 @@ struct TPhys {
   }
 
   // ---------------- collision ----------------
-  // height-field terrain under a point (hfield frame): elevation of MuJoCo's triangulated
-  // grid (cell split along its (0,0)-(1,1) diagonal) and the triangle's unit normal
-  static DK float hf_point(const float* hf, float x, float y, float* nrm) {
-    constexpr int NR = Md::HF_NROW > 1 ? Md::HF_NROW : 2, NCc = Md::HF_NCOL > 1 ? Md::HF_NCOL : 2;
-    constexpr float sx = Md::HF_SIZE[0], sy = Md::HF_SIZE[1], sz = Md::HF_SIZE[2];
-    constexpr float dx = 2.0f * sx / (NCc - 1), dy = 2.0f * sy / (NR - 1);
-    const float fx = (x + sx) / dx, fy = (y + sy) / dy;
-    const int c = min(max((int)floorf(fx), 0), NCc - 2), r = min(max((int)floorf(fy), 0), NR - 2);
-    const float u = fminf(fmaxf(fx - (float)c, 0.0f), 1.0f), w = fminf(fmaxf(fy - (float)r, 0.0f), 1.0f);
-    const float z00 = sz * hf[r * NCc + c], z10 = sz * hf[r * NCc + c + 1];
-    const float z01 = sz * hf[(r + 1) * NCc + c], z11 = sz * hf[(r + 1) * NCc + c + 1];
-    float z;
-    if (u >= w) {
-      z = z00 + u * (z10 - z00) + w * (z11 - z10);
-      nrm[0] = -(z10 - z00) * dy; nrm[1] = dx * (z10 - z11); nrm[2] = dx * dy;
-    } else {
-      z = z00 + w * (z01 - z00) + u * (z11 - z01);
-      nrm[0] = dy * (z01 - z11); nrm[1] = -dx * (z01 - z00); nrm[2] = dx * dy;
-    }
-    const float inv = 1.0f / sqrtf(nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2]);
-    nrm[0] *= inv; nrm[1] *= inv; nrm[2] *= inv;
-    return z;
-  }
-  // signed distance of a world point to the terrain (triangle plane under it) and the
-  // terrain normal in world coordinates
-  static DK float hf_dist(const float* hf, const float* pp, const float* PR, const float* vw, float* nw) {
-    const float d[3] = {vw[0] - pp[0], vw[1] - pp[1], vw[2] - pp[2]};
-    float pl[3], nl[3];
-    mulmtv3(pl, PR, d);
-    const float z = hf_point(hf, pl[0], pl[1], nl);
-    mulmv3(nw, PR, nl);
-    return (pl[2] - z) * nl[2];
-  }
-
   // world frame of collision geom slot gs (1 left foot, 2 right foot: moving bodies)
   static DK void cgeom_frame(LP L, int gs, float* gp, float* gR) {
     const int o = Md::B_CGEOM + 16 * gs, b = ti(o);
@@ -1190,9 +1163,9 @@ struct TPhys {
     mulmm3(gR, R, gm);
   }
 
-  // floor (plane or height field) vs hull for both feet at once: lanes 0-7 take the first
-  // floor pair, 8-15 the second
-  static DK void collide_planes(LP L, int lane, const float* hf) {
+  // plane floor vs hull for both feet at once (mjx collision_convex.plane_convex): lanes 0-7 take
+  // the first floor pair, 8-15 the second
+  static DK void collide_planes(LP L, int lane) {
     constexpr int NH = Md::NHV;
     const int h = lane >> 3, sub = lane & 7;
     const int p = Md::PLANE_PAIR[0] * (1 - h) + Md::PLANE_PAIR[1] * h;
@@ -1215,15 +1188,7 @@ struct TPhys {
       const int k = sub + 8 * r;
       const bool ok = k < NH;
       vx[r] = ok ? HVf(k, 0) : 0.0f; vy[r] = ok ? HVf(k, 1) : 0.0f; vz[r] = ok ? HVf(k, 2) : 0.0f;
-      if constexpr (Md::FLOOR_TYPE == 0) {
-        sup[r] = ok ? (pl[0] - vx[r]) * nl[0] + (pl[1] - vy[r]) * nl[1] + (pl[2] - vz[r]) * nl[2] : -1e30f;
-      } else {
-        const float v[3] = {vx[r], vy[r], vz[r]};
-        float vw[3], nw[3];
-        mulmv3(vw, CR, v);
-        for (int q = 0; q < 3; q++) vw[q] += cp[q];
-        sup[r] = ok ? -hf_dist(hf, pp, PR, vw, nw) : -1e30f;
-      }
+      sup[r] = ok ? (pl[0] - vx[r]) * nl[0] + (pl[1] - vy[r]) * nl[1] + (pl[2] - vz[r]) * nl[2] : -1e30f;
       smax = fmaxf(smax, sup[r]);
     }
     smax = hmax8(smax);
@@ -1244,16 +1209,6 @@ struct TPhys {
       return best < NH ? best : NH - 1;  // argmax_tol's default (also for NaN data)
     };
     auto vert = [&](int k, float* o) { o[0] = HVf(k, 0); o[1] = HVf(k, 1); o[2] = HVf(k, 2); };
-    if constexpr (Md::FLOOR_TYPE == 1) {
-      // manifold plane: the terrain normal under the deepest vertex, in the hull frame
-      const int kd = argmax(sup, 0.0f);
-      float v[3], vw[3], nw[3];
-      vert(kd, v);
-      mulmv3(vw, CR, v);
-      for (int q = 0; q < 3; q++) vw[q] += cp[q];
-      (void)hf_dist(hf, pp, PR, vw, nw);
-      mulmtv3(nl, CR, nw);
-    }
     float s[R];
     const int a = argmax(dm, 0.0f);
     float pa[3];
@@ -1310,19 +1265,421 @@ struct TPhys {
       float v[3], vw[3], pos[3], nw[3], fr[9];
       vert(me, v);
       mulmv3(vw, CR, v);
-      float sp;
-      if constexpr (Md::FLOOR_TYPE == 0) {
-        sp = (pl[0] - v[0]) * nl[0] + (pl[1] - v[1]) * nl[1] + (pl[2] - v[2]) * nl[2];
-        nw[0] = n[0]; nw[1] = n[1]; nw[2] = n[2];
-        for (int q = 0; q < 3; q++) vw[q] += cp[q];
-      } else {
-        for (int q = 0; q < 3; q++) vw[q] += cp[q];
-        sp = -hf_dist(hf, pp, PR, vw, nw);
-      }
+      const float sp = (pl[0] - v[0]) * nl[0] + (pl[1] - v[1]) * nl[1] + (pl[2] - v[2]) * nl[2];
+      nw[0] = n[0]; nw[1] = n[1]; nw[2] = n[2];
+      for (int q = 0; q < 3; q++) vw[q] += cp[q];
       const float dist = unique ? -sp : 1.0f;
       for (int q = 0; q < 3; q++) pos[q] = vw[q] - 0.5f * dist * nw[q];
       make_frame(fr, nw);
       P1::store_contact(Ls, 4 * p + sub, dist, pos, fr);
+    }
+  }
+
+  // ---------------- height field: MuJoCo's prism decomposition ----------------
+  // oracle/duck_oracle.c collide_hfield_convex in fp32 (MuJoCo mjc_ConvexHField; DESIGN.md §5 item
+  // 6): the hull's bounding box in the field's frame selects the sub-grid; each cell's two
+  // triangles (MuJoCo's strip triangulation, diagonal (c, r+1)-(c+1, r)) are the tops of prisms
+  // down to -size[3]; every prism that passes the height test is collided with the hull by the
+  // exact separating-axis penetration over the faces of the Minkowski difference P - H (prism
+  // faces, hull faces, edge pairs whose Gauss-map arcs cross; equal overlaps: the first in the
+  // oracle's order), one contact per prism at the penetration-weighted centroid of the vertices of
+  // each shape inside the other; the 4 slots are filled by mjx's _manifold_points from the
+  // deepest. The 8 lanes of a half-team work one prism at a time (hull vertices, faces and edges
+  // l + 8j on lane l); prism q's contact is kept by lane q & 7 in its slot q >> 3. The prism's
+  // bottom-edge pairs are not tested (the oracle tests them; they are never the minimum while the
+  // hull is above the prism's base, 0.1 m under the field: tests/test_oracle_physics.py).
+  // Coordinates: "local" = the field's axes with the origin at the hull frame, "mesh" = the hull frame.
+  static DK float hmin8f(float v) { return -hmax8(-v); }
+  static DK void collide_hfield(LP L, int lane, const float* hf) {
+    constexpr int NH = Md::NHV, NF = Md::NHF, NE = Md::NHE;
+    constexpr int NR = Md::HF_NROW, NCc = Md::HF_NCOL;
+    constexpr float SX = Md::HF_SIZE[0], SY = Md::HF_SIZE[1], SZ = Md::HF_SIZE[2], SB = Md::HF_SIZE[3];
+    constexpr float DXC = 2.0f * SX / (NCc - 1), DYC = 2.0f * SY / (NR - 1);
+    constexpr int MAXP = 2 * Md::HF_MAXCX * Md::HF_MAXCY, PPL = (MAXP + 7) / 8;
+    constexpr int VPL = (NH + 7) / 8, FPL = (NF + 7) / 8, EPL = (NE + 7) / 8;
+    constexpr int PRIO_T = 5 + NF, PRIO_V = 5 + NF + 3 * NE, NOPRIO = 1 << 28;
+    const int h = lane >> 3, sub = lane & 7;
+    const int p = Md::PLANE_PAIR[0] * (1 - h) + Md::PLANE_PAIR[1] * h;
+    const int gs = cgeom_slot<Md>(Md::pair_geom2[p]);
+    float pp[3], PR[9], cp[3], CR[9];
+    S1 Ls{L};
+    P1::geom_frame(Ls, 0, pp, PR);
+    cgeom_frame(L, gs, cp, CR);
+    float R[9], t[3];  // mesh -> local rotation; the hull frame's origin in the field frame
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) R[3 * a + b] = PR[a] * CR[b] + PR[3 + a] * CR[3 + b] + PR[6 + a] * CR[6 + b];
+    {
+      const float d[3] = {cp[0] - pp[0], cp[1] - pp[1], cp[2] - pp[2]};
+      mulmtv3(t, PR, d);
+    }
+    const float zc[3] = {R[6], R[7], R[8]};  // the field's z axis in the mesh frame
+    // this lane's hull vertices (local) and the hull's bounding box
+    float xl[VPL][3];
+    bool vok[VPL];
+    float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
+    const float GN = 1.0f / sqrtf(DXC * DXC + DYC * DYC);
+    const float GX = DYC * GN, GY = DXC * GN;  // the cells' diagonal side normal (dy, dx) / |.|
+    float gmin = 1e30f, gmax = -1e30f;
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+      const int k = sub + 8 * i;
+      vok[i] = k < NH;
+      const int kk = vok[i] ? k : 0;
+      const float v[3] = {tf(Md::B_HULL + 3 * kk), tf(Md::B_HULL + 3 * kk + 1), tf(Md::B_HULL + 3 * kk + 2)};
+      mulmv3(xl[i], R, v);
+      if (vok[i]) {
+        for (int a = 0; a < 3; a++) { lo[a] = fminf(lo[a], xl[i][a]); hi[a] = fmaxf(hi[a], xl[i][a]); }
+        const float g = GX * xl[i][0] + GY * xl[i][1];
+        gmin = fminf(gmin, g);
+        gmax = fmaxf(gmax, g);
+      }
+    }
+    for (int a = 0; a < 3; a++) { lo[a] = hmin8f(lo[a]); hi[a] = hmax8(hi[a]); }
+    gmin = hmin8f(gmin);
+    gmax = hmax8(gmax);
+    // the field's box and the sub-grid (vertex columns cmin..cmax, rows rmin..rmax)
+    const bool inside = !(hi[0] + t[0] < -SX || lo[0] + t[0] > SX || hi[1] + t[1] < -SY || lo[1] + t[1] > SY ||
+                          lo[2] + t[2] > SZ || hi[2] + t[2] < -SB);
+    // grid coordinates relative to the field's centre (vertex c at (c - (ncol - 1) / 2) dx): the
+    // robot walks near the centre, where these keep fp32's resolution (x + size would round to
+    // ~1e-6 m at size = 10 m)
+    constexpr float FXC = (NCc - 1) / (2.0f * SX), FYC = (NR - 1) / (2.0f * SY);
+    constexpr float CC0 = 0.5f * (NCc - 1), RC0 = 0.5f * (NR - 1);
+    const int cmin = max((int)floorf((lo[0] + t[0]) * FXC + CC0), 0);
+    const int cmax = min((int)ceilf((hi[0] + t[0]) * FXC + CC0), NCc - 1);
+    const int rmin = max((int)floorf((lo[1] + t[1]) * FYC + RC0), 0);
+    const int rmax = min((int)ceilf((hi[1] + t[1]) * FYC + RC0), NR - 1);
+    const int ncx = inside ? min(max(cmax - cmin, 0), Md::HF_MAXCX) : 0;
+    const int ncy = inside ? min(max(rmax - rmin, 0), Md::HF_MAXCY) : 0;
+    const int np = 2 * ncx * ncy;
+    const float X0 = ((float)cmin - CC0) * DXC - t[0], Y0 = ((float)rmin - RC0) * DYC - t[1];
+    const float base = -SB - t[2];  // the prisms' bottom (local z)
+    // the hull's lowest point along each side normal (the six directions of the two triangle
+    // kinds: A (-x, +g, -y), B (-g, +x, +y))
+    const float smin[2][3] = {{-hi[0], gmin, -hi[1]}, {-gmax, lo[0], lo[1]}};
+    // vertical-edge pairs: this lane's hull edges whose negated Gauss arc crosses the field's
+    // equator (silhouette edges seen along z); the crossing direction w (mesh) and the hull's
+    // support along it
+    float wv[EPL][3], wh[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; j++) {
+      const int e = sub + 8 * j, ee = e < NE ? e : 0, o = Md::B_HEDGE + 16 * ee;
+      const float C[3] = {tf(o), tf(o + 1), tf(o + 2)}, D[3] = {tf(o + 3), tf(o + 4), tf(o + 5)};
+      const float v0[3] = {tf(o + 12), tf(o + 13), tf(o + 14)};
+      const float sa = dot3(C, zc), sb = dot3(D, zc);
+      const bool sil = e < NE && sa * sb < 0.0f;
+      float w[3] = {fabsf(sb) * C[0] + fabsf(sa) * D[0], fabsf(sb) * C[1] + fabsf(sa) * D[1],
+                    fabsf(sb) * C[2] + fabsf(sa) * D[2]};
+      const float wn = sqrtf(dot3(w, w));
+      const float inv = sil && wn > 0.0f ? 1.0f / wn : 0.0f;
+      for (int a = 0; a < 3; a++) wv[j][a] = w[a] * inv;
+      wh[j] = sil && wn > 0.0f ? dot3(wv[j], v0) : -1e30f;
+    }
+    float cd[PPL], cn[PPL][3], cx[PPL][3];  // this lane's prism contacts: depth, normal, point (local)
+#pragma unroll
+    for (int s = 0; s < PPL; s++) {
+      cd[s] = -1.0f;
+      for (int a = 0; a < 3; a++) { cn[s][a] = 0.0f; cx[s][a] = 0.0f; }
+    }
+    for (int pi = 0; pi < np; pi++) {
+      const int rr = pi / (2 * ncx), rem = pi - rr * 2 * ncx, cc = rem >> 1, tri = rem & 1;
+      // top vertices: A = (c, r), (c, r + 1), (c + 1, r); B = (c, r + 1), (c + 1, r), (c + 1, r + 1)
+      float T[3][3];
+      {
+        const int dcs[2][3] = {{0, 0, 1}, {0, 1, 1}}, drs[2][3] = {{0, 1, 0}, {1, 0, 1}};
+        for (int k = 0; k < 3; k++) {
+          const int ci = cc + dcs[tri][k], ri = rr + drs[tri][k];
+          T[k][0] = X0 + (float)ci * DXC;
+          T[k][1] = Y0 + (float)ri * DYC;
+          T[k][2] = SZ * hf[(rmin + ri) * NCc + cmin + ci] - t[2];
+        }
+      }
+      // the prism height test
+      if (T[0][2] < lo[2] && T[1][2] < lo[2] && T[2][2] < lo[2]) continue;
+      // prism faces: top normal (z > 0) and the side normals of this triangle kind
+      float nt[3];
+      {
+        const float e0[3] = {T[1][0] - T[0][0], T[1][1] - T[0][1], T[1][2] - T[0][2]};
+        const float e1[3] = {T[2][0] - T[0][0], T[2][1] - T[0][1], T[2][2] - T[0][2]};
+        cross3(nt, e0, e1);
+        const float sg = (nt[2] < 0.0f ? -1.0f : 1.0f) / sqrtf(dot3(nt, nt));
+        for (int a = 0; a < 3; a++) nt[a] *= sg;
+      }
+      const float sx_[2][3] = {{-1.0f, GX, 0.0f}, {-GX, 1.0f, 0.0f}}, sy_[2][3] = {{0.0f, GY, -1.0f}, {-GY, 0.0f, 1.0f}};
+      float sl[3][3];
+      for (int k = 0; k < 3; k++) { sl[k][0] = sx_[tri][k]; sl[k][1] = sy_[tri][k]; sl[k][2] = 0.0f; }
+      // the axes of the prism's faces (uniform over the half-team): overlap = the prism's support
+      // minus the hull's lowest point along the axis
+      const float ptop = dot3(nt, T[0]);
+      float hm = 1e30f;
+#pragma unroll
+      for (int i = 0; i < VPL; i++)
+        if (vok[i]) hm = fminf(hm, dot3(nt, xl[i]));
+      hm = hmin8f(hm);
+      float mo = ptop - hm, mu[3];  // this lane's running minimum (overlap, priority, axis (mesh))
+      int mp = 0;
+      mulmtv3(mu, R, nt);
+      float osd[3];
+      for (int k = 0; k < 3; k++) osd[k] = sl[k][0] * T[k][0] + sl[k][1] * T[k][1] - smin[tri][k];
+      const float obot = hi[2] - base;
+      if (!(fminf(fminf(mo, obot), fminf(osd[0], fminf(osd[1], osd[2]))) > 0.0f)) continue;
+      float Tm[3][3], sm[3][3], ntm[3], hk[3];
+      for (int k = 0; k < 3; k++) {
+        mulmtv3(Tm[k], R, T[k]);
+        mulmtv3(sm[k], R, sl[k]);
+        hk[k] = T[k][2] - base;
+      }
+      for (int a = 0; a < 3; a++) ntm[a] = mu[a];
+      for (int k = 0; k < 3; k++)
+        if (osd[k] < mo) { mo = osd[k]; mp = 1 + k; for (int a = 0; a < 3; a++) mu[a] = sm[k][a]; }
+      if (obot < mo) { mo = obot; mp = 4; for (int a = 0; a < 3; a++) mu[a] = -zc[a]; }
+      // hull faces f = sub + 8j: the axis -n_f, overlap = offset_f - the prism's lowest point
+      // along n_f (a bottom vertex where n_f leans up)
+#pragma unroll
+      for (int j = 0; j < FPL; j++) {
+        const int f = sub + 8 * j, ff = f < NF ? f : 0, o = Md::B_HFACE + 4 * ff;
+        const float n[3] = {tf(o), tf(o + 1), tf(o + 2)}, off = tf(o + 3);
+        const float nz = fmaxf(dot3(n, zc), 0.0f);
+        float pm = 1e30f;
+        for (int k = 0; k < 3; k++) pm = fminf(pm, dot3(n, Tm[k]) - hk[k] * nz);
+        const float ov = off - pm;
+        if (f < NF && ov < mo) { mo = ov; mp = 5 + f; for (int a = 0; a < 3; a++) mu[a] = -n[a]; }
+      }
+      // top-edge pairs (hull edge e = sub + 8j, prism top edge k: faces nt, s_k)
+      float BxA[3][3], Em[3][3];
+      for (int k = 0; k < 3; k++) {
+        cross3(BxA[k], sm[k], ntm);
+        for (int a = 0; a < 3; a++) Em[k][a] = Tm[(k + 1) % 3][a] - Tm[k][a];
+      }
+#pragma unroll
+      for (int j = 0; j < EPL; j++) {
+        const int e = sub + 8 * j, ee = e < NE ? e : 0, o = Md::B_HEDGE + 16 * ee;
+        const float C[3] = {tf(o), tf(o + 1), tf(o + 2)}, D[3] = {tf(o + 3), tf(o + 4), tf(o + 5)};
+        const float DxC[3] = {tf(o + 6), tf(o + 7), tf(o + 8)}, ev[3] = {tf(o + 9), tf(o + 10), tf(o + 11)};
+        const float v0[3] = {tf(o + 12), tf(o + 13), tf(o + 14)};
+        const float ADC = dot3(ntm, DxC);
+        for (int k = 0; k < 3; k++) {
+          const float CBA = dot3(C, BxA[k]), DBA = dot3(D, BxA[k]), BDC = dot3(sm[k], DxC);
+          if (e < NE && CBA * DBA < 0.0f && ADC * BDC < 0.0f && CBA * BDC > 0.0f) {
+            float u[3];
+            cross3(u, ev, Em[k]);
+            const float un = sqrtf(dot3(u, u));
+            if (un >= 1e-6f * sqrtf(dot3(ev, ev)) * sqrtf(dot3(Em[k], Em[k]))) {
+              const float sg = (dot3(u, ntm) + dot3(u, sm[k]) < 0.0f ? -1.0f : 1.0f) / un;
+              for (int a = 0; a < 3; a++) u[a] *= sg;
+              const float ov = dot3(u, Tm[k]) - dot3(u, v0);
+              if (ov < mo) { mo = ov; mp = PRIO_T + 3 * e + k; for (int a = 0; a < 3; a++) mu[a] = u[a]; }
+            }
+          }
+        }
+      }
+      // vertical-edge pairs: the prism's support along w is the vertical edge at vertex k
+#pragma unroll
+      for (int j = 0; j < EPL; j++) {
+        const int e = sub + 8 * j;
+        const float q0 = dot3(wv[j], Tm[0]), q1 = dot3(wv[j], Tm[1]), q2 = dot3(wv[j], Tm[2]);
+        const int kk = q0 >= q1 ? (q0 >= q2 ? 0 : 2) : (q1 >= q2 ? 1 : 2);
+        const float ov = fmaxf(q0, fmaxf(q1, q2)) - wh[j];
+        if (ov < mo) { mo = ov; mp = PRIO_V + 3 * e + kk; for (int a = 0; a < 3; a++) mu[a] = wv[j][a]; }
+      }
+      // the minimum over the half-team; equal overlaps: the lowest priority
+      const float mn = hmin8f(mo);
+      const int wp = hmin8i(mo == mn ? mp : NOPRIO);
+      const int wl = hmin8i(mo == mn && mp == wp ? sub : 8);
+      float um[3];
+      for (int a = 0; a < 3; a++) um[a] = __shfl(mu[a], 8 * h + wl, TEAM);
+      if (!(mn > 0.0f)) continue;
+      // the contact point: hull vertices inside the prism and prism top vertices inside the hull,
+      // weighted by their penetration
+      float W = 0.0f, Cx[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int i = 0; i < VPL; i++) {
+        float pen = fminf(ptop - dot3(nt, xl[i]), xl[i][2] - base);
+        for (int k = 0; k < 3; k++) pen = fminf(pen, sl[k][0] * (T[k][0] - xl[i][0]) + sl[k][1] * (T[k][1] - xl[i][1]));
+        const float w = vok[i] ? fmaxf(pen, 0.0f) : 0.0f;
+        W += w;
+        for (int a = 0; a < 3; a++) Cx[a] += w * xl[i][a];
+      }
+      W = hsum8(W);
+      for (int a = 0; a < 3; a++) Cx[a] = hsum8(Cx[a]);
+      for (int k = 0; k < 3; k++) {
+        float pk = 1e30f;
+#pragma unroll
+        for (int j = 0; j < FPL; j++) {
+          const int f = sub + 8 * j, ff = f < NF ? f : 0, o = Md::B_HFACE + 4 * ff;
+          const float n[3] = {tf(o), tf(o + 1), tf(o + 2)};
+          if (f < NF) pk = fminf(pk, tf(o + 3) - dot3(n, Tm[k]));
+        }
+        pk = fmaxf(hmin8f(pk), 0.0f);
+        W += pk;
+        for (int a = 0; a < 3; a++) Cx[a] += pk * T[k][a];
+      }
+      float ul[3], pos[3];
+      mulmv3(ul, R, um);
+      if (W > 0.0f) {
+        const float iw = 1.0f / W;
+        for (int a = 0; a < 3; a++) pos[a] = Cx[a] * iw;
+      } else {
+        // crossing edges: the midpoint of the two shapes' support features along u
+        float hmu = 1e30f;
+#pragma unroll
+        for (int i = 0; i < VPL; i++)
+          if (vok[i]) hmu = fminf(hmu, dot3(ul, xl[i]));
+        hmu = hmin8f(hmu);
+        float wh_ = 0.0f, ch[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < VPL; i++) {
+          const float w = vok[i] ? fmaxf(0.0f, 1.0f - (dot3(ul, xl[i]) - hmu) * (1.0f / HF_WITNESS_BAND)) : 0.0f;
+          wh_ += w;
+          for (int a = 0; a < 3; a++) ch[a] += w * xl[i][a];
+        }
+        wh_ = hsum8(wh_);
+        for (int a = 0; a < 3; a++) ch[a] = hsum8(ch[a]);
+        const float q[3] = {dot3(ul, T[0]), dot3(ul, T[1]), dot3(ul, T[2])};
+        const float pmx = fmaxf(q[0], fmaxf(q[1], q[2]));
+        float wp_ = 0.0f, cq[3] = {0.0f, 0.0f, 0.0f};
+        for (int k = 0; k < 3; k++) {
+          const float w = fmaxf(0.0f, 1.0f - (pmx - q[k]) * (1.0f / HF_WITNESS_BAND));
+          wp_ += w;
+          for (int a = 0; a < 3; a++) cq[a] += w * T[k][a];
+        }
+        for (int a = 0; a < 3; a++) pos[a] = 0.5f * (ch[a] / wh_ + cq[a] / wp_);
+      }
+      // kept by lane pi & 7 in slot pi >> 3
+#pragma unroll
+      for (int s = 0; s < PPL; s++) {
+        const bool mine = sub == (pi & 7) && s == (pi >> 3);
+        cd[s] = mine ? mn : cd[s];
+        for (int a = 0; a < 3; a++) {
+          cn[s][a] = mine ? ul[a] : cn[s][a];
+          cx[s][a] = mine ? pos[a] : cx[s][a];
+        }
+      }
+    }
+    // 4 slots by mjx's _manifold_points over the prism contacts, from the deepest (the first prism
+    // within HF_DEPTH_TIE of it: prisms sharing a grid vertex or edge often tie exactly); index
+    // q = sub + 8 s is the prism's strip position
+    constexpr int QN = 8 * PPL;
+    float dmax = -1e30f;
+#pragma unroll
+    for (int s = 0; s < PPL; s++) dmax = fmaxf(dmax, cd[s] > 0.0f ? cd[s] : -1e30f);
+    dmax = hmax8(dmax);
+    const bool any = dmax > 0.0f;
+    int a_ = 1 << 20;
+#pragma unroll
+    for (int s = PPL - 1; s >= 0; s--)
+      if (cd[s] > 0.0f && cd[s] >= dmax - HF_DEPTH_TIE) a_ = sub + 8 * s;
+    a_ = hmin8i(a_);
+    a_ = a_ < QN ? a_ : 0;
+    // a contact's fields, fetched from its owner lane (q uniform over the half-team)
+    auto fetch = [&](int q, float* x, float* n, float& d) {
+      float px[3], pn[3], pd = cd[0];
+      for (int a = 0; a < 3; a++) { px[a] = cx[0][a]; pn[a] = cn[0][a]; }
+#pragma unroll
+      for (int s = 1; s < PPL; s++) {
+        const bool m = (q >> 3) == s;
+        pd = m ? cd[s] : pd;
+        for (int a = 0; a < 3; a++) { px[a] = m ? cx[s][a] : px[a]; pn[a] = m ? cn[s][a] : pn[a]; }
+      }
+      const int src = 8 * h + (q & 7);
+      d = __shfl(pd, src, TEAM);
+      for (int a = 0; a < 3; a++) { x[a] = __shfl(px[a], src, TEAM); n[a] = __shfl(pn[a], src, TEAM); }
+    };
+    // argmax with mjx's tolerance: the first index within tol of the maximum (valid contacts only)
+    auto argmax = [&](const float* v, float tol) -> int {
+      float mx = -1e30f;
+#pragma unroll
+      for (int s = 0; s < PPL; s++) mx = fmaxf(mx, v[s]);
+      mx = hmax8(mx);
+      int best = 1 << 20;
+#pragma unroll
+      for (int s = PPL - 1; s >= 0; s--)
+        if (cd[s] > 0.0f && v[s] >= mx - tol) best = sub + 8 * s;
+      best = hmin8i(best);
+      return best < QN ? best : a_;
+    };
+    float pa[3], na[3], da, sc[PPL];
+    fetch(a_, pa, na, da);
+#pragma unroll
+    for (int s = 0; s < PPL; s++) {
+      const float dx = pa[0] - cx[s][0], dy = pa[1] - cx[s][1], dz = pa[2] - cx[s][2];
+      sc[s] = cd[s] > 0.0f ? dx * dx + dy * dy + dz * dz : -1e30f;
+    }
+    const int b_ = argmax(sc, MANIFOLD_TOL);
+    float pb[3], nb[3], db;
+    fetch(b_, pb, nb, db);
+    float ab[3];
+    {
+      const float amb[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
+      cross3(ab, na, amb);
+    }
+#pragma unroll
+    for (int s = 0; s < PPL; s++) {
+      const float ap[3] = {pa[0] - cx[s][0], pa[1] - cx[s][1], pa[2] - cx[s][2]};
+      sc[s] = cd[s] > 0.0f ? fabsf(dot3(ap, ab)) : -1e30f;
+    }
+    const int c_ = argmax(sc, MANIFOLD_TOL);
+    float pc[3], nc_[3], dcc;
+    fetch(c_, pc, nc_, dcc);
+    float ac[3], bc[3];
+    {
+      const float amc[3] = {pa[0] - pc[0], pa[1] - pc[1], pa[2] - pc[2]};
+      const float bmc[3] = {pb[0] - pc[0], pb[1] - pc[1], pb[2] - pc[2]};
+      cross3(ac, na, amc);
+      cross3(bc, na, bmc);
+    }
+    int d_;
+    {
+      float s1[PPL], s2[PPL], mx = -1e30f;
+#pragma unroll
+      for (int s = 0; s < PPL; s++) {
+        const float bp[3] = {pb[0] - cx[s][0], pb[1] - cx[s][1], pb[2] - cx[s][2]};
+        const float ap[3] = {pa[0] - cx[s][0], pa[1] - cx[s][1], pa[2] - cx[s][2]};
+        s1[s] = cd[s] > 0.0f ? fabsf(dot3(bp, bc)) : -1e30f;
+        s2[s] = cd[s] > 0.0f ? fabsf(dot3(ap, ac)) : -1e30f;
+        mx = fmaxf(mx, fmaxf(s1[s], s2[s]));
+      }
+      mx = hmax8(mx);
+      int best = 1 << 20;
+#pragma unroll
+      for (int s = PPL - 1; s >= 0; s--) {
+        if (cd[s] > 0.0f && s2[s] >= mx - MANIFOLD_TOL) best = QN + sub + 8 * s;
+      }
+#pragma unroll
+      for (int s = PPL - 1; s >= 0; s--) {
+        if (cd[s] > 0.0f && s1[s] >= mx - MANIFOLD_TOL) best = sub + 8 * s;
+      }
+      d_ = hmin8i(best);
+      d_ = d_ < 2 * QN ? (d_ >= QN ? d_ - QN : d_) : a_;
+    }
+    // slot sub (< 4) of this pair: its contact, repeats inactive (fetches are uniform over the
+    // half-team: a lane's shuffle source selects its slot with the requester's index)
+    float pdd[3], ndd[3], ddd;
+    fetch(d_, pdd, ndd, ddd);
+    const int myq = sub == 0 ? a_ : (sub == 1 ? b_ : (sub == 2 ? c_ : d_));
+    float px[3], pn[3], pd;
+    for (int a = 0; a < 3; a++) {
+      px[a] = sub == 0 ? pa[a] : (sub == 1 ? pb[a] : (sub == 2 ? pc[a] : pdd[a]));
+      pn[a] = sub == 0 ? na[a] : (sub == 1 ? nb[a] : (sub == 2 ? nc_[a] : ndd[a]));
+    }
+    pd = sub == 0 ? da : (sub == 1 ? db : (sub == 2 ? dcc : ddd));
+    if (sub < 4) {
+      const int idx[4] = {a_, b_, c_, d_};
+      bool unique = true;
+      for (int e = 0; e < 4; e++) unique = unique && !(e < sub && idx[e] == myq);
+      float fr[9], pw[3], nw[3];
+      if (any) {
+        const float pl[3] = {px[0] + t[0], px[1] + t[1], px[2] + t[2]};
+        mulmv3(pw, PR, pl);
+        for (int a = 0; a < 3; a++) pw[a] += pp[a];
+        mulmv3(nw, PR, pn);
+        make_frame(fr, nw);
+        P1::store_contact(Ls, 4 * p + sub, unique ? -pd : 1.0f, pw, fr);
+      } else {
+        const float nofr[9] = {0, 0, 1, 0, 1, 0, -1, 0, 0};
+        const float zero[3] = {L[Ly::COM], L[Ly::COM + 1], L[Ly::COM + 2]};
+        P1::store_contact(Ls, 4 * p + sub, 1.0f, zero, nofr);
+      }
     }
   }
 
@@ -1597,7 +1954,8 @@ struct TPhys {
 
   static DK void collision(LP L, int lane, const float* hf) {
     STAGE_T0();
-    collide_planes(L, lane, hf);
+    if constexpr (Md::FLOOR_TYPE == 1) collide_hfield(L, lane, hf);
+    else collide_planes(L, lane);
     STAGE_MARK(26);
     if (Md::FOOT_PAIR >= 0) {
       constexpr int p = Md::FOOT_PAIR;

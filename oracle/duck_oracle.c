@@ -648,16 +648,22 @@ static void collide_plane_convex(const oracle_model* m, oracle_data* d, int g1, 
  * the faces of the Minkowski difference P - H of its support function (separating-axis test over
  * the prism's 5 face normals, the hull's face normals and the edge pairs whose Gauss-map arcs
  * cross -- Gregorius, GDC 2013), and MJX's fixed DUCK_CON_PER_PAIR slots per pair, filled from the
- * prism contacts by MJX's _manifold_points starting at the deepest. Declared choices (DESIGN.md
- * §5 item 6): near-equal axes resolve to the first in the priority order (prism top, sides,
- * bottom, hull faces, edge pairs) within HF_SAT_TIE of the minimum; the contact point of a prism
+ * prism contacts by MJX's _manifold_points starting at the deepest (within HF_DEPTH_TIE). Declared choices (DESIGN.md
+ * §5 item 6): equal overlaps resolve to the first axis in the order prism top, sides, bottom, hull
+ * faces, top-edge pairs, vertical-edge pairs, bottom-edge pairs; the contact point of a prism
  * is the penetration-weighted centroid of the vertices of each shape inside the other, or, when
  * none is (crossing edges), the midpoint of the two shapes' support features (the centroid of each
  * shape's vertices within HF_WITNESS_BAND of its support plane along the normal, weighted 1 at the
  * plane to 0 at the band edge; the prism's top vertices only). */
-#define HF_SAT_TIE 1e-6      /* m; = codegen.HF_SAT_TIE */
-#define HF_WITNESS_BAND 1e-3 /* m; = codegen.HF_WITNESS_BAND */
+#define HF_WITNESS_BAND 1e-3 /* m; = TPhys HF_WITNESS_BAND */
+#define HF_DEPTH_TIE 1e-6    /* m; = TPhys HF_DEPTH_TIE: prisms sharing a grid vertex or edge often tie exactly */
 #define HF_MAXPRISM 128      /* prisms under one hull (the sub-grid of a 0.11 m foot: <= 18) */
+
+/* test aid: how often each class of separating axis gave a prism's penetration (oracle_hfield_axis_wins) */
+static long long hf_axis_wins[7];
+void oracle_hfield_axis_wins(long long out[7], int reset) {
+  for (int i = 0; i < 7; i++) { out[i] = hf_axis_wins[i]; if (reset) hf_axis_wins[i] = 0; }
+}
 
 /* the hull in the local frame (the height field's axes, origin at the hull's frame) */
 typedef struct {
@@ -720,6 +726,7 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
   /* candidate axes in priority order */
   enum { NAX = 5 + DUCK_MAXHULLF + 9 * DUCK_MAXHULLE };
   double ax[NAX][3], ov[NAX];
+  int kind_of_axis[NAX];
   int na = 0;
   memcpy(ax[na++], nt, sizeof(nt));
   for (int k = 0; k < 3; k++) memcpy(ax[na++], s[k], sizeof(double) * 3);
@@ -727,40 +734,42 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
   for (int f = 0; f < H->nf; f++)
     for (int a = 0; a < 3; a++) ax[na + f][a] = -H->FN[f][a];
   na += H->nf;
-  /* prism edges: top k (T_k, T_k+1; faces nt, s_k), vertical k (at vertex k; faces s_k-1, s_k),
-   * bottom k (faces -z, s_k) */
+  /* edge pairs, in the order top edges (hull edge e, prism top edge k), vertical edges (e, k),
+   * bottom edges (e, k): prism top edge k (T_k, T_k+1; faces nt, s_k), vertical edge k (at
+   * vertex k; faces s_k-1, s_k), bottom edge k (faces -z, s_k) */
   const double mz[3] = {0, 0, -1};
-  for (int e = 0; e < H->ne; e++) {
-    const int v0 = m->hull_edge[e][0], v1 = m->hull_edge[e][1];
-    const double *nA = H->FN[m->hull_edge_face[e][0]], *nB = H->FN[m->hull_edge_face[e][1]];
-    const double C[3] = {-nA[0], -nA[1], -nA[2]}, D[3] = {-nB[0], -nB[1], -nB[2]};
-    double eh[3];
-    for (int a = 0; a < 3; a++) eh[a] = H->V[v1][a] - H->V[v0][a];
-    for (int q = 0; q < 9; q++) {
-      const int k = q % 3, kind = q / 3;
-      const double *fa, *fb;
-      double ep[3];
-      if (kind == 0) {
-        fa = nt; fb = s[k];
-        for (int a = 0; a < 3; a++) ep[a] = T[(k + 1) % 3][a] - T[k][a];
-      } else if (kind == 1) {
-        fa = s[(k + 2) % 3]; fb = s[k];
-        ep[0] = 0; ep[1] = 0; ep[2] = 1;
-      } else {
-        fa = mz; fb = s[k];
-        for (int a = 0; a < 2; a++) ep[a] = T[(k + 1) % 3][a] - T[k][a];
-        ep[2] = 0;
+  for (int kind = 0; kind < 3; kind++)
+    for (int e = 0; e < H->ne; e++) {
+      const int v0 = m->hull_edge[e][0], v1 = m->hull_edge[e][1];
+      const double *nA = H->FN[m->hull_edge_face[e][0]], *nB = H->FN[m->hull_edge_face[e][1]];
+      const double C[3] = {-nA[0], -nA[1], -nA[2]}, D[3] = {-nB[0], -nB[1], -nB[2]};
+      double eh[3];
+      for (int a = 0; a < 3; a++) eh[a] = H->V[v1][a] - H->V[v0][a];
+      for (int k = 0; k < 3; k++) {
+        const double *fa, *fb;
+        double ep[3];
+        if (kind == 0) {
+          fa = nt; fb = s[k];
+          for (int a = 0; a < 3; a++) ep[a] = T[(k + 1) % 3][a] - T[k][a];
+        } else if (kind == 1) {
+          fa = s[(k + 2) % 3]; fb = s[k];
+          ep[0] = 0; ep[1] = 0; ep[2] = 1;
+        } else {
+          fa = mz; fb = s[k];
+          for (int a = 0; a < 2; a++) ep[a] = T[(k + 1) % 3][a] - T[k][a];
+          ep[2] = 0;
+        }
+        if (!minkowski_face(fa, fb, C, D)) continue;
+        double u[3];
+        cross3(u, eh, ep);
+        const double un = norm3(u);
+        if (un < 1e-6 * norm3(eh) * norm3(ep)) continue;
+        const double sg = (dot3(u, fa) + dot3(u, fb)) < 0 ? -1.0 : 1.0;
+        for (int a = 0; a < 3; a++) ax[na][a] = sg * u[a] / un;
+        kind_of_axis[na] = kind;
+        na++;
       }
-      if (!minkowski_face(fa, fb, C, D)) continue;
-      double u[3];
-      cross3(u, eh, ep);
-      const double un = norm3(u);
-      if (un < 1e-9 * norm3(eh) * norm3(ep)) continue;
-      const double sg = (dot3(u, fa) + dot3(u, fb)) < 0 ? -1.0 : 1.0;
-      for (int a = 0; a < 3; a++) ax[na][a] = sg * u[a] / un;
-      na++;
     }
-  }
   double mn = 1e300;
   for (int i = 0; i < na; i++) {
     ov[i] = pts_max(ax[i], (const double(*)[3])P, 6) - pts_min(ax[i], (const double(*)[3])H->V, H->nv);
@@ -768,7 +777,17 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
   }
   if (!(mn > 0)) return 0;
   int w = 0;
-  while (ov[w] > mn + HF_SAT_TIE) w++;
+  while (ov[w] > mn) w++;
+  {
+    /* which class of axis won (hf_axis_wins: prism top, sides, bottom, hull faces, top-edge,
+     * vertical-edge, bottom-edge pairs) */
+    int cls = w == 0 ? 0 : (w < 4 ? 1 : (w == 4 ? 2 : (w < 5 + H->nf ? 3 : 4)));
+    if (cls == 4) cls = 4 + kind_of_axis[w];
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+    hf_axis_wins[cls]++;
+  }
   const double* u = ax[w];
   /* the contact point: the centroid of the vertices of each shape inside the other (hull
    * vertices inside the prism, prism top vertices inside the hull), each weighted by its
@@ -884,12 +903,14 @@ static void collide_hfield_convex(const oracle_model* m, oracle_data* d, int g1,
         if (hf_prism_contact(m, &H, (const double(*)[3])T, base, &dep[n], nrm[n], pt[n])) n++;
       }
   if (n == 0) return;
-  /* 4 of the prism contacts by mjx's _manifold_points over their points, from the deepest (first
-   * in strip order among equal depths), areas taken in the plane of its normal; repeats stay
-   * inactive (plane_convex's rule) */
+  /* 4 of the prism contacts by mjx's _manifold_points over their points, from the deepest (the
+   * first in strip order within HF_DEPTH_TIE of the deepest: prisms that share a grid vertex or
+   * edge often reach the same depth through it), areas taken in the plane of its normal; repeats
+   * stay inactive (plane_convex's rule) */
+  double dmax = dep[0];
+  for (int i = 1; i < n; i++) dmax = fmax(dmax, dep[i]);
   int a = 0;
-  for (int i = 1; i < n; i++)
-    if (dep[i] > dep[a]) a = i;
+  while (dep[a] < dmax - HF_DEPTH_TIE) a++;
   int mask[HF_MAXPRISM], idx[4];
   for (int i = 0; i < n; i++) mask[i] = 1;
   manifold_points_from((const double(*)[3])pt, mask, n, nrm[a], a, idx);

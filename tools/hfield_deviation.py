@@ -6,8 +6,8 @@ Minkowski-face axis set, the tie rule and MJX's 4 slots) against the brute-force
 Both are evaluated by the oracle on the same states: the final substep of env-steps of the rough
 scenes with domain randomisation (C4: rough_terrain, C5's shard: rough_terrain_backlash), random
 U(-1,1) actions. Per foot and env-step: contact flag (any penetration) of each, the deepest
-penetration of each, the angle between their deepest contacts' normals, and whether the 4 slots
-hold the 4 deepest prisms' depths. CPU only.
+penetration of each, the angle between their deepest contacts' normals, and which class of axis
+gave the prism contacts (the kernel skips the bottom-edge pairs: never the minimum). CPU only.
 
 usage: python tools/hfield_deviation.py [n_envs] [n_steps]   (prints one JSON line per scene)
 """
@@ -49,6 +49,8 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
         pairs[g] = p
     rng = np.random.default_rng(seed)
     rows = []
+    wins = (C.c_longlong * 7)()
+    lib().oracle_hfield_axis_wins(wins, 1)
     for e in range(n_envs):
         om = OracleModel(m, dr=base.dr_sample(seed + 1, e))
         env = OracleEnv(om, cfg)
@@ -67,12 +69,10 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
                     n1 = frames[int(np.argmin(dist))][:3]
                     n2 = nrm[int(np.argmax(dep))]
                     ang = float(np.degrees(np.arccos(np.clip(n1 @ n2, -1, 1))))
-                top = np.sort(dep)[::-1][:4]
-                mine = np.sort(-dist[dist < 0])[::-1]
-                slots = float(np.abs(top - mine).max(initial=0.0)) if len(top) == len(mine) else np.inf
-                rows.append((ours > 0, ref > 0, max(ours, 0.0), max(ref, 0.0), ang, slots, len(dep)))
+                rows.append((ours > 0, ref > 0, max(ours, 0.0), max(ref, 0.0), ang, len(dep)))
+    lib().oracle_hfield_axis_wins(wins, 1)
     a = np.array(rows, dtype=float)
-    flag_o, flag_r, dep_o, dep_r, ang, slots, nprism = a.T
+    flag_o, flag_r, dep_o, dep_r, ang, nprism = a.T
     both = (flag_o > 0) & (flag_r > 0)
     dd = np.abs(dep_o - dep_r)[both]
     return {"scene": task, "foot_samples": len(a), "contact_ours": int(flag_o.sum()), "contact_prism": int(flag_r.sum()),
@@ -82,7 +82,8 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
             "depth_prism_median_m": float(np.median(dep_r[both])),
             "normal_angle_deg": {"median": float(np.nanmedian(ang)), "p99": float(np.nanquantile(ang, 0.99)),
                                  "max": float(np.nanmax(ang))},
-            "slots_hold_4_deepest_max_abs_diff_m": float(slots.max()),
+            "axis_wins": dict(zip(("top", "side", "bottom", "hull_face", "top_edge", "vertical_edge", "bottom_edge"),
+                                  [int(x) for x in wins])),
             "penetrating_prisms_per_foot": {"mean": float(nprism[flag_r > 0].mean()), "max": int(nprism.max())}}
 
 
