@@ -191,7 +191,7 @@ def main():
     pool = [torch.rand(n, env.action_size, device=dev, generator=g) * 2 - 1 for _ in range(8)]
 
     for i in range(args.warmup):
-        env.step(state, pool[i % len(pool)])
+        env.step(state, pool[i % len(pool)], inplace=True)
     K = args.steps
     # launch durations from HIP events on every 8th timed launch: bracketing every launch puts two
     # event records between back-to-back kernels and cost 2.3 % of the wall time (same box, 400
@@ -209,10 +209,10 @@ def main():
     for i in range(K):
         if ev[i] is not None:
             ev[i][0].record()
-            env.step(state, pool[i % len(pool)])
+            env.step(state, pool[i % len(pool)], inplace=True)
             ev[i][1].record()
         else:
-            env.step(state, pool[i % len(pool)])
+            env.step(state, pool[i % len(pool)], inplace=True)
     ev_all[1].record()
     torch.cuda.synchronize()
     if world > 1:

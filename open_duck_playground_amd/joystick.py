@@ -10,9 +10,13 @@ that follow from running a batch of envs in one launch on the GPU:
   tensor in ``State`` has a leading env axis (what brax's ``VmapWrapper`` produces),
 * ``rng`` is an integer seed; env ``i`` draws from a counter-based threefry stream keyed
   by ``(seed, env_offset + i)`` (shard-invariant), not a JAX key,
-* ``step`` advances the state buffers in place and returns the same ``State`` object,
+* ``step(state, action)`` returns a new ``State`` in new buffers and leaves ``state`` as it was
+  (the reference's ``state.replace(...)``, joystick.py:480-481); ``step(state, action,
+  inplace=True)`` advances ``state``'s own buffers instead (what a rollout loop that drops the
+  previous state wants: brax's jitted unroll donates them the same way),
 * physics, obs, rewards and termination all run inside ``libduck.so``
-  (``csrc/duck_kernels.hip``); this module only allocates torch buffers and launches.
+  (``csrc/duck_env_kernels.h`` via ``duck_step``); this module only allocates torch buffers and
+  launches.
 
 ``wrap_for_brax_training`` / ``domain_randomize`` provide the training-side behaviour the
 reference gets from ``mujoco_playground.wrapper`` and ``common/randomize.py``.
@@ -61,9 +65,10 @@ class State:
     istate: torch.Tensor = field(repr=False, default=None)
 
     def replace(self, **kw) -> "State":
-        for k, v in kw.items():
-            setattr(self, k, v)
-        return self
+        """A new State with the given fields replaced (flax struct.dataclass semantics); the
+        tensors themselves are shared, not copied."""
+        import dataclasses
+        return dataclasses.replace(self, **kw)
 
 
 class OpenDuckMiniV2Env:
@@ -286,12 +291,18 @@ class Joystick(OpenDuckMiniV2Env):
             state.done.zero_()
         return state
 
-    def step(self, state: State, action: torch.Tensor) -> State:
-        """Joystick.step (joystick.py:323-481) for all envs, in place."""
+    def step(self, state: State, action: torch.Tensor, inplace: bool = False) -> State:
+        """Joystick.step (joystick.py:323-481) for all envs: the next State, in new buffers (``state``
+        is left as it was), or with ``inplace=True`` in ``state``'s own buffers (returned)."""
         n = self.num_envs
         if action.numel() != n * self.action_size:
             raise DuckError(f"action must hold {n} x {self.action_size} values, got {tuple(action.shape)}")
         action = action.to(device=self.device, dtype=torch.float32).reshape(n, self.action_size).contiguous()
+        if not inplace:
+            # the step reads and writes every state row (obs, reward and done are outputs only)
+            state = self._views(state.fstate.clone(), state.istate.clone(), torch.empty_like(state.obs["state"]),
+                                torch.empty_like(state.obs["privileged_state"]), torch.empty_like(state.reward),
+                                torch.empty_like(state.done))
         check(self._lib.duck_step(self._sim, n, state.fstate.data_ptr(), state.istate.data_ptr(),
                               self.dr.data_ptr() if self.dr is not None else None, action.data_ptr(),
                               state.obs["state"].data_ptr(), state.obs["privileged_state"].data_ptr(),

@@ -398,7 +398,7 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
                     raw = d.sample_raw(gen)
                     data["raw_action"][t, cols] = raw
                     data["log_prob"][t, cols] = d.log_prob(raw)
-                    env.step(state, torch.tanh(raw))
+                    env.step(state, torch.tanh(raw), inplace=True)  # obs already copied out
                     data["reward"][t, cols] = state.reward
                     data["done"][t, cols] = state.done
                     data["truncation"][t, cols] = state.info["truncation"]
@@ -450,7 +450,7 @@ def evaluate(net: ActorCritic, eval_env, cfg: PPOConfig, rng: int) -> Dict[str, 
     active = torch.ones(n, device=eval_env.device)
     for _ in range(cfg.episode_length // cfg.action_repeat):
         act = NormalTanh(net.policy_logits(state.obs[cfg.policy_obs_key])).mode()
-        eval_env.step(state, act)
+        eval_env.step(state, act, inplace=True)
         ret += state.reward * active
         length += active
         active = active * (1.0 - state.done)

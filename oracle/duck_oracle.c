@@ -71,7 +71,11 @@ struct oracle_model {
 oracle_model* oracle_model_create(const duck_model_desc* s) {
   if (s->nbody > DUCK_MAXBODY || s->nv > DUCK_MAXV || s->nq > DUCK_MAXQ || s->nu > DUCK_MAXU ||
       s->njnt > DUCK_MAXJNT || s->ngeom > DUCK_MAXGEOM || s->npair > DUCK_MAXPAIR ||
-      s->hull_nvert > DUCK_MAXHULLV || s->hull_nface > DUCK_MAXHULLF || s->hull_nedge > DUCK_MAXHULLE)
+      s->hull_nvert > DUCK_MAXHULLV || s->hull_nface > DUCK_MAXHULLF || s->hull_nedge > DUCK_MAXHULLE ||
+      s->nsite > DUCK_MAXSITE || s->nsensor > DUCK_MAXSENSOR || s->nsensordata > DUCK_MAXSENSORDATA ||
+      /* every constraint row fits the fixed-capacity Jacobian: friction <= nv, limits <= njnt, 4
+       * pyramid rows per contact slot */
+      s->nv + s->njnt + 4 * DUCK_CON_PER_PAIR * s->npair > MAXEFC)
     return NULL;
   oracle_model* m = (oracle_model*)calloc(1, sizeof(oracle_model));
   m->nq = s->nq; m->nv = s->nv; m->nu = s->nu; m->nbody = s->nbody; m->njnt = s->njnt; m->ngeom = s->ngeom;
@@ -1177,6 +1181,7 @@ static void kbi(const oracle_model* m, const double* solref, const double* solim
 static void add_row(const oracle_model* m, oracle_data* d, fwd_ws* w, const double* J, double pos,
                     double invweight, const double* solref, const double* solimp, double frictionloss, int ineq) {
   int r = w->nefc++;
+  if (r >= MAXEFC) abort(); /* fixed-capacity rows (oracle_model_create bounds nefc) */
   memcpy(w->J[r], J, sizeof(double) * NV);
   double k, b, imp;
   kbi(m, solref, solimp, pos, &k, &b, &imp);

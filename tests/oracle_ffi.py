@@ -18,7 +18,8 @@ from open_duck_playground_amd.cabi import (DuckEnvConfig, DuckRefMotion, ModelDe
 from open_duck_playground_amd.mjcf import Model
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+# ORACLE_LIB selects another build of the same checker (oracle/Makefile ASAN=1: liboracle_asan.so)
+LIB = os.environ.get("ORACLE_LIB") or os.path.join(ROOT, "oracle", "liboracle.so")
 
 MAXQ, MAXV, MAXU, MAXSD, MAXBODY, MAXSITE, MAXGEOM, MAXCON = 40, 32, 16, 64, 20, 8, 64, 16
 
@@ -51,7 +52,8 @@ class OracleData(C.Structure):
 def build(force: bool = False) -> str:
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
             os.path.getmtime(os.path.join(ROOT, "oracle", f)) for f in ("duck_oracle.c", "duck_oracle.h")):
-        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")] +
+                              (["ASAN=1"] if LIB.endswith("_asan.so") else []))
     return LIB
 
 

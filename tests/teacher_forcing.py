@@ -46,6 +46,8 @@ class Report:
     steps: List[StepStats] = field(default_factory=list)
     tol: Dict[str, float] = field(default_factory=dict)
     pre: list = field(default_factory=list)   # per step (fs, is, action) before the step (keep_states)
+    post: list = field(default_factory=list)  # per step the GPU's fstate after the step (keep_states)
+    reset: dict = field(default_factory=dict)  # the strict post-reset comparison (reset_stats)
     env: object = None
     models: object = None
 
@@ -112,6 +114,8 @@ def run(task: str, imitation: bool, n: int, steps: int, device, seed: int = 7, d
     ob.reset(seed=seed)
     rng = np.random.default_rng(action_seed)
     rep = Report(tol=default_tol(), env=env, models=models)
+    torch.cuda.synchronize()
+    rep.reset = reset_stats(L, st, ob, n)
     I = lambda name: L.ioff[name]  # noqa: E731
     for t in range(steps):
         isv = ob.is_.reshape(L.nint, n)
@@ -127,11 +131,13 @@ def run(task: str, imitation: bool, n: int, steps: int, device, seed: int = 7, d
         a = rng.uniform(-1, 1, (n, env.action_size)).astype(np.float32)
         if keep_states:
             rep.pre.append((ob.fs.copy(), ob.is_.copy(), a.copy()))
-        env.step(st, torch.from_numpy(a).to(st.fstate.device))
+        st = env.step(st, torch.from_numpy(a).to(st.fstate.device))
         ob.step(a.astype(np.float64))
         torch.cuda.synchronize()
         gf = st.fstate.cpu().numpy().astype(np.float64)
         gi = st.istate.cpu().numpy()
+        if keep_states:
+            rep.post.append(gf.copy())
         err = _fs_err(L, gf, ob.fs, n)
         obs = st.obs["state"].cpu().numpy().astype(np.float64)
         priv = st.obs["privileged_state"].cpu().numpy().astype(np.float64)
@@ -146,6 +152,33 @@ def run(task: str, imitation: bool, n: int, steps: int, device, seed: int = 7, d
                 int_mm |= GI[L.ioff[name]] != OI[L.ioff[name]]
         rep.steps.append(StepStats(err=err, done_mismatch=done_mm, int_mismatch=int_mm))
     return rep
+
+
+def reset_stats(L, st, ob, n: int) -> dict:
+    """Joystick.reset (joystick.py:206-321) strictly, field by field: every fstate row of every env
+    (state, info, the auto-reset snapshot) against oracle_env_reset at the teacher-forced bar (qpos
+    rows 1e-4, qacc_warmstart rows 2e-2, every other row 2e-3, relative to 1 + |oracle|), obs and
+    privileged obs at 2e-3, every istate word exact. Returns per-env worst row error / its bar
+    ("norm", > 1 fails), the worst row's name, and the integer / obs mismatches."""
+    A = st.fstate.cpu().numpy().astype(np.float64).reshape(L.nfloat, n)
+    B = ob.fs.reshape(L.nfloat, n)
+    tol = np.full(L.nfloat, 2e-3)
+    name = np.empty(L.nfloat, dtype=object)
+    bounds = sorted(L.off.items(), key=lambda kv: kv[1]) + [("end", L.nfloat)]
+    for (k, a), (_, b) in zip(bounds[:-1], bounds[1:]):
+        name[a:b] = k
+        if k in ("qpos", "first_qpos"):
+            tol[a:b] = 1e-4
+        elif k in ("qacc_warmstart", "first_qacc_warmstart"):
+            tol[a:b] = 2e-2
+    r = _rel(A, B) / tol[:, None]
+    worst = r.argmax(axis=0)
+    obs = st.obs["state"].cpu().numpy().astype(np.float64)
+    priv = st.obs["privileged_state"].cpu().numpy().astype(np.float64)
+    oerr = np.maximum(_rel(obs, ob.obs).max(axis=1), _rel(priv, ob.priv).max(axis=1)) / 2e-3
+    GI, OI = st.istate.cpu().numpy().reshape(L.nint, n), ob.is_.reshape(L.nint, n)
+    return {"norm": np.maximum(r.max(axis=0), oerr), "worst_row": name[worst],
+            "int_mismatch": np.any(GI != OI, axis=0), "fs_norm": r.max(axis=0), "obs_norm": oerr}
 
 
 def _short_push():
@@ -262,13 +295,17 @@ def flip_level(om, x: np.ndarray, target: np.ndarray, rng, levels=(1e-6, 1e-5)) 
     return None
 
 
-def explain(rep: Report, t: int, e: int, sub_tol: float = 1e-3, seed: int = 0) -> dict:
+def explain(rep: Report, t: int, e: int, sub_tol: float = 1e-4, seed: int = 0) -> dict:
     """Why env e differs after env-step t. The GPU replays the env-step as a chain of single
-    substeps from the oracle's substep-0 input, each from its own previous output; at every substep
-    the oracle takes the same substep from the GPU's (fp32) input. If every substep agrees (or the
-    GPU's result is a branch a 1e-6/1e-5 input perturbation of the oracle also takes), the kernel is
-    right at every state it visited and the env-step difference is the oracle's own sensitivity to
-    fp32-sized input differences, amplified over the 10 substeps: "sensitive". Otherwise "defect"."""
+    substeps (physics_kernel) from the oracle's substep-0 input, each from its own previous output;
+    at every substep the oracle takes the same substep from the GPU's (fp32) input. If every substep
+    agrees to sub_tol (or the GPU's result is a branch a 1e-6/1e-5 input perturbation of the oracle
+    also takes), the physics kernel is right at every state it visited. That explains step_kernel's
+    outlier only if the chain lands where step_kernel did (a different code object: its substeps
+    are inlined): the chain's final state must be closer to step_kernel's output than a quarter of
+    step_kernel's distance from the oracle (and within 1e-3). Then the env-step difference is the
+    oracle's own sensitivity to fp32-sized input differences, amplified over the 10 substeps:
+    "sensitive". Otherwise "defect". Needs keep_states=True."""
     env = rep.env
     m = env.mj_model
     om, tr = substep_trace(rep, e, t)
@@ -287,4 +324,16 @@ def explain(rep: Report, t: int, e: int, sub_tol: float = 1e-3, seed: int = 0) -
             flips.append((s, lev))
         x = g
     chain_vs_oracle = _state_rel(m, x, tr[-1])
-    return {"kind": "sensitive", "substep_err": per, "flips": flips, "chain_vs_oracle": chain_vs_oracle}
+    # step_kernel's own result for this env-step (qpos, qvel, qacc_warmstart; ctrl as traced)
+    L, n = env._layout, env.num_envs
+    G = rep.post[t].reshape(L.nfloat, n)[:, e]
+    o = L.off
+    step_out = np.concatenate([G[o["qpos"]:o["qpos"] + m.nq], G[o["qvel"]:o["qvel"] + m.nv],
+                               G[o["qacc_warmstart"]:o["qacc_warmstart"] + m.nv], tr[-1, m.nq + 2 * m.nv:]])
+    chain_vs_step = _state_rel(m, x, step_out)
+    step_vs_oracle = _state_rel(m, step_out, tr[-1])
+    res = {"substep_err": per, "flips": flips, "chain_vs_oracle": chain_vs_oracle, "chain_vs_step": chain_vs_step,
+           "step_vs_oracle": step_vs_oracle}
+    if chain_vs_step > min(0.25 * step_vs_oracle, 1e-3):
+        return {"kind": "defect", "substep": "step_kernel != physics_kernel chain", **res}
+    return {"kind": "sensitive", **res}

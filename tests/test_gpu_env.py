@@ -48,7 +48,7 @@ def test_reset_step_parity(task, imit, gpu):
     rng = np.random.default_rng(0)
     for t in range(5):
         a = rng.uniform(-1, 1, (n, env.action_size)).astype(np.float32)
-        env.step(st, torch.tensor(a, device=gpu))
+        st = env.step(st, torch.tensor(a, device=gpu))
         ob.step(a.astype(np.float64))
         good &= _compare(env, st, ob, L)
     assert good.mean() > 0.9
@@ -71,7 +71,7 @@ def test_standing_reset_step_parity(task, gpu):
     rng = np.random.default_rng(1)
     for t in range(5):
         a = rng.uniform(-1, 1, (n, env.action_size)).astype(np.float32)
-        env.step(st, torch.tensor(a, device=gpu))
+        st = env.step(st, torch.tensor(a, device=gpu))
         ob.step(a.astype(np.float64))
         good &= _compare(env, st, ob, L)
     assert good.mean() > 0.9
@@ -86,13 +86,13 @@ def test_autoreset_and_episode(gpu):
     st = env.reset(rng=3)
     first_obs = st.obs["state"].clone()
     for t in range(5):
-        env.step(st, torch.zeros(n, env.action_size, device=gpu))
+        st = env.step(st, torch.zeros(n, env.action_size, device=gpu))
     torch.cuda.synchronize()
     # episode_length reached: every env is done and restored to its first state
     assert torch.all(st.done == 1)
     assert torch.allclose(st.obs["state"], first_obs)
     assert torch.all(st.info["steps"] == 5)
-    env.step(st, torch.zeros(n, env.action_size, device=gpu))
+    st = env.step(st, torch.zeros(n, env.action_size, device=gpu))
     assert torch.all(st.info["steps"] == 1)
 
 
@@ -117,7 +117,7 @@ def test_domain_randomization_parity(task, gpu):
     rng = np.random.default_rng(1)
     for t in range(3):
         a = rng.uniform(-1, 1, (n, env.action_size)).astype(np.float32)
-        env.step(st, torch.tensor(a, device=gpu))
+        st = env.step(st, torch.tensor(a, device=gpu))
         ob.step(a.astype(np.float64))
         good &= _compare(env, st, ob, L)
     print(task, "free-running envs within tolerance after 3 steps:", good.mean())
@@ -128,7 +128,7 @@ def test_edge_sizes(gpu):
     for n in (1, 17):
         env = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
         st = env.reset(rng=1)
-        env.step(st, torch.zeros(n, env.action_size, device=gpu))
+        st = env.step(st, torch.zeros(n, env.action_size, device=gpu))
         torch.cuda.synchronize()
         assert torch.isfinite(st.obs["state"]).all()
 
@@ -136,7 +136,7 @@ def test_edge_sizes(gpu):
 def test_host_action_is_moved(gpu):
     env = Joystick("flat_terrain", num_envs=4, device=gpu, use_imitation=False)
     st = env.reset(rng=1)
-    out = env.step(st, torch.zeros(4, env.action_size))  # host tensor is moved to the device
+    out = env.step(st, torch.zeros(4, env.action_size), inplace=True)  # host tensor is moved to the device
     assert out is st
 
 
@@ -150,9 +150,9 @@ def test_env_offset_shards_are_bit_identical(gpu):
     parts = [Joystick("flat_terrain", num_envs=h, device=gpu, use_imitation=True, env_offset=k * h) for k in range(2)]
     sp = [p.reset(rng=9) for p in parts]
     for a in acts:
-        full.step(sf, a)
+        sf = full.step(sf, a)
         for k in range(2):
-            parts[k].step(sp[k], a[k * h:(k + 1) * h])
+            sp[k] = parts[k].step(sp[k], a[k * h:(k + 1) * h])
     for key in ("state", "privileged_state"):
         got = torch.cat([s.obs[key] for s in sp])
         assert torch.equal(got, sf.obs[key]), key
@@ -176,7 +176,7 @@ def test_full_size_runs_are_deterministic(cfg, gpu):
                                      episode_length=1000, randomization_fn=domain_randomize if c["dr"] else None)
         st = env.reset(rng=3)
         for a in acts:
-            env.step(st, a)
+            st = env.step(st, a)
         torch.cuda.synchronize()
         out.append([st.obs["state"].clone(), st.obs["privileged_state"].clone(), st.reward.clone(), st.done.clone()])
     for x, y in zip(*out):
@@ -197,7 +197,7 @@ def test_full_size_long_rollout_with_auto_reset(gpu):
     ep = torch.zeros(n, device=gpu)
     falls = truncs = 0
     for t in range(300):
-        env.step(st, torch.rand(n, 14, device=gpu, generator=g) * 2 - 1)
+        st = env.step(st, torch.rand(n, 14, device=gpu, generator=g) * 2 - 1)
         ep += 1
         done, trunc = st.done, st.info["truncation"]
         assert bool((trunc <= done).all())
@@ -209,3 +209,75 @@ def test_full_size_long_rollout_with_auto_reset(gpu):
         if t % 50 == 49:
             assert torch.isfinite(st.obs["state"]).all() and torch.isfinite(st.obs["privileged_state"]).all()
     assert truncs > 0 and falls > 0
+
+
+def test_c5_full_shape_equals_eight_shards(gpu):
+    """C5's full shape on one GPU: 32,768 envs of rough terrain + DR + backlash with the training
+    wrappers (EpisodeWrapper at 2 env-steps + AutoReset, so the restore path runs) against the same
+    batch as 8 shards of 4,096 (env_offset = k * 4096, what each of the 8 ranks runs): per-env DR,
+    reset, pushes and steps are keyed by the global env id (randomize.py:26-146), so obs,
+    privileged obs, reward and done are bit-identical after 3 env-steps."""
+    from open_duck_playground_amd.joystick import domain_randomize, wrap_for_brax_training
+    n, k = 32768, 8
+    h = n // k
+    g = torch.Generator(device=gpu)
+    g.manual_seed(11)
+    acts = [torch.rand(n, 14, device=gpu, generator=g) * 2 - 1 for _ in range(3)]
+
+    def make(num, off):
+        env = Joystick("rough_terrain_backlash", num_envs=num, device=gpu, use_imitation=False, env_offset=off)
+        return wrap_for_brax_training(env, episode_length=2, randomization_fn=domain_randomize, rng=4)
+
+    full = make(n, 0)
+    sf = full.reset(rng=9)
+    for a in acts:
+        sf = full.step(sf, a)
+    ref = {key: sf.obs[key].clone() for key in ("state", "privileged_state")}
+    ref["reward"], ref["done"] = sf.reward.clone(), sf.done.clone()
+    del full, sf
+    got = {key: [] for key in ref}
+    for s in range(k):
+        part = make(h, s * h)
+        sp = part.reset(rng=9)
+        for a in acts:
+            sp = part.step(sp, a[s * h:(s + 1) * h])
+        for key in ("state", "privileged_state"):
+            got[key].append(sp.obs[key].clone())
+        got["reward"].append(sp.reward.clone())
+        got["done"].append(sp.done.clone())
+        del part, sp
+    assert float(ref["done"].sum()) > 0  # the auto-reset restore ran
+    for key in ref:
+        assert torch.equal(torch.cat(got[key]), ref[key]), key
+
+
+def test_step_is_functional(gpu):
+    """Joystick.step returns a new State and leaves its input as it was (the reference's
+    state.replace, joystick.py:480-481; brax's unroll keeps both state and nstate), and the new
+    State equals the in-place step bit for bit."""
+    n = 64
+    env = wrap_for_brax_training(Joystick("rough_terrain", num_envs=n, device=gpu, use_imitation=False),
+                                 episode_length=2, randomization_fn=domain_randomize, rng=3)
+    s0 = env.reset(rng=5)
+    a = torch.rand(n, env.action_size, device=gpu) * 2 - 1
+    keep = {"obs": s0.obs["state"].clone(), "priv": s0.obs["privileged_state"].clone(),
+            "qpos": s0.data.qpos.clone(), "fstate": s0.fstate.clone(), "istate": s0.istate.clone()}
+    s1 = env.step(s0, a)
+    s2 = env.step(s1, a)  # the auto-reset restore (episode_length 2)
+    torch.cuda.synchronize()
+    assert s1 is not s0 and s1.fstate.data_ptr() != s0.fstate.data_ptr()
+    assert torch.equal(s0.obs["state"], keep["obs"]) and torch.equal(s0.obs["privileged_state"], keep["priv"])
+    assert torch.equal(s0.data.qpos, keep["qpos"])
+    assert torch.equal(s0.fstate, keep["fstate"]) and torch.equal(s0.istate, keep["istate"])
+    # in place from a copy of s0: bit-identical to the functional chain
+    t = env.step(s0, torch.zeros_like(a))  # any State in fresh buffers
+    t.fstate.copy_(keep["fstate"])
+    t.istate.copy_(keep["istate"])
+    for _ in range(2):
+        out = env.step(t, a, inplace=True)
+        assert out is t
+    for key in ("state", "privileged_state"):
+        assert torch.equal(t.obs[key], s2.obs[key]), key
+    assert torch.equal(t.fstate, s2.fstate) and torch.equal(t.istate, s2.istate)
+    assert torch.equal(t.reward, s2.reward) and torch.equal(t.done, s2.done)
+    assert torch.equal(s1.data.qpos, env.step(s0, a).data.qpos)  # s0 still steps to s1

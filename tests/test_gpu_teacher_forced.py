@@ -8,8 +8,11 @@ bookkeeping, and the EpisodeWrapper/AutoReset wrappers of common/runner.py:117 w
 Bar: qpos rel 1e-4, qvel 2e-3, qacc_warmstart 2e-2, every info field / obs / privileged obs / reward
 2e-3 (|gpu - oracle| / (1 + |oracle|)), done and every integer field exact, for >= 99.5 % of
 env-steps; and every env-step outside that bar is explained at substep resolution (the kernel's
-substep from its own input matches the oracle's substep from the same input to 1e-3, or is a
-branch the oracle also takes under a 1e-6/1e-5 input perturbation). Measured on MI355X: median
+substep from its own input matches the oracle's substep from the same input to 1e-4, or is a
+branch the oracle also takes under a 1e-6/1e-5 input perturbation; and that substep chain
+reproduces step_kernel's own result for the env-step). The reset before step 0 is compared
+strictly: every fstate row (incl. the auto-reset snapshot), obs, privileged obs and istate word of
+every env at the same bar (teacher_forcing.reset_stats). Measured on MI355X: median
 errors 1e-7 (qpos) .. 4e-6 (obs), p99 <= 3e-4, at most 2 outliers in 1536 env-steps per case, all
 explained (tools/tf_outliers.py).
 """
@@ -27,6 +30,12 @@ def test_teacher_forced_step_parity(case, gpu):
     rep = run_case(case, gpu, n=256, steps=6, keep_states=True)
     s = rep.summary()
     print(case, {k: v for k, v in s.items()})
+    # the reset itself, strictly: every fstate row, obs, privileged obs and istate word of every env
+    r = rep.reset
+    bad = (r["norm"] > 1) | r["int_mismatch"]
+    print(f"  reset: worst err/bar {r['norm'].max():.3f} ({r['worst_row'][r['norm'].argmax()]}), "
+          f"int mismatches {int(r['int_mismatch'].sum())}")
+    assert not bad.any(), [(int(e), r["worst_row"][e], float(r["norm"][e])) for e in bad.nonzero()[0][:8]]
     assert s["good_frac"] >= 0.995, s
     unexplained = []
     for t, st in enumerate(rep.steps):

@@ -45,7 +45,7 @@ class ToyEnv:
                                reward=torch.zeros(self.num_envs), done=torch.zeros(self.num_envs),
                                info={"truncation": torch.zeros(self.num_envs), "steps": steps})
 
-    def step(self, state, action):
+    def step(self, state, action, inplace=True):  # in place, like Joystick.step(..., inplace=True)
         t = state.obs["state"]
         err = (action - t).abs()
         state.reward.copy_(1.0 - err.mean(1))

@@ -67,11 +67,11 @@ def timing(task="flat_terrain", n=4096, steps=20, imit=False):
     st = env.reset(rng=0)
     a = torch.zeros(n, env.action_size, device="cuda:0")
     for _ in range(3):
-        env.step(st, a)
+        env.step(st, a, inplace=True)
     torch.cuda.synchronize()
     t = time.time()
     for _ in range(steps):
-        env.step(st, a)
+        env.step(st, a, inplace=True)
     torch.cuda.synchronize()
     dt = (time.time() - t) / steps
     print(f"[timing {task} imit={imit}] n={n}: {dt * 1e3:.2f} ms/env-step -> {n / dt:,.0f} env-steps/s;"
