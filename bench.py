@@ -245,10 +245,13 @@ def main():
         src = {"source": os.path.relpath(PMC_PROFILE, ROOT), "build_id_matches": current}
         if current:
             traffic = prof["hbm_bytes_per_launch"]
-        valu = prof["SQ_INSTS_VALU"] * 64 / (kern_ms * 1e-3) / 1e12     # lane-instructions / s
-        issue_rf = {"bound": "valu", "achieved": valu, "peak": VALU_PEAK_TLANE, "unit": "T lane-instr/s",
-                    "frac": valu / VALU_PEAK_TLANE, "valu_insts_per_launch": prof["SQ_INSTS_VALU"],
-                    "valu_busy_frac": prof["valu_busy_frac"], "waitcnt_frac": prof["waitcnt_frac"], **src}
+            valu = prof["SQ_INSTS_VALU"] * 64 / (kern_ms * 1e-3) / 1e12     # lane-instructions / s
+            issue_rf = {"bound": "valu", "achieved": valu, "peak": VALU_PEAK_TLANE, "unit": "T lane-instr/s",
+                        "frac": valu / VALU_PEAK_TLANE, "valu_insts_per_launch": prof["SQ_INSTS_VALU"],
+                        "valu_busy_frac": prof["valu_busy_frac"], "waitcnt_frac": prof["waitcnt_frac"], **src}
+        else:  # another build's counters: no rate is derived from them
+            issue_rf = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_TLANE, "unit": "T lane-instr/s",
+                        "frac": None, **src}
     if rank == 0:
         B = algorithmic_bytes(env)
         achieved = B * n / (kern_ms * 1e-3) / 1e9

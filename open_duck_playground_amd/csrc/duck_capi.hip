@@ -130,6 +130,9 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
   if (cfg->n_substeps < 1 || cfg->action_max_delay < 1 || cfg->action_max_delay > 3)
     return duck_fail(DUCK_EINVAL, "bad config (n_substeps >= 1, 1 <= action_max_delay <= 3)");
   if (kVariants[v]->lds_bytes() > 160 * 1024) return duck_fail(DUCK_EUNSUPPORTED, "per-workgroup LDS over 160 KiB");
+  // the elevation is uploaded here, not baked (the fingerprint covers nrow / ncol / size only)
+  if (kVariants[v]->floor_type == 1 && (!model->hfield_data || model->hfield_nrow < 2 || model->hfield_ncol < 2))
+    return duck_fail(DUCK_EINVAL, "height-field model without hfield_data [nrow >= 2][ncol >= 2]");
   HIPCHECK(hipSetDevice(device));
   duck_sim* s = new duck_sim();
   memset(s, 0, sizeof(*s));

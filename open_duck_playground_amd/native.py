@@ -107,14 +107,21 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no
         bad = [src for src, p in procs if p.wait() != 0]
         if bad:
             raise DuckError(f"hipcc failed on {bad}")
-        subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-shared", "-o", out + ".tmp"] + objs, cwd=CSRC)
-    if isa_check:
-        bad = isa_exec_faults(out + ".tmp")
-        if bad:
-            os.remove(out + ".tmp")
-            raise DuckError("register-allocation fault in the compiled kernels (split copies ahead of an exec "
-                            "restore, tools/isa_exec_check.py):\n" + "\n".join(bad))
-    os.replace(out + ".tmp", out)
+        # a per-process temporary: concurrent builders (ranks, model_library callers) never link over
+        # or scan each other's file; os.replace publishes the checked library atomically
+        tmp_out = f"{out}.{os.getpid()}.tmp"
+        subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-shared", "-o", tmp_out] + objs, cwd=CSRC)
+    try:
+        if isa_check:
+            nvar = sum(os.path.basename(f).startswith("variant_") for f in srcs)
+            bad = isa_exec_faults(tmp_out, min_step_kernels=nvar)
+            if bad:
+                raise DuckError("register-allocation fault in the compiled kernels (split copies ahead of an exec "
+                                "restore, tools/isa_exec_check.py):\n" + "\n".join(bad))
+        os.replace(tmp_out, out)
+    finally:
+        if os.path.exists(tmp_out):
+            os.remove(tmp_out)
     return out
 
 
@@ -130,33 +137,59 @@ def model_library(m, verbose: bool = False) -> str:
         hdr = os.path.join(CSRC, "generated", f"duck_model_{var}.h")
         if os.path.exists(hdr) and f"FINGERPRINT = 0x{fp:016x}ull" in open(hdr).read():
             return LIB_PATH
+    import fcntl
     name = f"m{fp:016x}"
     out = os.path.join(BUILD, f"libduck_{name}.so")
-    if os.path.exists(out) and os.path.getmtime(out) >= max(
-            os.path.getmtime(os.path.join(CSRC, f)) for f in os.listdir(CSRC) if f.endswith((".h", ".hip"))):
-        return out
     gen = os.path.join(BUILD, f"gen_{name}")
     os.makedirs(gen, exist_ok=True)
-    files = {f"duck_model_{name}.h": codegen.model_header(m, name),
-             f"variant_{name}.hip": codegen.variant_unit(name, f"duck_model_{name}.h"),
-             "duck_variants.inc": codegen.variant_registry([name])}
-    for fn, text in files.items():
-        path = os.path.join(gen, fn)
-        if not os.path.exists(path) or open(path).read() != text:
-            with open(path, "w") as f:
-                f.write(text)
-    return build(verbose=verbose, out=out, gen_dir=gen)
+    # one builder per model at a time (torchrun ranks, several envs on the same edited XML): the
+    # others wait on the lock and then find the library fresh
+    with open(os.path.join(BUILD, f"libduck_{name}.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        try:
+            # regenerate first: a codegen change that alters the header or unit rewrites it, and
+            # build()'s freshness check (sources, headers, include/, native.py) then rebuilds
+            files = {f"duck_model_{name}.h": codegen.model_header(m, name),
+                     f"variant_{name}.hip": codegen.variant_unit(name, f"duck_model_{name}.h"),
+                     "duck_variants.inc": codegen.variant_registry([name])}
+            for fn, text in files.items():
+                path = os.path.join(gen, fn)
+                if not os.path.exists(path) or open(path).read() != text:
+                    with open(path, "w") as f:
+                        f.write(text)
+            return build(verbose=verbose, out=out, gen_dir=gen)
+        finally:
+            fcntl.flock(lock, fcntl.LOCK_UN)
 
 
-def isa_exec_faults(so_path: str):
+def isa_kernels(texts) -> list:
+    """The kernel symbols (amdgpu_kernel entry labels) in disassembled code objects."""
+    import re
+    out = []
+    for t in texts:
+        out += re.findall(r"^[0-9a-f]+ <(_Z\d+(?:step|physics|reset|randomize)_kernel\w*)>:$", t, re.M)
+    return out
+
+
+def isa_exec_faults(so_path: str, min_step_kernels: int = 1):
     """Blocks of the gfx950 code in so_path whose exec-restoring join starts with AGPR/scratch moves
-    (tools/isa_exec_check.py): each is a lane-masked live-range split, i.e. a wrong-result kernel."""
+    (tools/isa_exec_check.py): each is a lane-masked live-range split, i.e. a wrong-result kernel.
+    Fails closed: raises DuckError when no code object could be disassembled or fewer than
+    min_step_kernels step_kernel / physics_kernel symbols were scanned (a missing fat binary, an
+    unbundling failure or a compressed bundle must not pass as "no faults")."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("isa_exec_check", os.path.join(ROOT, "tools", "isa_exec_check.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    texts = mod.code_objects(so_path)
+    kern = isa_kernels(texts)
+    nstep = sum("step_kernel" in k for k in kern)
+    nphys = sum("physics_kernel" in k for k in kern)
+    if not texts or nstep < min_step_kernels or nphys < min_step_kernels:
+        raise DuckError(f"ISA gate scanned nothing usable in {so_path}: {len(texts)} code object(s), "
+                        f"{nstep} step_kernel / {nphys} physics_kernel symbol(s), {min_step_kernels} expected")
     found = []
-    for text in mod.code_objects(so_path):
+    for text in texts:
         found += mod.scan(text, os.path.basename(so_path))
     return [f"{func[:80]}: {len(pre)} move(s) before '{ins}'" for _, func, _, pre, ins in found]
 

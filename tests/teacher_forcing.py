@@ -178,7 +178,43 @@ def reset_stats(L, st, ob, n: int) -> dict:
     oerr = np.maximum(_rel(obs, ob.obs).max(axis=1), _rel(priv, ob.priv).max(axis=1)) / 2e-3
     GI, OI = st.istate.cpu().numpy().reshape(L.nint, n), ob.is_.reshape(L.nint, n)
     return {"norm": np.maximum(r.max(axis=0), oerr), "worst_row": name[worst],
-            "int_mismatch": np.any(GI != OI, axis=0), "fs_norm": r.max(axis=0), "obs_norm": oerr}
+            "int_mismatch": np.any(GI != OI, axis=0), "fs_norm": r.max(axis=0), "obs_norm": oerr,
+            "gpu_fs": A.copy(), "ora_fs": B.copy()}
+
+
+def explain_reset(rep: Report, e: int, seed: int = 0) -> dict:
+    """Why env e's reset differs: the reset ends with mjx.forward (mjx_env.init, joystick.py:258),
+    whose constrained qacc (stored as qacc_warmstart; the accelerometer in obs) can take another
+    contact branch from fp32-sized differences of the sampled state. "sensitive" when the oracle's
+    forward from its reset state, perturbed by 1e-6 / 1e-5, lands on the GPU's qacc (a branch the
+    oracle also takes) and every integer word matches; otherwise "defect"."""
+    env, m = rep.env, rep.env.mj_model
+    L, o = env._layout, env._layout.off
+    G, B = rep.reset["gpu_fs"][:, e], rep.reset["ora_fs"][:, e]
+    if rep.reset["int_mismatch"][e]:
+        return {"kind": "defect", "why": "integer words"}
+    om = rep.models[e] if isinstance(rep.models, list) else rep.models
+    x = np.concatenate([B[o["qpos"]:o["qpos"] + m.nq], B[o["qvel"]:o["qvel"] + m.nv], np.zeros(m.nv),
+                        B[o["ctrl"]:o["ctrl"] + m.nu]])
+    target = np.concatenate([G[o["qpos"]:o["qpos"] + m.nq], G[o["qvel"]:o["qvel"] + m.nv],
+                             G[o["qacc_warmstart"]:o["qacc_warmstart"] + m.nv], G[o["ctrl"]:o["ctrl"] + m.nu]])
+
+    def fwd(y):
+        q, v, w, c = _split(m, y)
+        d = om.new_data(qpos=q, qvel=v, ctrl=c, warm=w)
+        om.forward(d)
+        return np.concatenate([q, v, d.arr("qacc", m.nv), c])
+    d0 = _state_rel(m, fwd(x), target)
+    rng = np.random.default_rng(seed)
+    k = m.nq + m.nv
+    for lev in (1e-6, 1e-5):
+        for _ in range(24):
+            y = x.copy()
+            y[:k] *= 1 + lev * rng.choice([-1.0, 1.0], size=k)
+            y[:k] += 1e-3 * lev * rng.choice([-1.0, 1.0], size=k)
+            if _state_rel(m, fwd(y), target) < 0.25 * d0:
+                return {"kind": "sensitive", "flip": lev, "forward_err": d0}
+    return {"kind": "defect", "why": "forward", "forward_err": d0}
 
 
 def _short_push():

@@ -210,5 +210,27 @@ def test_isa_check_flags_lane_masked_split_copies():
 @pytest.mark.skipif(not os.path.exists(native.LIB_PATH), reason="libduck.so not built")
 def test_built_library_has_no_lane_masked_split_copies():
     """Every kernel of the shipped libduck.so (all four scenes, max-ILP schedule) is free of
-    register moves placed ahead of an exec restore."""
-    assert native.isa_exec_faults(native.LIB_PATH) == []
+    register moves placed ahead of an exec restore -- and the gate really disassembled them: the
+    objdump path build() uses finds the step / physics / reset kernels of every scene."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("isa_exec_check", os.path.join(ROOT, "tools", "isa_exec_check.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    kern = native.isa_kernels(mod.code_objects(native.LIB_PATH))
+    for scene in ("flat", "backlash", "rough", "rough_backlash"):
+        for k in ("step_kernel", "physics_kernel", "reset_kernel"):
+            sym = f"DuckModel_{scene}"
+            assert any(k in x and f"{len(sym)}{sym}" in x for x in kern), (k, scene, kern)
+    assert native.isa_exec_faults(native.LIB_PATH, min_step_kernels=4) == []
+
+
+def test_isa_gate_fails_closed(tmp_path):
+    """A library without gfx950 code objects (here: a host-only shared object) is an error for the
+    gate, not a clean bill of health."""
+    import subprocess
+    src = tmp_path / "x.c"
+    src.write_text("int f(void) { return 1; }\n")
+    so = tmp_path / "libx.so"
+    subprocess.check_call(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)])
+    with pytest.raises(native.DuckError):
+        native.isa_exec_faults(str(so))

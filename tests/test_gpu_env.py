@@ -216,7 +216,7 @@ def test_c5_full_shape_equals_eight_shards(gpu):
     wrappers (EpisodeWrapper at 2 env-steps + AutoReset, so the restore path runs) against the same
     batch as 8 shards of 4,096 (env_offset = k * 4096, what each of the 8 ranks runs): per-env DR,
     reset, pushes and steps are keyed by the global env id (randomize.py:26-146), so obs,
-    privileged obs, reward and done are bit-identical after 3 env-steps."""
+    privileged obs, reward and done are bit-identical at each of 3 env-steps."""
     from open_duck_playground_amd.joystick import domain_randomize, wrap_for_brax_training
     n, k = 32768, 8
     h = n // k
@@ -228,27 +228,28 @@ def test_c5_full_shape_equals_eight_shards(gpu):
         env = Joystick("rough_terrain_backlash", num_envs=num, device=gpu, use_imitation=False, env_offset=off)
         return wrap_for_brax_training(env, episode_length=2, randomization_fn=domain_randomize, rng=4)
 
+    keys = ("state", "privileged_state", "reward", "done")
+    pick = lambda st: [st.obs["state"], st.obs["privileged_state"], st.reward, st.done]  # noqa: E731
     full = make(n, 0)
     sf = full.reset(rng=9)
+    ref = []
     for a in acts:
         sf = full.step(sf, a)
-    ref = {key: sf.obs[key].clone() for key in ("state", "privileged_state")}
-    ref["reward"], ref["done"] = sf.reward.clone(), sf.done.clone()
+        ref.append([x.clone() for x in pick(sf)])
     del full, sf
-    got = {key: [] for key in ref}
+    got = [[[] for _ in keys] for _ in acts]
     for s in range(k):
         part = make(h, s * h)
         sp = part.reset(rng=9)
-        for a in acts:
+        for t, a in enumerate(acts):
             sp = part.step(sp, a[s * h:(s + 1) * h])
-        for key in ("state", "privileged_state"):
-            got[key].append(sp.obs[key].clone())
-        got["reward"].append(sp.reward.clone())
-        got["done"].append(sp.done.clone())
+            for j, x in enumerate(pick(sp)):
+                got[t][j].append(x.clone())
         del part, sp
-    assert float(ref["done"].sum()) > 0  # the auto-reset restore ran
-    for key in ref:
-        assert torch.equal(torch.cat(got[key]), ref[key]), key
+    assert float(ref[1][3].sum()) > n // 2  # episode_length 2: the envs truncate at step 2, then restore
+    for t in range(len(acts)):
+        for j, key in enumerate(keys):
+            assert torch.equal(torch.cat(got[t][j]), ref[t][j]), (t, key)
 
 
 def test_step_is_functional(gpu):
