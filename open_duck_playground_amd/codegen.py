@@ -274,16 +274,22 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     # height-field prism SAT (TPhys::collide_hfield): per hull face its outward normal and offset,
     # per hull edge the Gauss-map arc of the negated hull (C = -n_A, D = -n_B), D x C, the edge
     # vector and its first vertex (mesh frame)
+    # (height-field scenes only; the two tables are contiguous: TLay::HT_LDS copies them to LDS
+    # when the whole blob does not fit)
     hull = m.hulls[0]
-    put("hface", [f2i(x) for f in range(len(hull.face_normal))
-                  for x in list(hull.face_normal[f]) + [hull.face_offset[f]]])  # stride 4
-    hef = hull_edge_faces(hull)
-    rec = []
-    for e, (a, b) in enumerate(hull.edge):
-        C_, D_ = -np.asarray(hull.face_normal[hef[e][0]]), -np.asarray(hull.face_normal[hef[e][1]])
-        v0, v1 = np.asarray(hull.vert[a]), np.asarray(hull.vert[b])
-        rec += [f2i(x) for x in np.concatenate([C_, D_, np.cross(D_, C_), v1 - v0, v0, [0.0]])]
-    put("hedge", rec)  # stride 16: C3, D3, DxC3, edge3, v0 3, pad
+    if int(m.geom_type[floor]) == 1:
+        put("hface", [f2i(x) for f in range(len(hull.face_normal))
+                      for x in list(hull.face_normal[f]) + [hull.face_offset[f]]])  # stride 4
+        hef = hull_edge_faces(hull)
+        rec = []
+        for e, (a, b) in enumerate(hull.edge):
+            C_, D_ = -np.asarray(hull.face_normal[hef[e][0]]), -np.asarray(hull.face_normal[hef[e][1]])
+            v0, v1 = np.asarray(hull.vert[a]), np.asarray(hull.vert[b])
+            rec += [f2i(x) for x in np.concatenate([C_, D_, np.cross(D_, C_), v1 - v0, v0, [0.0]])]
+        put("hedge", rec)  # stride 16: C3, D3, DxC3, edge3, v0 3, pad
+        boff["hend"] = len(blob)
+    else:
+        boff["hface"] = boff["hedge"] = boff["hend"] = -1
     d2f, d2l = [-1] * nv, [-1] * nv
     for r, i in enumerate(fric):
         d2f[i] = r

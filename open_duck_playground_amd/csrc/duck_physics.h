@@ -294,7 +294,7 @@ struct Phys {
   }
 
   // debug record: qacc, qacc_smooth, qvel (pre-integration), qfrc_smooth, actuator_force,
-  // sensordata, con_dist, con_pos, M
+  // sensordata, con_dist, con_pos, con_normal, M
   static DNI void write_aux(S L, float* aux, int stride) {
     int o = 0;
     for (int i = 0; i < NV; i++) aux[(o++) * stride] = L[Ly::QACC + i];
@@ -306,6 +306,8 @@ struct Phys {
     for (int s = 0; s < NCON; s++) aux[(o++) * stride] = L[Ly::CDIST + s];
     for (int s = 0; s < NCON; s++)
       for (int a = 0; a < 3; a++) aux[(o++) * stride] = L[Ly::CR + 3 * s + a] + L[Ly::COM + a];
+    for (int s = 0; s < NCON; s++)
+      for (int a = 0; a < 3; a++) aux[(o++) * stride] = L[Ly::CFR + 9 * s + a];  // contact normal
     for (int k = 0; k < Md::NM; k++) aux[(o++) * stride] = L[Ly::M + k];
 #ifdef DUCK_AUX_LDS
     // debug builds: the whole env slice (Lay fields + the team's chain/spatial scratch)
@@ -316,7 +318,7 @@ struct Phys {
 
 template <class Md>
 constexpr int aux_size() {
-  return 4 * Md::NV + Md::NU + Md::NSENSORDATA + 4 * Lay<Md>::NCON + Md::NM
+  return 4 * Md::NV + Md::NU + Md::NSENSORDATA + 7 * Lay<Md>::NCON + Md::NM
 #ifdef DUCK_AUX_LDS
          + Lay<Md>::TOTAL + 12 * Md::MAXCHAIN + 24
 #endif

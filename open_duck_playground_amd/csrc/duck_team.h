@@ -143,7 +143,11 @@ struct TLay {
   static constexpr size_t LDS_MAX = 160 * 1024 / 4;
   // LDS priority: model blob (read every substep), then the hot state (read once per env-step)
   static constexpr bool TAB_LDS = (size_t)(TAB + Md::NBLOB) <= LDS_MAX;
-  static constexpr int ES = TAB + (TAB_LDS ? Md::NBLOB : 0);
+  // the height field's hull SAT tables (hull faces + edges, contiguous in the blob) in LDS on their
+  // own when the whole blob is not (rough + backlash: the prism loop reads them per prism)
+  static constexpr int NHT = Md::B_HEND > Md::B_HFACE ? Md::B_HEND - Md::B_HFACE : 0;
+  static constexpr bool HT_LDS = !TAB_LDS && NHT > 0 && (size_t)(TAB + NHT) <= LDS_MAX;
+  static constexpr int ES = TAB + (TAB_LDS ? Md::NBLOB : (HT_LDS ? NHT : 0));
   static constexpr bool ES_LDS = (size_t)(ES + ES_FLOATS) <= LDS_MAX;
   static constexpr int LDS_FLOATS = ES + (ES_LDS ? ES_FLOATS : 0);
   static_assert((size_t)LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
@@ -170,6 +174,21 @@ DK void load_model_tables(float* lds) {
       if (i < Md::NBLOB) dst[i] = w[kk];
     }
     __syncthreads();
+  } else if constexpr (TLay<Md>::HT_LDS) {
+    int* dst = (int*)(lds + TLay<Md>::TAB);
+    constexpr int N = TLay<Md>::NHT, NK = (N + TPB_TEAM - 1) / TPB_TEAM;
+    int w[NK];
+#pragma unroll
+    for (int kk = 0; kk < NK; kk++) {
+      const int i = (int)threadIdx.x + TPB_TEAM * kk;
+      w[kk] = Md::t_blob()[Md::B_HFACE + (i < N ? i : N - 1)];
+    }
+#pragma unroll
+    for (int kk = 0; kk < NK; kk++) {
+      const int i = (int)threadIdx.x + TPB_TEAM * kk;
+      if (i < N) dst[i] = w[kk];
+    }
+    __syncthreads();
   }
 }
 
@@ -192,6 +211,15 @@ struct TPhys {
     }
   }
   static DK float tf(int off) { return __int_as_float(ti(off)); }
+  // the hull SAT tables (blob words B_HFACE .. B_HEND): LDS whenever they fit
+  static DK float th(int off) {
+    if constexpr (!TL::TAB_LDS && TL::HT_LDS) {
+      extern __shared__ float lds_dyn[];
+      return ((lds_float*)(lds_dyn + TL::TAB))[off - Md::B_HFACE];
+    } else {
+      return tf(off);
+    }
+  }
   static constexpr int LIMW = 13, PAIRW = 13;
   // row -> dof and dof -> row maps of the friction and limit rows: affine when the rows cover
   // consecutive dofs (codegen B_FRIC0 / B_LIM0 >= 0), else index words of the model blob
@@ -1290,14 +1318,25 @@ struct TPhys {
   // hull is above the prism's base, 0.1 m under the field: tests/test_oracle_physics.py).
   // Coordinates: "local" = the field's axes with the origin at the hull frame, "mesh" = the hull frame.
   static DK float hmin8f(float v) { return -hmax8(-v); }
+  // this lane's rank within its 8-lane half of the wave's ballot word
+  static DK unsigned half_bits(unsigned long long b, int lane) {
+    const int base = ((int)threadIdx.x & 63) & ~7;
+    (void)lane;
+    return (unsigned)(b >> base) & 0xFFu;
+  }
   static DK void collide_hfield(LP L, int lane, const float* hf) {
+    STAGE_T0();
     constexpr int NH = Md::NHV, NF = Md::NHF, NE = Md::NHE;
     constexpr int NR = Md::HF_NROW, NCc = Md::HF_NCOL;
     constexpr float SX = Md::HF_SIZE[0], SY = Md::HF_SIZE[1], SZ = Md::HF_SIZE[2], SB = Md::HF_SIZE[3];
     constexpr float DXC = 2.0f * SX / (NCc - 1), DYC = 2.0f * SY / (NR - 1);
     constexpr int MAXP = 2 * Md::HF_MAXCX * Md::HF_MAXCY, PPL = (MAXP + 7) / 8;
+    static_assert(MAXP <= 32, "prism masks are 32-bit");
+    constexpr int NGV = (Md::HF_MAXCX + 1) * (Md::HF_MAXCY + 1), GPL = (NGV + 7) / 8;
     constexpr int VPL = (NH + 7) / 8, FPL = (NF + 7) / 8, EPL = (NE + 7) / 8;
-    constexpr int PRIO_T = 5 + NF, PRIO_V = 5 + NF + 3 * NE, NOPRIO = 1 << 28;
+    // axis priorities (equal overlaps: the lowest wins, the oracle's order): prism top 0, sides 1-3,
+    // bottom 4, hull faces, top-edge pairs by (hull edge, k), vertical-edge pairs by (edge, k)
+    constexpr int PRIO_T = 5 + NF, PRIO_V = PRIO_T + 3 * NE, NOPRIO = 1 << 28;
     const int h = lane >> 3, sub = lane & 7;
     const int p = Md::PLANE_PAIR[0] * (1 - h) + Md::PLANE_PAIR[1] * h;
     const int gs = cgeom_slot<Md>(Md::pair_geom2[p]);
@@ -1319,7 +1358,6 @@ struct TPhys {
     float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
     const float GN = 1.0f / sqrtf(DXC * DXC + DYC * DYC);
     const float GX = DYC * GN, GY = DXC * GN;  // the cells' diagonal side normal (dy, dx) / |.|
-    float gmin = 1e30f, gmax = -1e30f;
 #pragma unroll
     for (int i = 0; i < VPL; i++) {
       const int k = sub + 8 * i;
@@ -1329,20 +1367,14 @@ struct TPhys {
       mulmv3(xl[i], R, v);
       if (vok[i]) {
         for (int a = 0; a < 3; a++) { lo[a] = fminf(lo[a], xl[i][a]); hi[a] = fmaxf(hi[a], xl[i][a]); }
-        const float g = GX * xl[i][0] + GY * xl[i][1];
-        gmin = fminf(gmin, g);
-        gmax = fmaxf(gmax, g);
       }
     }
     for (int a = 0; a < 3; a++) { lo[a] = hmin8f(lo[a]); hi[a] = hmax8(hi[a]); }
-    gmin = hmin8f(gmin);
-    gmax = hmax8(gmax);
-    // the field's box and the sub-grid (vertex columns cmin..cmax, rows rmin..rmax)
+    // the field's box and the sub-grid (vertex columns cmin..cmax, rows rmin..rmax); grid
+    // coordinates relative to the field's centre (vertex c at (c - (ncol - 1) / 2) dx): the robot
+    // walks near the centre, where these keep fp32's resolution (x + size would round to ~1e-6 m)
     const bool inside = !(hi[0] + t[0] < -SX || lo[0] + t[0] > SX || hi[1] + t[1] < -SY || lo[1] + t[1] > SY ||
                           lo[2] + t[2] > SZ || hi[2] + t[2] < -SB);
-    // grid coordinates relative to the field's centre (vertex c at (c - (ncol - 1) / 2) dx): the
-    // robot walks near the centre, where these keep fp32's resolution (x + size would round to
-    // ~1e-6 m at size = 10 m)
     constexpr float FXC = (NCc - 1) / (2.0f * SX), FYC = (NR - 1) / (2.0f * SY);
     constexpr float CC0 = 0.5f * (NCc - 1), RC0 = 0.5f * (NR - 1);
     const int cmin = max((int)floorf((lo[0] + t[0]) * FXC + CC0), 0);
@@ -1354,18 +1386,121 @@ struct TPhys {
     const int np = 2 * ncx * ncy;
     const float X0 = ((float)cmin - CC0) * DXC - t[0], Y0 = ((float)rmin - RC0) * DYC - t[1];
     const float base = -SB - t[2];  // the prisms' bottom (local z)
+    // the sub-grid's elevations (local z), one global load per lane: vertex v = iy (ncx + 1) + ix
+    // on lane v & 7, register v >> 3; prisms read them by shuffles
+    float zg[GPL];
+#pragma unroll
+    for (int i = 0; i < GPL; i++) {
+      const int v = sub + 8 * i, iy = v / (ncx + 1), ix = v - iy * (ncx + 1);
+      const bool ok = np > 0 && iy <= ncy;
+      zg[i] = ok ? SZ * hf[(rmin + iy) * NCc + cmin + ix] - t[2] : 0.0f;
+    }
+    auto zat = [&](int ix, int iy) -> float {  // any lane pattern: every lane supplies both registers
+      const int v = iy * (ncx + 1) + ix, src = 8 * h + (v & 7);
+      float z = __shfl(zg[0], src, TEAM);
+#pragma unroll
+      for (int i = 1; i < GPL; i++) {
+        const float zi = __shfl(zg[i], src, TEAM);
+        z = (v >> 3) == i ? zi : z;
+      }
+      return z;
+    };
+    // prism q (strip order): cell (rr, cc) of the sub-grid, triangle tri; top vertices (local)
+    // A = (c, r), (c, r + 1), (c + 1, r); B = (c, r + 1), (c + 1, r), (c + 1, r + 1)
+    auto prism_top = [&](int q, float (*T)[3], int& tri) {
+      const int rr = q / (2 * ncx), rem = q - rr * 2 * ncx, cc = rem >> 1;
+      tri = rem & 1;
+      const int dcs[2][3] = {{0, 0, 1}, {0, 1, 1}}, drs[2][3] = {{0, 1, 0}, {1, 0, 1}};
+      for (int k = 0; k < 3; k++) {
+        const int ci = cc + (tri ? dcs[1][k] : dcs[0][k]), ri = rr + (tri ? drs[1][k] : drs[0][k]);
+        T[k][0] = X0 + (float)ci * DXC;
+        T[k][1] = Y0 + (float)ri * DYC;
+        T[k][2] = zat(ci, ri);
+      }
+    };
+    auto top_normal = [&](const float (*T)[3], float* nt) {
+      const float e0[3] = {T[1][0] - T[0][0], T[1][1] - T[0][1], T[1][2] - T[0][2]};
+      const float e1[3] = {T[2][0] - T[0][0], T[2][1] - T[0][1], T[2][2] - T[0][2]};
+      cross3(nt, e0, e1);
+      const float sg = (nt[2] < 0.0f ? -1.0f : 1.0f) / sqrtf(dot3(nt, nt));
+      for (int a = 0; a < 3; a++) nt[a] *= sg;
+    };
     // the hull's lowest point along each side normal (the six directions of the two triangle
     // kinds: A (-x, +g, -y), B (-g, +x, +y))
-    const float smin[2][3] = {{-hi[0], gmin, -hi[1]}, {-gmax, lo[0], lo[1]}};
-    // vertical-edge pairs: this lane's hull edges whose negated Gauss arc crosses the field's
-    // equator (silhouette edges seen along z); the crossing direction w (mesh) and the hull's
-    // support along it
+    // the hull's lowest point along each side normal (the six directions of the two triangle kinds:
+    // A (-x, +g, -y), B (-g, +x, +y))
+    const float sx_[2][3] = {{-1.0f, GX, 0.0f}, {-GX, 1.0f, 0.0f}}, sy_[2][3] = {{0.0f, GY, -1.0f}, {-GY, 0.0f, 1.0f}};
+    float smin[2][3];
+#pragma unroll
+    for (int ty = 0; ty < 2; ty++)
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        float mv = 1e30f;
+#pragma unroll
+        for (int i = 0; i < VPL; i++)
+          if (vok[i]) mv = fminf(mv, sx_[ty][k] * xl[i][0] + sy_[ty][k] * xl[i][1]);
+        smin[ty][k] = hmin8f(mv);
+      }
+    const float obot = hi[2] - base;
+    // 1. lane-parallel screen: prism q = sub + 8 j passes the height test and the axes of its own
+    // faces and the bottom (the hull's support along its top normal from the compile-time
+    // vertices); only survivors get the full separating-axis test
+    unsigned surv = 0;
+#pragma unroll
+    for (int j = 0; j < PPL; j++) {
+      const int q = sub + 8 * j;
+      float T[3][3], nt[3];
+      int tri;
+      prism_top(q < np ? q : 0, T, tri);
+      top_normal(T, nt);
+      float ntm[3];
+      mulmtv3(ntm, R, nt);
+      float hm = 1e30f;
+#pragma unroll
+      for (int k = 0; k < NH; k++) hm = fminf(hm, dot3(ntm, Md::hull_vert[k]));
+      float o = dot3(nt, T[0]) - hm;
+      for (int k = 0; k < 3; k++) {  // (tri is 0 or 1: two-way selects, not an indexed register array)
+        const float sxk = tri ? sx_[1][k] : sx_[0][k], syk = tri ? sy_[1][k] : sy_[0][k];
+        o = fminf(o, sxk * T[k][0] + syk * T[k][1] - (tri ? smin[1][k] : smin[0][k]));
+      }
+      // ... and the hull's faces (compile-time normals): the prism's lowest point along n_f, a
+      // bottom vertex where n_f leans up the field's z
+#ifndef DUCK_HF_NO_FACE_SCREEN
+      {
+        float Tm[3][3], hk[3];
+        for (int k = 0; k < 3; k++) { mulmtv3(Tm[k], R, T[k]); hk[k] = T[k][2] - base; }
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+          const float* n = Md::hull_face_normal[f];
+          const float nz = fmaxf(dot3(n, zc), 0.0f);
+          float pm = dot3(n, Tm[0]) - hk[0] * nz;
+          pm = fminf(pm, dot3(n, Tm[1]) - hk[1] * nz);
+          pm = fminf(pm, dot3(n, Tm[2]) - hk[2] * nz);
+          o = fminf(o, Md::hull_face_offset[f] - pm);
+        }
+      }
+#endif
+      const bool high = !(T[0][2] < lo[2] && T[1][2] < lo[2] && T[2][2] < lo[2]);
+      const bool ok = q < np && high && fminf(o, obot) > 0.0f;
+      surv |= half_bits(__ballot(ok), lane) << (8 * j);
+    }
+    // per-lane constants of the survivor loop: this lane's hull faces f = sub + 8 j (mesh normal,
+    // offset, the normal's lean up the field's z) and silhouette edges e = sub + 8 j (the crossing
+    // direction w of the negated Gauss arc with the field's equator, the hull's support along it)
+    float fnv[FPL][3], fof[FPL], fnz[FPL];
+#pragma unroll
+    for (int j = 0; j < FPL; j++) {
+      const int f = sub + 8 * j, ff = f < NF ? f : 0, o = Md::B_HFACE + 4 * ff;
+      for (int a = 0; a < 3; a++) fnv[j][a] = th(o + a);
+      fof[j] = f < NF ? th(o + 3) : 1e30f;  // a padding face never wins and never bounds
+      fnz[j] = fmaxf(dot3(fnv[j], zc), 0.0f);
+    }
     float wv[EPL][3], wh[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; j++) {
       const int e = sub + 8 * j, ee = e < NE ? e : 0, o = Md::B_HEDGE + 16 * ee;
-      const float C[3] = {tf(o), tf(o + 1), tf(o + 2)}, D[3] = {tf(o + 3), tf(o + 4), tf(o + 5)};
-      const float v0[3] = {tf(o + 12), tf(o + 13), tf(o + 14)};
+      const float C[3] = {th(o), th(o + 1), th(o + 2)}, D[3] = {th(o + 3), th(o + 4), th(o + 5)};
+      const float v0[3] = {th(o + 12), th(o + 13), th(o + 14)};
       const float sa = dot3(C, zc), sb = dot3(D, zc);
       const bool sil = e < NE && sa * sb < 0.0f;
       float w[3] = {fabsf(sb) * C[0] + fabsf(sa) * D[0], fabsf(sb) * C[1] + fabsf(sa) * D[1],
@@ -1381,35 +1516,35 @@ struct TPhys {
       cd[s] = -1.0f;
       for (int a = 0; a < 3; a++) { cn[s][a] = 0.0f; cx[s][a] = 0.0f; }
     }
-    for (int pi = 0; pi < np; pi++) {
-      const int rr = pi / (2 * ncx), rem = pi - rr * 2 * ncx, cc = rem >> 1, tri = rem & 1;
-      // top vertices: A = (c, r), (c, r + 1), (c + 1, r); B = (c, r + 1), (c + 1, r), (c + 1, r + 1)
-      float T[3][3];
+    STAGE_MARK(37);
+    // 2. the survivors, one at a time over the half-team (the mask is uniform over it)
+    while (surv) {
+#ifdef DUCK_ASM_MARKS
+      asm volatile("; HF_LOOP_TOP" ::: "memory");
+#endif
+      const int pi = __builtin_ctz(surv);
+      surv &= surv - 1;
+#ifdef DUCK_STAGE_PROF
+      if (threadIdx.x == 0) STAGE_ADD(40, 1ull);  // survivors of one foot (team 0, first half)
       {
-        const int dcs[2][3] = {{0, 0, 1}, {0, 1, 1}}, drs[2][3] = {{0, 1, 0}, {1, 0, 1}};
-        for (int k = 0; k < 3; k++) {
-          const int ci = cc + dcs[tri][k], ri = rr + drs[tri][k];
-          T[k][0] = X0 + (float)ci * DXC;
-          T[k][1] = Y0 + (float)ri * DYC;
-          T[k][2] = SZ * hf[(rmin + ri) * NCc + cmin + ci] - t[2];
-        }
+        const unsigned long long act = __ballot(1);  // iterations the wave runs (any half active)
+        if (threadIdx.x < 64 && (int)threadIdx.x == __ffsll((long long)act) - 1) STAGE_ADD(46, 1ull);
       }
-      // the prism height test
-      if (T[0][2] < lo[2] && T[1][2] < lo[2] && T[2][2] < lo[2]) continue;
-      // prism faces: top normal (z > 0) and the side normals of this triangle kind
-      float nt[3];
-      {
-        const float e0[3] = {T[1][0] - T[0][0], T[1][1] - T[0][1], T[1][2] - T[0][2]};
-        const float e1[3] = {T[2][0] - T[0][0], T[2][1] - T[0][1], T[2][2] - T[0][2]};
-        cross3(nt, e0, e1);
-        const float sg = (nt[2] < 0.0f ? -1.0f : 1.0f) / sqrtf(dot3(nt, nt));
-        for (int a = 0; a < 3; a++) nt[a] *= sg;
-      }
-      const float sx_[2][3] = {{-1.0f, GX, 0.0f}, {-GX, 1.0f, 0.0f}}, sy_[2][3] = {{0.0f, GY, -1.0f}, {-GY, 0.0f, 1.0f}};
+#endif
+      float T[3][3], nt[3];
+      int tri;
+      prism_top(pi, T, tri);
+      top_normal(T, nt);
       float sl[3][3];
-      for (int k = 0; k < 3; k++) { sl[k][0] = sx_[tri][k]; sl[k][1] = sy_[tri][k]; sl[k][2] = 0.0f; }
-      // the axes of the prism's faces (uniform over the half-team): overlap = the prism's support
-      // minus the hull's lowest point along the axis
+      float smk[3];  // this triangle kind's side normals and the hull's minima along them
+      for (int k = 0; k < 3; k++) {
+        sl[k][0] = tri ? sx_[1][k] : sx_[0][k];
+        sl[k][1] = tri ? sy_[1][k] : sy_[0][k];
+        sl[k][2] = 0.0f;
+        smk[k] = tri ? smin[1][k] : smin[0][k];
+      }
+      // the axes of the prism's faces (uniform): overlap = the prism's support minus the hull's
+      // lowest point along the axis
       const float ptop = dot3(nt, T[0]);
       float hm = 1e30f;
 #pragma unroll
@@ -1419,10 +1554,6 @@ struct TPhys {
       float mo = ptop - hm, mu[3];  // this lane's running minimum (overlap, priority, axis (mesh))
       int mp = 0;
       mulmtv3(mu, R, nt);
-      float osd[3];
-      for (int k = 0; k < 3; k++) osd[k] = sl[k][0] * T[k][0] + sl[k][1] * T[k][1] - smin[tri][k];
-      const float obot = hi[2] - base;
-      if (!(fminf(fminf(mo, obot), fminf(osd[0], fminf(osd[1], osd[2]))) > 0.0f)) continue;
       float Tm[3][3], sm[3][3], ntm[3], hk[3];
       for (int k = 0; k < 3; k++) {
         mulmtv3(Tm[k], R, T[k]);
@@ -1430,49 +1561,22 @@ struct TPhys {
         hk[k] = T[k][2] - base;
       }
       for (int a = 0; a < 3; a++) ntm[a] = mu[a];
-      for (int k = 0; k < 3; k++)
-        if (osd[k] < mo) { mo = osd[k]; mp = 1 + k; for (int a = 0; a < 3; a++) mu[a] = sm[k][a]; }
+      for (int k = 0; k < 3; k++) {
+        const float osd = sl[k][0] * T[k][0] + sl[k][1] * T[k][1] - smk[k];
+        if (osd < mo) { mo = osd; mp = 1 + k; for (int a = 0; a < 3; a++) mu[a] = sm[k][a]; }
+      }
       if (obot < mo) { mo = obot; mp = 4; for (int a = 0; a < 3; a++) mu[a] = -zc[a]; }
-      // hull faces f = sub + 8j: the axis -n_f, overlap = offset_f - the prism's lowest point
-      // along n_f (a bottom vertex where n_f leans up)
+      STAGE_MARK(41);
+      // hull faces: the axis -n_f, overlap = offset_f - the prism's lowest point along n_f (a
+      // bottom vertex where n_f leans up)
 #pragma unroll
       for (int j = 0; j < FPL; j++) {
-        const int f = sub + 8 * j, ff = f < NF ? f : 0, o = Md::B_HFACE + 4 * ff;
-        const float n[3] = {tf(o), tf(o + 1), tf(o + 2)}, off = tf(o + 3);
-        const float nz = fmaxf(dot3(n, zc), 0.0f);
         float pm = 1e30f;
-        for (int k = 0; k < 3; k++) pm = fminf(pm, dot3(n, Tm[k]) - hk[k] * nz);
-        const float ov = off - pm;
-        if (f < NF && ov < mo) { mo = ov; mp = 5 + f; for (int a = 0; a < 3; a++) mu[a] = -n[a]; }
+        for (int k = 0; k < 3; k++) pm = fminf(pm, dot3(fnv[j], Tm[k]) - hk[k] * fnz[j]);
+        const float ov = fof[j] - pm;
+        if (ov < mo) { mo = ov; mp = 5 + sub + 8 * j; for (int a = 0; a < 3; a++) mu[a] = -fnv[j][a]; }
       }
-      // top-edge pairs (hull edge e = sub + 8j, prism top edge k: faces nt, s_k)
-      float BxA[3][3], Em[3][3];
-      for (int k = 0; k < 3; k++) {
-        cross3(BxA[k], sm[k], ntm);
-        for (int a = 0; a < 3; a++) Em[k][a] = Tm[(k + 1) % 3][a] - Tm[k][a];
-      }
-#pragma unroll
-      for (int j = 0; j < EPL; j++) {
-        const int e = sub + 8 * j, ee = e < NE ? e : 0, o = Md::B_HEDGE + 16 * ee;
-        const float C[3] = {tf(o), tf(o + 1), tf(o + 2)}, D[3] = {tf(o + 3), tf(o + 4), tf(o + 5)};
-        const float DxC[3] = {tf(o + 6), tf(o + 7), tf(o + 8)}, ev[3] = {tf(o + 9), tf(o + 10), tf(o + 11)};
-        const float v0[3] = {tf(o + 12), tf(o + 13), tf(o + 14)};
-        const float ADC = dot3(ntm, DxC);
-        for (int k = 0; k < 3; k++) {
-          const float CBA = dot3(C, BxA[k]), DBA = dot3(D, BxA[k]), BDC = dot3(sm[k], DxC);
-          if (e < NE && CBA * DBA < 0.0f && ADC * BDC < 0.0f && CBA * BDC > 0.0f) {
-            float u[3];
-            cross3(u, ev, Em[k]);
-            const float un = sqrtf(dot3(u, u));
-            if (un >= 1e-6f * sqrtf(dot3(ev, ev)) * sqrtf(dot3(Em[k], Em[k]))) {
-              const float sg = (dot3(u, ntm) + dot3(u, sm[k]) < 0.0f ? -1.0f : 1.0f) / un;
-              for (int a = 0; a < 3; a++) u[a] *= sg;
-              const float ov = dot3(u, Tm[k]) - dot3(u, v0);
-              if (ov < mo) { mo = ov; mp = PRIO_T + 3 * e + k; for (int a = 0; a < 3; a++) mu[a] = u[a]; }
-            }
-          }
-        }
-      }
+      STAGE_MARK(42);
       // vertical-edge pairs: the prism's support along w is the vertical edge at vertex k
 #pragma unroll
       for (int j = 0; j < EPL; j++) {
@@ -1480,14 +1584,84 @@ struct TPhys {
         const float q0 = dot3(wv[j], Tm[0]), q1 = dot3(wv[j], Tm[1]), q2 = dot3(wv[j], Tm[2]);
         const int kk = q0 >= q1 ? (q0 >= q2 ? 0 : 2) : (q1 >= q2 ? 1 : 2);
         const float ov = fmaxf(q0, fmaxf(q1, q2)) - wh[j];
-        if (ov < mo) { mo = ov; mp = PRIO_V + 3 * e + kk; for (int a = 0; a < 3; a++) mu[a] = wv[j][a]; }
+        const int pr = PRIO_V + 3 * e + kk;
+        if (ov < mo || (ov == mo && pr < mp)) { mo = ov; mp = pr; for (int a = 0; a < 3; a++) mu[a] = wv[j][a]; }
       }
+      // top-edge pairs (hull edge e = sub + 8j, prism top edge k: faces nt, s_k): Gregorius'
+      // Minkowski-face test, the same enumeration as the oracle's. (A lower bound per arc that skips
+      // arcs which cannot beat the running minimum cost more than it saved: -1.5 % C4 / C5.)
+      float BxA[3][3], Em[3][3];
+      for (int k = 0; k < 3; k++) {
+        cross3(BxA[k], sm[k], ntm);
+        for (int a = 0; a < 3; a++) Em[k][a] = Tm[(k + 1) % 3][a] - Tm[k][a];
+      }
+      // pass 1: the Minkowski-face tests of this lane's (edge, arc) pairs into a bit mask
+#ifdef DUCK_ASM_MARKS
+      asm volatile("; HF_PASS1" ::: "memory");
+#endif
+      unsigned pass = 0;
+      {
+#pragma unroll
+        for (int j = 0; j < EPL; j++) {
+          const int e = sub + 8 * j, ee = e < NE ? e : 0, o = Md::B_HEDGE + 16 * ee;
+          const float C[3] = {th(o), th(o + 1), th(o + 2)}, D[3] = {th(o + 3), th(o + 4), th(o + 5)};
+          const float DxC[3] = {th(o + 6), th(o + 7), th(o + 8)};
+          const float ADC = dot3(ntm, DxC);
+          unsigned bits = 0;
+#pragma unroll
+          for (int k = 0; k < 3; k++) {
+            // the arcs cross when CBA DBA < 0, ADC BDC < 0 and CBA BDC > 0: all three products
+            // negative, i.e. the sign bit of their maximum (branch-free, no condition masks)
+            const float CBA = dot3(C, BxA[k]), DBA = dot3(D, BxA[k]), BDC = dot3(sm[k], DxC);
+            const float mx = fmaxf(fmaxf(CBA * DBA, ADC * BDC), -(CBA * BDC));
+            bits |= (__float_as_uint(mx) >> 31) << k;
+          }
+          if (j == EPL - 1 && NE < 8 * EPL) bits = e < NE ? bits : 0u;
+          pass |= bits << (3 * j);
+        }
+      }
+      // pass 2: the overlap of each passing pair (a few per lane: the wave loops over the most any
+      // lane has, not over all 3 x EPL)
+#ifdef DUCK_ASM_MARKS
+      asm volatile("; HF_PASS2" ::: "memory");
+#endif
+      while (pass) {
+        const int jk = __builtin_ctz(pass);
+        pass &= pass - 1;
+        const int j = jk / 3, k = jk - 3 * j, e = sub + 8 * j, o = Md::B_HEDGE + 16 * e;
+        const float ev[3] = {th(o + 9), th(o + 10), th(o + 11)}, v0[3] = {th(o + 12), th(o + 13), th(o + 14)};
+        float em[3], tm[3], sk[3];
+        for (int a = 0; a < 3; a++) {
+          em[a] = k == 0 ? Em[0][a] : (k == 1 ? Em[1][a] : Em[2][a]);
+          tm[a] = k == 0 ? Tm[0][a] : (k == 1 ? Tm[1][a] : Tm[2][a]);
+          sk[a] = k == 0 ? sm[0][a] : (k == 1 ? sm[1][a] : sm[2][a]);
+        }
+        float u[3];
+        cross3(u, ev, em);
+        const float u2 = dot3(u, u);
+        if (u2 >= 1e-12f * dot3(ev, ev) * dot3(em, em)) {
+          const float sg = (dot3(u, ntm) + dot3(u, sk) < 0.0f ? -1.0f : 1.0f) * __builtin_amdgcn_rsqf(u2);
+          const float ov = sg * (dot3(u, tm) - dot3(u, v0));
+          const int pr = PRIO_T + 3 * e + k;
+          if (ov < mo || (ov == mo && pr < mp)) {
+            mo = ov;
+            mp = pr;
+            for (int a = 0; a < 3; a++) mu[a] = sg * u[a];
+          }
+        }
+      }
+      STAGE_MARK(43);
+      STAGE_MARK(44);
       // the minimum over the half-team; equal overlaps: the lowest priority
+#ifdef DUCK_ASM_MARKS
+      asm volatile("; HF_AXES_DONE" ::: "memory");
+#endif
       const float mn = hmin8f(mo);
       const int wp = hmin8i(mo == mn ? mp : NOPRIO);
       const int wl = hmin8i(mo == mn && mp == wp ? sub : 8);
       float um[3];
       for (int a = 0; a < 3; a++) um[a] = __shfl(mu[a], 8 * h + wl, TEAM);
+      STAGE_MARK(45);
       if (!(mn > 0.0f)) continue;
       // the contact point: hull vertices inside the prism and prism top vertices inside the hull,
       // weighted by their penetration
@@ -1500,19 +1674,18 @@ struct TPhys {
         W += w;
         for (int a = 0; a < 3; a++) Cx[a] += w * xl[i][a];
       }
+      float pk[3];
+      for (int k = 0; k < 3; k++) {
+        pk[k] = 1e30f;
+#pragma unroll
+        for (int j = 0; j < FPL; j++) pk[k] = fminf(pk[k], fof[j] - dot3(fnv[j], Tm[k]));
+      }
       W = hsum8(W);
       for (int a = 0; a < 3; a++) Cx[a] = hsum8(Cx[a]);
       for (int k = 0; k < 3; k++) {
-        float pk = 1e30f;
-#pragma unroll
-        for (int j = 0; j < FPL; j++) {
-          const int f = sub + 8 * j, ff = f < NF ? f : 0, o = Md::B_HFACE + 4 * ff;
-          const float n[3] = {tf(o), tf(o + 1), tf(o + 2)};
-          if (f < NF) pk = fminf(pk, tf(o + 3) - dot3(n, Tm[k]));
-        }
-        pk = fmaxf(hmin8f(pk), 0.0f);
-        W += pk;
-        for (int a = 0; a < 3; a++) Cx[a] += pk * T[k][a];
+        const float w = fmaxf(hmin8f(pk[k]), 0.0f);
+        W += w;
+        for (int a = 0; a < 3; a++) Cx[a] += w * T[k][a];
       }
       float ul[3], pos[3];
       mulmv3(ul, R, um);
@@ -1556,6 +1729,10 @@ struct TPhys {
         }
       }
     }
+#ifdef DUCK_ASM_MARKS
+    asm volatile("; HF_LOOP_END" ::: "memory");
+#endif
+    STAGE_MARK(38);
     // 4 slots by mjx's _manifold_points over the prism contacts, from the deepest (the first prism
     // within HF_DEPTH_TIE of it: prisms sharing a grid vertex or edge often tie exactly); index
     // q = sub + 8 s is the prism's strip position
@@ -1681,6 +1858,7 @@ struct TPhys {
         P1::store_contact(Ls, 4 * p + sub, 1.0f, zero, nofr);
       }
     }
+    STAGE_MARK(39);
   }
 
   // Are the boxes enclosing the two hulls (mesh frames p, R) separated? 15-axis box/box SAT

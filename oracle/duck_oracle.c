@@ -664,9 +664,9 @@ static void collide_plane_convex(const oracle_model* m, oracle_data* d, int g1, 
 #define HF_MAXPRISM 128      /* prisms under one hull (the sub-grid of a 0.11 m foot: <= 18) */
 
 /* test aid: how often each class of separating axis gave a prism's penetration (oracle_hfield_axis_wins) */
-static long long hf_axis_wins[7];
-void oracle_hfield_axis_wins(long long out[7], int reset) {
-  for (int i = 0; i < 7; i++) { out[i] = hf_axis_wins[i]; if (reset) hf_axis_wins[i] = 0; }
+static long long hf_axis_wins[14];
+void oracle_hfield_axis_wins(long long out[14], int reset) {
+  for (int i = 0; i < 14; i++) { out[i] = hf_axis_wins[i]; if (reset) hf_axis_wins[i] = 0; }
 }
 
 /* the hull in the local frame (the height field's axes, origin at the hull's frame) */
@@ -779,7 +779,21 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
     ov[i] = pts_max(ax[i], (const double(*)[3])P, 6) - pts_min(ax[i], (const double(*)[3])H->V, H->nv);
     mn = fmin(mn, ov[i]);
   }
-  if (!(mn > 0)) return 0;
+  if (!(mn > 0)) {
+    /* separated: which class of axis separates, when the prism's own faces do not (kernel screen) */
+    int cheap = 1;
+    for (int i = 0; i < 5; i++) cheap &= ov[i] > 0;
+    if (cheap) {
+      int w = 0;
+      while (ov[w] > mn) w++;
+      int cls = w < 5 + H->nf ? 3 : 4 + kind_of_axis[w];
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+      hf_axis_wins[7 + cls]++;
+    }
+    return 0;
+  }
   int w = 0;
   while (ov[w] > mn) w++;
   {

@@ -73,8 +73,9 @@ int oracle_env_reset(const oracle_model* m, const duck_env_config* cfg, const du
 int oracle_hfield_prisms(const oracle_model* m, const oracle_data* d, int g_hf, int g_cvx, int max, double* depth,
                          double* normal, double* point, int* index);
 /* test aid: counts of the axis class that gave each prism contact (top, sides, bottom, hull faces,
- * top-edge pairs, vertical-edge pairs, bottom-edge pairs) since the last reset */
-void oracle_hfield_axis_wins(long long out[7], int reset);
+ * top-edge pairs, vertical-edge pairs, bottom-edge pairs) since the last reset, then [7 + class]
+ * the class that separated a prism whose own 5 faces do not */
+void oracle_hfield_axis_wins(long long out[14], int reset);
 void oracle_set_trace(double* buf); /* test aid: record substep inputs of oracle_env_step */
 int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref,
                     double* fstate, int32_t* istate, const double* action, double* obs, double* priv,

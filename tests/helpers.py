@@ -32,7 +32,8 @@ def parse_aux(m: Model, aux: np.ndarray):
     _, adr, nm = sparse_pattern(m)
     out, o = {}, 0
     for name, k in (("qacc", nv), ("qacc_smooth", nv), ("qvel", nv), ("qfrc_smooth", nv), ("actuator_force", nu),
-                    ("sensordata", nsd), ("con_dist", ncon), ("con_pos", 3 * ncon), ("M", nm)):
+                    ("sensordata", nsd), ("con_dist", ncon), ("con_pos", 3 * ncon), ("con_normal", 3 * ncon),
+                    ("M", nm)):
         out[name] = aux[o:o + k].T
         o += k
     n = aux.shape[1]

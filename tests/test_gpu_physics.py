@@ -209,3 +209,20 @@ def test_hfield_prism_contacts_match_oracle(task, height, gpu):
     print(f"{task} {height}: active slots {act.sum()}, envs ok dist {okd.mean():.4f} pos {okp.mean():.4f}")
     assert act.sum() > n
     assert okd.mean() >= 0.98 and okp.mean() >= 0.98, (okd.mean(), okp.mean())
+
+
+@pytest.mark.parametrize("task", ["rough_terrain", "rough_terrain_backlash"])
+def test_hfield_kernel_matches_brute_force_prisms(task, gpu):
+    """The kernel's height-field contacts against the brute-force prism reference (every axis of
+    every prism, fp64; tools/hfield_deviation.py --gpu) at oracle rollout states of rough + DR: the
+    feet's contact flags agree, the deepest depth to fp32 (1e-6 m at p99) and its normal to 0.1 deg
+    at p99 (fp32 ties of equal-depth prisms aside)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
+    from hfield_deviation import measure_gpu
+    r = measure_gpu(task, 32, 12, device=gpu)
+    print(r)
+    assert r["contact_kernel"] > 200
+    assert r["flag_agreement"] >= 0.999, r
+    assert r["depth_abs_diff_m"]["p99"] < 1e-6 and r["normal_angle_deg"]["p99"] < 0.1, r

@@ -9,7 +9,8 @@ U(-1,1) actions. Per foot and env-step: contact flag (any penetration) of each, 
 penetration of each, the angle between their deepest contacts' normals, and which class of axis
 gave the prism contacts (the kernel skips the bottom-edge pairs: never the minimum). CPU only.
 
-usage: python tools/hfield_deviation.py [n_envs] [n_steps]   (prints one JSON line per scene)
+usage: python tools/hfield_deviation.py [n_envs] [n_steps] [--gpu]   (one JSON line per scene)
+  --gpu: the HIP kernel's contacts at the oracle's rollout states against the brute-force prisms
 """
 
 import ctypes as C
@@ -49,7 +50,7 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
         pairs[g] = p
     rng = np.random.default_rng(seed)
     rows = []
-    wins = (C.c_longlong * 7)()
+    wins = (C.c_longlong * 14)()
     lib().oracle_hfield_axis_wins(wins, 1)
     for e in range(n_envs):
         om = OracleModel(m, dr=base.dr_sample(seed + 1, e))
@@ -83,15 +84,87 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
             "normal_angle_deg": {"median": float(np.nanmedian(ang)), "p99": float(np.nanquantile(ang, 0.99)),
                                  "max": float(np.nanmax(ang))},
             "axis_wins": dict(zip(("top", "side", "bottom", "hull_face", "top_edge", "vertical_edge", "bottom_edge"),
-                                  [int(x) for x in wins])),
+                                  [int(x) for x in wins[:7]])),
+            "separated_past_prism_faces_by": dict(zip(("hull_face", "top_edge", "vertical_edge", "bottom_edge"),
+                                                      [int(x) for x in wins[10:14]])),
             "penetrating_prisms_per_foot": {"mean": float(nprism[flag_r > 0].mean()), "max": int(nprism.max())}}
 
 
+def measure_gpu(task: str, n_envs: int, n_steps: int, seed: int = 0, device="cuda:0"):
+    """The HIP kernel's contacts (TPhys::collide_hfield, through duck_physics_step's forward) against
+    the brute-force prisms at the same states: oracle rollouts (rough + DR, U(-1,1) actions) give
+    the states; per foot the contact flag, the deepest depth and its normal are compared."""
+    import torch
+    from open_duck_playground_amd.joystick import Joystick, domain_randomize
+    from tests.helpers import parse_aux
+    m = Model.load(constants.task_to_xml(task))
+    base = OracleModel(m)
+    cfg = env_config_struct(m, default_config(), False, domain_randomize=True)
+    floor = m.id("geom", "floor")
+    pairs = {}
+    for foot in constants.FEET_GEOMS:
+        g = m.id("geom", foot)
+        pairs[g] = [k for k in range(m.npair) if {int(m.pair_geom1[k]), int(m.pair_geom2[k])} == {floor, g}][0]
+    env = Joystick(task, num_envs=n_envs, device=device, use_imitation=False)
+    domain_randomize(env, rng=seed + 1)  # column e carries dr_sample(seed + 1, e), as the oracle models
+    models = [OracleModel(m, dr=base.dr_sample(seed + 1, e)) for e in range(n_envs)]
+    envs = [OracleEnv(models[e], cfg) for e in range(n_envs)]
+    for e in range(n_envs):
+        envs[e].reset(seed=seed, env_id=e)
+    rng = np.random.default_rng(seed)
+    L = envs[0].L
+    o = L.off
+    rows = []
+    for t in range(n_steps):
+        X = np.zeros((n_envs, m.nq + 2 * m.nv + m.nu))
+        for e in range(n_envs):
+            envs[e].step(rng.uniform(-1, 1, m.nu))
+            f = envs[e].fs
+            X[e] = np.concatenate([f[o["qpos"]:o["qpos"] + m.nq], f[o["qvel"]:o["qvel"] + m.nv],
+                                   f[o["qacc_warmstart"]:o["qacc_warmstart"] + m.nv], f[o["ctrl"]:o["ctrl"] + m.nu]])
+        X = X.astype(np.float32).astype(np.float64)  # the state the kernel sees
+        T = lambda a: torch.tensor(np.ascontiguousarray(a.T), dtype=torch.float32, device=device)  # noqa: E731
+        sl = np.cumsum([0, m.nq, m.nv, m.nv, m.nu])
+        tq, tv, tw, tc = (T(X[:, sl[i]:sl[i + 1]]) for i in range(4))
+        aux = torch.zeros(env.aux_size() * n_envs, dtype=torch.float32, device=device).view(-1, n_envs)
+        env.physics_step(tq, tv, tw, tc, 0, aux)
+        torch.cuda.synchronize()
+        g = parse_aux(m, aux.cpu().numpy().astype(np.float64))
+        for e in range(n_envs):
+            d = models[e].new_data(qpos=X[e, :m.nq], qvel=X[e, m.nq:m.nq + m.nv], ctrl=X[e, sl[3]:],
+                                   warm=X[e, sl[2]:sl[3]])
+            models[e].forward(d)
+            for gid, p in pairs.items():
+                gd = g["con_dist"][e, 4 * p:4 * p + 4]
+                gn = g["con_normal"][e].reshape(-1, 3)[4 * p:4 * p + 4]
+                dep, nrm = prisms(models[e], d, floor, gid)
+                ours = -gd.min()
+                ref = dep.max() if len(dep) else -1.0
+                ang = np.nan
+                if ours > 0 and ref > 0:
+                    n1 = gn[int(np.argmin(gd))]
+                    n2 = nrm[int(np.argmax(dep))]
+                    ang = float(np.degrees(np.arccos(np.clip(n1 @ n2 / np.linalg.norm(n1), -1, 1))))
+                rows.append((ours > 0, ref > 0, max(ours, 0.0), max(ref, 0.0), ang))
+    a = np.array(rows, dtype=float)
+    flag_o, flag_r, dep_o, dep_r, ang = a.T
+    both = (flag_o > 0) & (flag_r > 0)
+    dd = np.abs(dep_o - dep_r)[both]
+    q = lambda x: {"median": float(np.median(x)), "p99": float(np.quantile(x, 0.99)), "max": float(np.max(x))}  # noqa: E731
+    return {"scene": task, "side": "HIP kernel (fp32) vs brute-force prisms (fp64)", "foot_samples": len(a),
+            "contact_kernel": int(flag_o.sum()), "contact_prism": int(flag_r.sum()),
+            "flag_agreement": float((flag_o == flag_r).mean()),
+            "flag_disagree_max_depth_m": float(np.max(np.maximum(dep_o, dep_r)[flag_o != flag_r], initial=0.0)),
+            "depth_abs_diff_m": q(dd), "normal_angle_deg": q(ang[both & np.isfinite(ang)])}
+
+
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    n = int(args[0]) if len(args) > 0 else 64
+    steps = int(args[1]) if len(args) > 1 else 50
     for task in ("rough_terrain", "rough_terrain_backlash"):
-        print(json.dumps(measure(task, n, steps)), flush=True)
+        r = measure_gpu(task, n, steps) if "--gpu" in sys.argv else measure(task, n, steps)
+        print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
