@@ -28,6 +28,7 @@ Extra JSON objects:
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -47,7 +48,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # FP32 VALU issue peak: 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz = 39.3 T lane-instructions/s (a wave64
 # VALU instruction occupies a SIMD for 4 cycles); = the 157.3 TFLOPS vector spec / 2 (FMA) / 2 (packed)
 VALU_PEAK_TLANE = 256 * 4 * 16 * 2.4e9 / 1e12
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r02_pmc_c2.json")  # tools/gpu_pmc.sh r02 C2
+# newest tools/gpu_pmc.sh <rNN> C2 summary; only used when its build id matches the loaded library
+PMC_PROFILE = (sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_c2.json")))
+               or [os.path.join(ROOT, "profiles", "r02_pmc_c2.json")])[-1]
 
 # BASELINE.json configs[1..4] (configs[0] is the reference's 1-env CPU plumbing case)
 CONFIGS = {

@@ -49,7 +49,7 @@ def test_teacher_forced_step_parity(case, gpu):
         for e in out.nonzero()[0]:
             x = explain(rep, t, int(e))
             print(f"  outlier step {t} env {e}: {x['kind']} max substep err {max(x['substep_err']):.2e} "
-                  f"flips {x.get('flips')}")
+                  f"flips {x.get('flips')} gpu_flip {x.get('gpu_flip')} chain_vs_step {x.get('chain_vs_step', 0):.2e}")
             if x["kind"] != "sensitive":
                 unexplained.append((t, int(e), x))
     assert not unexplained, unexplained
