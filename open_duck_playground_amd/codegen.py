@@ -271,13 +271,15 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         c = chain_of(m, m.geom_bodyid[m.id("geom", g)])
         put(name, c + [-1] * (maxchain_of(m) - len(c)))
     put("hull", [f2i(x) for x in np.asarray(m.hulls[0].vert, dtype=np.float64).reshape(-1)])
-    # height-field prism SAT (TPhys::collide_hfield): per hull face its outward normal and offset,
-    # per hull edge the Gauss-map arc of the negated hull (C = -n_A, D = -n_B), D x C, the edge
-    # vector and its first vertex (mesh frame)
-    # (height-field scenes only; the two tables are contiguous: TLay::HT_LDS copies them to LDS
-    # when the whole blob does not fit)
+    # height-field prism SAT (TPhys::collide_hfield / hf_exec): per hull face its outward normal
+    # and offset, per hull edge the Gauss-map arc of the negated hull (C = -n_A, D = -n_B), D x C,
+    # the edge vector and its first vertex, per hull vertex its position (mesh frame), each vector
+    # in its own 16-B record so that one ds_read_b128 fetches it (height-field scenes only; the
+    # three tables are contiguous and 16-B aligned: TLay::HT_LDS copies them to LDS when the whole
+    # blob does not fit)
     hull = m.hulls[0]
     if int(m.geom_type[floor]) == 1:
+        blob.extend([0] * (-len(blob) % 4))
         put("hface", [f2i(x) for f in range(len(hull.face_normal))
                       for x in list(hull.face_normal[f]) + [hull.face_offset[f]]])  # stride 4
         hef = hull_edge_faces(hull)
@@ -285,11 +287,13 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         for e, (a, b) in enumerate(hull.edge):
             C_, D_ = -np.asarray(hull.face_normal[hef[e][0]]), -np.asarray(hull.face_normal[hef[e][1]])
             v0, v1 = np.asarray(hull.vert[a]), np.asarray(hull.vert[b])
-            rec += [f2i(x) for x in np.concatenate([C_, D_, np.cross(D_, C_), v1 - v0, v0, [0.0]])]
-        put("hedge", rec)  # stride 16: C3, D3, DxC3, edge3, v0 3, pad
+            for v in (C_, D_, np.cross(D_, C_), v1 - v0, v0):
+                rec += [f2i(x) for x in v] + [f2i(0.0)]
+        put("hedge", rec)  # stride 20: C, D, D x C, edge, v0 (each + pad)
+        put("hvert", [f2i(x) for v in np.asarray(hull.vert) for x in list(v) + [0.0]])  # stride 4
         boff["hend"] = len(blob)
     else:
-        boff["hface"] = boff["hedge"] = boff["hend"] = -1
+        boff["hface"] = boff["hedge"] = boff["hvert"] = boff["hend"] = -1
     d2f, d2l = [-1] * nv, [-1] * nv
     for r, i in enumerate(fric):
         d2f[i] = r
@@ -443,6 +447,20 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
     return dev, acc
 
 
+def silhouette_cap(hull, hef, n_dir: int = 20000) -> int:
+    """The most hull edges on one silhouette (edges whose two faces lie on opposite sides of a
+    plane through the hull's Gauss map centre), over a Fibonacci sphere of view directions, plus
+    a margin of 4: the capacity of TPhys::collide_hfield's per-foot silhouette list."""
+    i = np.arange(n_dir) + 0.5
+    zz = 1 - 2 * i / n_dir
+    ph = np.pi * (1 + 5 ** 0.5) * i
+    r = np.sqrt(1 - zz * zz)
+    d = np.stack([r * np.cos(ph), r * np.sin(ph), zz], axis=1)
+    fn = np.asarray(hull.face_normal, dtype=np.float64)
+    sa, sb = d @ fn[hef[:, 0]].T, d @ fn[hef[:, 1]].T
+    return int(((sa * sb) < 0).sum(axis=1).max()) + 4
+
+
 def hull_edge_faces(hull) -> np.ndarray:
     """The two faces adjacent to each hull edge (from the merged polygons): edge e is the
     Gauss-map arc between the normals of faces [e][0] and [e][1] — the edge-pair filter of the
@@ -586,6 +604,12 @@ def model_header(m: Model, variant: str) -> str:
     out.append(_arr("hull_face_normal", hull.face_normal, "float"))
     out.append(_arr("hull_face_offset", hull.face_offset, "float"))
     out.append(_arr("hull_edge", hull.edge, "int"))
+    # the height field's per-lane prism SAT (TPhys::hf_exec): per hull edge its two faces (the
+    # Gauss-map arc C = -n_a -> D = -n_b) and D x C; HF_SILCAP bounds the edges on a silhouette
+    fnrm = np.asarray(hull.face_normal, dtype=np.float64)
+    out.append(_arr("hull_edge_face", hef, "int"))
+    out.append(_arr("hull_edge_dxc", np.cross(-fnrm[hef[:, 1]], -fnrm[hef[:, 0]]), "float"))
+    out.append(f"  static constexpr int HF_SILCAP = {silhouette_cap(hull, hef)};\n")
     # sparse mass-matrix pattern
     out.append(_arr("M_adr", adr, "int"))
     out.append(_arr("M_rowlen", [len(r) for r in rows], "int"))

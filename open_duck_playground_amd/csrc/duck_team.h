@@ -21,6 +21,8 @@ constexpr int TEAM = 16;
 constexpr int TEAM_WG = 16;  // envs (teams) per workgroup: 256 threads = 4 waves
 constexpr int TPB_TEAM = TEAM * TEAM_WG;
 typedef __attribute__((address_space(3))) int lds_int;
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) f4v lds_f4;
 
 // fp32 reciprocal as one v_rcp_f32 (1 ulp; operands here are never denormal or zero)
 DK float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
@@ -100,6 +102,35 @@ DK int hmin8i(int v) {
   v = min(v, dppi<0x4E>(v));
   v = min(v, dppi<0x141>(v));
   return v;
+}
+
+// Compile-time loops and compile-time vectors as instruction literals. The height field's SAT
+// multiplies per-lane vectors by hundreds of hull constants (face normals, edge directions,
+// vertices), each used several times: the compiler keeps such a constant in an SGPR, and with
+// this many the SGPRs spill to VGPR lanes (one v_readlane per use, 20 % of the SAT's
+// instructions). As a 32-bit literal of a VOP2 multiply / multiply-add it costs nothing.
+template <int B, int E, class F>
+DK void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+constexpr int fbits(float v) { return __builtin_bit_cast(int, v); }
+// c . x for c = (C0, C1, C2) (float bit patterns)
+template <int C0, int C1, int C2>
+DK float cdot(const float* x) {
+  float r;
+  asm("v_mul_f32_e32 %0, %1, %2" : "=v"(r) : "i"(C0), "v"(x[0]));
+  asm("v_fmac_f32_e32 %0, %1, %2" : "+v"(r) : "i"(C1), "v"(x[1]));
+  asm("v_fmac_f32_e32 %0, %1, %2" : "+v"(r) : "i"(C2), "v"(x[2]));
+  return r;
+}
+// a + c * x (fma with a literal c)
+template <int C>
+DK float cfma(float x, float a) {
+  asm("v_fmac_f32_e32 %0, %1, %2" : "+v"(a) : "i"(C), "v"(x));
+  return a;
 }
 
 // the height field's contact point when no vertex of either shape is inside the other: the
@@ -219,6 +250,14 @@ struct TPhys {
     } else {
       return tf(off);
     }
+  }
+  // a 16-B record of the hull SAT tables (blob words B_HFACE .. B_HEND, 16-B aligned, in LDS for
+  // the height-field scenes): the reads indexed per lane (the unrolled loops over all faces and
+  // edges take the compile-time constants instead: as LDS reads they were 28 % slower)
+  static DK f4v ht4(int off) {
+    extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+    static_assert(Md::FLOOR_TYPE != 1 || TL::TAB_LDS || TL::HT_LDS, "the hull SAT tables must be in LDS");
+    return *(const lds_f4*)((lds_float*)lds_dyn + TL::TAB + (TL::TAB_LDS ? off : off - Md::B_HFACE));
   }
   static constexpr int LIMW = 13, PAIRW = 13;
   // row -> dof and dof -> row maps of the friction and limit rows: affine when the rows cover
@@ -1324,6 +1363,212 @@ struct TPhys {
     (void)lane;
     return (unsigned)(b >> base) & 0xFFu;
   }
+  // products with the hull's compile-time faces, vertices and edge arcs (literal operands)
+  template <int F>
+  static DK float nf_dot(const float* x) {
+    return cdot<fbits(Md::hull_face_normal[F][0]), fbits(Md::hull_face_normal[F][1]), fbits(Md::hull_face_normal[F][2])>(x);
+  }
+  template <int K>
+  static DK float hv_dot(const float* x) {
+    return cdot<fbits(Md::hull_vert[K][0]), fbits(Md::hull_vert[K][1]), fbits(Md::hull_vert[K][2])>(x);
+  }
+  template <int E>
+  static DK float dxc_dot(const float* x) {
+    return cdot<fbits(Md::hull_edge_dxc[E][0]), fbits(Md::hull_edge_dxc[E][1]), fbits(Md::hull_edge_dxc[E][2])>(x);
+  }
+  template <int F>
+  static DK float nf_off_minus(float x) {  // offset_F - x
+    float r;
+    asm("v_sub_f32_e32 %0, %1, %2" : "=v"(r) : "i"(fbits(Md::hull_face_offset[F])), "v"(x));
+    return r;
+  }
+
+  // queue and silhouette-list layout of the height-field SAT (collide_hfield / hf_exec), in the
+  // env slice: the survivor queue in the H + constraint-row storage (dead until make_rows()),
+  // the per-foot silhouette lists in the composite inertias (dead after crb())
+  static constexpr int HF_PRIO_T = 5 + Md::NHF, HF_PRIO_V = HF_PRIO_T + 3 * Md::NHE;
+  static constexpr int HF_ENT = 28, HF_QH0 = (Ly::H + 3) & ~3;
+  static constexpr int HF_QE = (Ly::CR - HF_QH0) / HF_ENT, HF_QR = 4 * HF_QE < 64 ? 4 * HF_QE : 64;
+  static constexpr int HF_CINQ = (Ly::CIN + 3) & ~3, HF_SLF = (1 + Md::HF_SILCAP + 3) & ~3;
+  static constexpr int HF_SLSZ = HF_SLF + 4 * Md::HF_SILCAP;
+  static_assert(Md::FLOOR_TYPE != 1 || (HF_QE >= 2 && HF_CINQ + 2 * HF_SLSZ <= Ly::CIN + 10 * Md::NB),
+                "height-field SAT queue / silhouette lists must fit their LDS storage");
+
+  // One prism's separating-axis test against the hull for the lane that runs queue entry E
+  // (collide_hfield), in the hull's mesh frame with the hull's compile-time vertices, faces and
+  // edges: the screen's minimum over the prism's faces, bottom and the hull's faces is continued
+  // with the vertical-edge pairs (the foot's silhouette list) and the top-edge pairs whose Gauss
+  // arcs cross (Gregorius' Minkowski-face test over all hull edges, then the overlap of each
+  // crossing pair); equal overlaps: the lowest priority (oracle hf_prism_contact's order). Then
+  // the contact point (oracle: the penetration-weighted centroid of the vertices of each shape
+  // inside the other, or the midpoint of the support features). Writes (depth, normal, point)
+  // over the entry's first 8 floats; depth -1 when separated.
+  static DK void hf_exec(lds_float* E, LP L, int tw) {
+    constexpr int NH = Md::NHV, NF = Md::NHF, NE = Md::NHE;
+    constexpr int NPW = (3 * NE + 63) / 64;
+    static_assert(NPW <= 3, "top-edge pair masks");
+    constexpr float DXC = 2.0f * Md::HF_SIZE[0] / (Md::HF_NCOL - 1), DYC = 2.0f * Md::HF_SIZE[1] / (Md::HF_NROW - 1);
+    const float GN = 1.0f / sqrtf(DXC * DXC + DYC * DYC);
+    const float GX = DYC * GN, GY = DXC * GN;
+    lds_f4* E4 = (lds_f4*)E;
+    const f4v d0 = E4[0], d1 = E4[1], d2 = E4[2], d3 = E4[3], d4 = E4[4], d5 = E4[5], d6 = E4[6];
+    const float Tm[3][3] = {{d0.x, d0.y, d0.z}, {d1.x, d1.y, d1.z}, {d2.x, d2.y, d2.z}};
+    const float base = d0.w;
+    float mo = d1.w;
+    int mp = __float_as_int(d2.w);
+    const int tag = __float_as_int(d3.w), tri = tag & 1, foot = tag >> 1;
+    const float ntm[3] = {d3.x, d3.y, d3.z}, zc[3] = {d4.x, d4.y, d4.z};
+    const float xc[3] = {d5.x, d5.y, d5.z}, yc[3] = {d6.x, d6.y, d6.z};
+    // the prism's side normals (triangle kind A: -x, (g_x, g_y), -y; B: -(g_x, g_y), +x, +y)
+    float sm[3][3];
+    {
+      const float sx[3] = {tri ? -GX : -1.0f, tri ? 1.0f : GX, 0.0f};
+      const float sy[3] = {tri ? -GY : 0.0f, tri ? 0.0f : GY, tri ? 1.0f : -1.0f};
+      for (int k = 0; k < 3; k++)
+        for (int a = 0; a < 3; a++) sm[k][a] = sx[k] * xc[a] + sy[k] * yc[a];
+    }
+    float mu[3] = {0.0f, 0.0f, 0.0f};
+    auto take = [&](float ov, int pr, const float* u) {
+      const bool b = (ov < mo) | ((ov == mo) & (pr < mp));
+      mo = b ? ov : mo;
+      mp = b ? pr : mp;
+      for (int a = 0; a < 3; a++) mu[a] = b ? u[a] : mu[a];
+    };
+    // vertical-edge pairs: the prism's support along w is its vertical edge at vertex kk
+    {
+      const lds_float* SL = L + ((foot >> 1) - tw) * TL::STRIDE + HF_CINQ + (foot & 1) * HF_SLSZ;
+      const int n = ((const lds_int*)SL)[0];
+      for (int i = 0; i < n; i++) {
+        const int e = ((const lds_int*)SL)[1 + i];
+        const f4v w = ((const lds_f4*)(SL + HF_SLF))[i];
+        const float wv[3] = {w.x, w.y, w.z};
+        const float q0 = dot3(wv, Tm[0]), q1 = dot3(wv, Tm[1]), q2 = dot3(wv, Tm[2]);
+        const int kk = q0 >= q1 ? (q0 >= q2 ? 0 : 2) : (q1 >= q2 ? 1 : 2);
+        take(fmaxf(q0, fmaxf(q1, q2)) - w.w, HF_PRIO_V + 3 * e + kk, wv);
+      }
+    }
+    // top-edge pairs (hull edge e, prism top edge k: faces ntm, sm_k). Pass 1: the arcs cross when
+    // CBA DBA < 0, ADC BDC < 0 and CBA BDC > 0 (C = -n_a, D = -n_b, B x A = sm_k x ntm: CBA =
+    // -phi_a), all three products negative: the sign bit of their maximum, bit 3 e + k of pm
+    unsigned long long pm[3] = {0ull, 0ull, 0ull};
+    {
+      float hx[3][3];
+      for (int k = 0; k < 3; k++) cross3(hx[k], sm[k], ntm);
+      // (one prism edge at a time: 30 face products live, not 90)
+      float ADC[NE];
+      static_for<0, NE>([&](auto eI) { ADC[eI.value] = dxc_dot<eI.value>(ntm); });
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        float phi[NF];
+        static_for<0, NF>([&](auto fI) { phi[fI.value] = nf_dot<fI.value>(hx[k]); });
+        static_for<0, NE>([&](auto eI) {
+          constexpr int e = eI.value, fa = Md::hull_edge_face[e][0], fb = Md::hull_edge_face[e][1];
+          const float BDC = dxc_dot<e>(sm[k]);
+          const float mx = fmaxf(fmaxf(phi[fa] * phi[fb], ADC[e] * BDC), phi[fa] * BDC);
+          const int p = 3 * e + k;
+          pm[p >> 6] |= (unsigned long long)(__float_as_uint(mx) >> 31) << (p & 63);
+        });
+      }
+    }
+    // pass 2: each crossing pair's overlap along ev x em (lowest pair first)
+    while (pm[0] | pm[1] | pm[2]) {
+      const bool z0 = pm[0] == 0ull, z1 = pm[1] == 0ull;
+      const unsigned long long w = z0 ? (z1 ? pm[2] : pm[1]) : pm[0];
+      const int p = (z0 ? (z1 ? 128 : 64) : 0) + __builtin_ctzll(w);
+      const unsigned long long wc = w & (w - 1ull);
+      pm[0] = z0 ? pm[0] : wc;
+      pm[1] = z0 && !z1 ? wc : pm[1];
+      pm[2] = z0 && z1 ? wc : pm[2];
+      const int e = p / 3, k = p - 3 * e, o = Md::B_HEDGE + 20 * e;
+      const f4v ev4 = ht4(o + 12), v04 = ht4(o + 16);
+      const float ev[3] = {ev4.x, ev4.y, ev4.z}, v0[3] = {v04.x, v04.y, v04.z};
+      float em[3], tm[3], sk[3];
+      for (int a = 0; a < 3; a++) {
+        const float t0 = Tm[0][a], t1 = Tm[1][a], t2 = Tm[2][a];
+        tm[a] = k == 0 ? t0 : (k == 1 ? t1 : t2);
+        em[a] = (k == 0 ? t1 : (k == 1 ? t2 : t0)) - tm[a];
+        sk[a] = k == 0 ? sm[0][a] : (k == 1 ? sm[1][a] : sm[2][a]);
+      }
+      float u[3];
+      cross3(u, ev, em);
+      const float u2 = dot3(u, u);
+      if (u2 >= 1e-12f * dot3(ev, ev) * dot3(em, em)) {
+        const float sg = (dot3(u, ntm) + dot3(u, sk) < 0.0f ? -1.0f : 1.0f) * __builtin_amdgcn_rsqf(u2);
+        const float un[3] = {sg * u[0], sg * u[1], sg * u[2]};
+        take(sg * (dot3(u, tm) - dot3(u, v0)), HF_PRIO_T + p, un);
+      }
+    }
+    if (!(mo > 0.0f)) {
+      E4[0] = f4v{-1.0f, 0.0f, 0.0f, 0.0f};
+      return;
+    }
+    // the screen's axes: the prism's top, sides, bottom or a hull face
+    if (mp < HF_PRIO_T) {
+      const int f = mp - 5;
+      const f4v n4 = ht4(Md::B_HFACE + 4 * (f > 0 ? f : 0));
+      const float nf[3] = {-n4.x, -n4.y, -n4.z};
+      for (int a = 0; a < 3; a++) {
+        const float s = mp == 1 ? sm[0][a] : (mp == 2 ? sm[1][a] : sm[2][a]);
+        mu[a] = mp == 0 ? ntm[a] : (mp < 4 ? s : (mp == 4 ? -zc[a] : nf[a]));
+      }
+    }
+    // the contact point: hull vertices inside the prism and prism top vertices inside the hull,
+    // weighted by their penetration
+    const float ptop = dot3(ntm, Tm[0]);
+    const float smt[3] = {dot3(sm[0], Tm[0]), dot3(sm[1], Tm[1]), dot3(sm[2], Tm[2])};
+    float W = 0.0f, Cx[3] = {0.0f, 0.0f, 0.0f};
+    static_for<0, NH>([&](auto kI) {
+      constexpr int k = kI.value;
+      float pen = fminf(ptop - hv_dot<k>(ntm), hv_dot<k>(zc) - base);
+      for (int j = 0; j < 3; j++) pen = fminf(pen, smt[j] - hv_dot<k>(sm[j]));
+      const float w = fmaxf(pen, 0.0f);
+      W += w;
+      Cx[0] = cfma<fbits(Md::hull_vert[k][0])>(w, Cx[0]);
+      Cx[1] = cfma<fbits(Md::hull_vert[k][1])>(w, Cx[1]);
+      Cx[2] = cfma<fbits(Md::hull_vert[k][2])>(w, Cx[2]);
+    });
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      float pk = 1e30f;
+      static_for<0, NF>([&](auto fI) { pk = fminf(pk, nf_off_minus<fI.value>(nf_dot<fI.value>(Tm[j]))); });
+      const float w = fmaxf(pk, 0.0f);
+      W += w;
+      for (int a = 0; a < 3; a++) Cx[a] += w * Tm[j][a];
+    }
+    float pos[3];
+    if (W > 0.0f) {
+      const float iw = 1.0f / W;
+      for (int a = 0; a < 3; a++) pos[a] = Cx[a] * iw;
+    } else {
+      // crossing edges: the midpoint of the two shapes' support features along mu
+      float hmu = 1e30f;
+      float hv[NH];
+      static_for<0, NH>([&](auto kI) { hv[kI.value] = hv_dot<kI.value>(mu); });
+#pragma unroll
+      for (int k = 0; k < NH; k++) hmu = fminf(hmu, hv[k]);
+      float wh_ = 0.0f, ch[3] = {0.0f, 0.0f, 0.0f};
+      static_for<0, NH>([&](auto kI) {
+        constexpr int k = kI.value;
+        const float w = fmaxf(0.0f, 1.0f - (hv[k] - hmu) * (1.0f / HF_WITNESS_BAND));
+        wh_ += w;
+        ch[0] = cfma<fbits(Md::hull_vert[k][0])>(w, ch[0]);
+        ch[1] = cfma<fbits(Md::hull_vert[k][1])>(w, ch[1]);
+        ch[2] = cfma<fbits(Md::hull_vert[k][2])>(w, ch[2]);
+      });
+      const float q[3] = {dot3(mu, Tm[0]), dot3(mu, Tm[1]), dot3(mu, Tm[2])};
+      const float pmx = fmaxf(q[0], fmaxf(q[1], q[2]));
+      float wp_ = 0.0f, cq[3] = {0.0f, 0.0f, 0.0f};
+      for (int k = 0; k < 3; k++) {
+        const float w = fmaxf(0.0f, 1.0f - (pmx - q[k]) * (1.0f / HF_WITNESS_BAND));
+        wp_ += w;
+        for (int a = 0; a < 3; a++) cq[a] += w * Tm[k][a];
+      }
+      for (int a = 0; a < 3; a++) pos[a] = 0.5f * (ch[a] / wh_ + cq[a] / wp_);
+    }
+    E4[0] = f4v{mo, mu[0], mu[1], mu[2]};
+    E4[1] = f4v{pos[0], pos[1], pos[2], 0.0f};
+  }
+
   static DK void collide_hfield(LP L, int lane, const float* hf) {
     STAGE_T0();
     constexpr int NH = Md::NHV, NF = Md::NHF, NE = Md::NHE;
@@ -1334,9 +1579,6 @@ struct TPhys {
     static_assert(MAXP <= 32, "prism masks are 32-bit");
     constexpr int NGV = (Md::HF_MAXCX + 1) * (Md::HF_MAXCY + 1), GPL = (NGV + 7) / 8;
     constexpr int VPL = (NH + 7) / 8, FPL = (NF + 7) / 8, EPL = (NE + 7) / 8;
-    // axis priorities (equal overlaps: the lowest wins, the oracle's order): prism top 0, sides 1-3,
-    // bottom 4, hull faces, top-edge pairs by (hull edge, k), vertical-edge pairs by (edge, k)
-    constexpr int PRIO_T = 5 + NF, PRIO_V = PRIO_T + 3 * NE, NOPRIO = 1 << 28;
     const int h = lane >> 3, sub = lane & 7;
     const int p = Md::PLANE_PAIR[0] * (1 - h) + Md::PLANE_PAIR[1] * h;
     const int gs = cgeom_slot<Md>(Md::pair_geom2[p]);
@@ -1443,8 +1685,11 @@ struct TPhys {
       }
     const float obot = hi[2] - base;
     // 1. lane-parallel screen: prism q = sub + 8 j passes the height test and the axes of its own
-    // faces and the bottom (the hull's support along its top normal from the compile-time
-    // vertices); only survivors get the full separating-axis test
+    // faces, the bottom and the hull's faces (the hull's support along its top normal from the
+    // compile-time vertices). The running minimum and its axis priority are kept: the survivors'
+    // SAT (hf_exec) continues from them with the edge pairs.
+    float smo[PPL], szt[PPL][3];
+    int smp[PPL];
     unsigned surv = 0;
 #pragma unroll
     for (int j = 0; j < PPL; j++) {
@@ -1456,59 +1701,75 @@ struct TPhys {
       float ntm[3];
       mulmtv3(ntm, R, nt);
       float hm = 1e30f;
-#pragma unroll
-      for (int k = 0; k < NH; k++) hm = fminf(hm, dot3(ntm, Md::hull_vert[k]));
-      float o = dot3(nt, T[0]) - hm;
+      static_for<0, NH>([&](auto kI) { hm = fminf(hm, hv_dot<kI.value>(ntm)); });
+      // priority order (equal overlaps: the first): top 0, sides 1-3, bottom 4, hull faces 5 + f
+      float mo = dot3(nt, T[0]) - hm;
+      int mp = 0;
       for (int k = 0; k < 3; k++) {  // (tri is 0 or 1: two-way selects, not an indexed register array)
         const float sxk = tri ? sx_[1][k] : sx_[0][k], syk = tri ? sy_[1][k] : sy_[0][k];
-        o = fminf(o, sxk * T[k][0] + syk * T[k][1] - (tri ? smin[1][k] : smin[0][k]));
+        const float ov = sxk * T[k][0] + syk * T[k][1] - (tri ? smin[1][k] : smin[0][k]);
+        mp = ov < mo ? 1 + k : mp;
+        mo = fminf(mo, ov);
       }
-      // ... and the hull's faces (compile-time normals): the prism's lowest point along n_f, a
-      // bottom vertex where n_f leans up the field's z
-#ifndef DUCK_HF_NO_FACE_SCREEN
+      mp = obot < mo ? 4 : mp;
+      mo = fminf(mo, obot);
       {
+        // the hull's faces (compile-time normals): the prism's lowest point along n_f, a bottom
+        // vertex where n_f leans up the field's z
         float Tm[3][3], hk[3];
         for (int k = 0; k < 3; k++) { mulmtv3(Tm[k], R, T[k]); hk[k] = T[k][2] - base; }
+        static_for<0, NF>([&](auto fI) {
+          constexpr int f = fI.value;
+          const float nz = fmaxf(nf_dot<f>(zc), 0.0f);
+          float pm = nf_dot<f>(Tm[0]) - hk[0] * nz;
+          pm = fminf(pm, nf_dot<f>(Tm[1]) - hk[1] * nz);
+          pm = fminf(pm, nf_dot<f>(Tm[2]) - hk[2] * nz);
+          const float ov = nf_off_minus<f>(pm);
+          mp = ov < mo ? 5 + f : mp;
+          mo = fminf(mo, ov);
+        });
+      }
+      const bool high = !(T[0][2] < lo[2] && T[1][2] < lo[2] && T[2][2] < lo[2]);
+      const bool ok = q < np && high && mo > 0.0f;
+      surv |= half_bits(__ballot(ok), lane) << (8 * j);
+      smo[j] = mo;
+      smp[j] = mp;
+      for (int k = 0; k < 3; k++) szt[j][k] = T[k][2];
+    }
+    // this foot's silhouette edges (the hull's edges whose faces straddle the field's horizontal
+    // plane: the only ones whose Gauss arc crosses a prism's vertical-edge arc), compacted in edge
+    // order into the env slice's composite-inertia storage (dead after crb()): the direction w in
+    // which the negated arc crosses the equator and the hull's support along it
+    lds_float* const SLo = L + HF_CINQ + h * HF_SLSZ;
+    {
+      unsigned long long M = 0;
+      float wv[EPL][3], wh[EPL];
+      bool sl[EPL];
 #pragma unroll
-        for (int f = 0; f < NF; f++) {
-          const float* n = Md::hull_face_normal[f];
-          const float nz = fmaxf(dot3(n, zc), 0.0f);
-          float pm = dot3(n, Tm[0]) - hk[0] * nz;
-          pm = fminf(pm, dot3(n, Tm[1]) - hk[1] * nz);
-          pm = fminf(pm, dot3(n, Tm[2]) - hk[2] * nz);
-          o = fminf(o, Md::hull_face_offset[f] - pm);
+      for (int j = 0; j < EPL; j++) {
+        const int e = sub + 8 * j, ee = e < NE ? e : 0, o = Md::B_HEDGE + 20 * ee;
+        const f4v C4 = ht4(o), D4 = ht4(o + 4), v04 = ht4(o + 16);
+        const float C[3] = {C4.x, C4.y, C4.z}, D[3] = {D4.x, D4.y, D4.z}, v0[3] = {v04.x, v04.y, v04.z};
+        const float sa = dot3(C, zc), sb = dot3(D, zc);
+        const float w[3] = {fabsf(sb) * C[0] + fabsf(sa) * D[0], fabsf(sb) * C[1] + fabsf(sa) * D[1],
+                            fabsf(sb) * C[2] + fabsf(sa) * D[2]};
+        const float wn = sqrtf(dot3(w, w));
+        sl[j] = e < NE && sa * sb < 0.0f && wn > 0.0f;
+        const float inv = sl[j] ? 1.0f / wn : 0.0f;
+        for (int a = 0; a < 3; a++) wv[j][a] = w[a] * inv;
+        wh[j] = dot3(wv[j], v0);
+        M |= (unsigned long long)half_bits(__ballot(sl[j]), lane) << (8 * j);
+      }
+#pragma unroll
+      for (int j = 0; j < EPL; j++) {
+        const int e = sub + 8 * j;
+        const int r = __popcll(M & ((1ull << e) - 1ull));
+        if (sl[j] && r < Md::HF_SILCAP) {
+          ((lds_int*)SLo)[1 + r] = e;
+          ((lds_f4*)(SLo + HF_SLF))[r] = f4v{wv[j][0], wv[j][1], wv[j][2], wh[j]};
         }
       }
-#endif
-      const bool high = !(T[0][2] < lo[2] && T[1][2] < lo[2] && T[2][2] < lo[2]);
-      const bool ok = q < np && high && fminf(o, obot) > 0.0f;
-      surv |= half_bits(__ballot(ok), lane) << (8 * j);
-    }
-    // per-lane constants of the survivor loop: this lane's hull faces f = sub + 8 j (mesh normal,
-    // offset, the normal's lean up the field's z) and silhouette edges e = sub + 8 j (the crossing
-    // direction w of the negated Gauss arc with the field's equator, the hull's support along it)
-    float fnv[FPL][3], fof[FPL], fnz[FPL];
-#pragma unroll
-    for (int j = 0; j < FPL; j++) {
-      const int f = sub + 8 * j, ff = f < NF ? f : 0, o = Md::B_HFACE + 4 * ff;
-      for (int a = 0; a < 3; a++) fnv[j][a] = th(o + a);
-      fof[j] = f < NF ? th(o + 3) : 1e30f;  // a padding face never wins and never bounds
-      fnz[j] = fmaxf(dot3(fnv[j], zc), 0.0f);
-    }
-    float wv[EPL][3], wh[EPL];
-#pragma unroll
-    for (int j = 0; j < EPL; j++) {
-      const int e = sub + 8 * j, ee = e < NE ? e : 0, o = Md::B_HEDGE + 16 * ee;
-      const float C[3] = {th(o), th(o + 1), th(o + 2)}, D[3] = {th(o + 3), th(o + 4), th(o + 5)};
-      const float v0[3] = {th(o + 12), th(o + 13), th(o + 14)};
-      const float sa = dot3(C, zc), sb = dot3(D, zc);
-      const bool sil = e < NE && sa * sb < 0.0f;
-      float w[3] = {fabsf(sb) * C[0] + fabsf(sa) * D[0], fabsf(sb) * C[1] + fabsf(sa) * D[1],
-                    fabsf(sb) * C[2] + fabsf(sa) * D[2]};
-      const float wn = sqrtf(dot3(w, w));
-      const float inv = sil && wn > 0.0f ? 1.0f / wn : 0.0f;
-      for (int a = 0; a < 3; a++) wv[j][a] = w[a] * inv;
-      wh[j] = sil && wn > 0.0f ? dot3(wv[j], v0) : -1e30f;
+      if (sub == 0) ((lds_int*)SLo)[0] = min(__popcll(M), Md::HF_SILCAP);
     }
     float cd[PPL], cn[PPL][3], cx[PPL][3];  // this lane's prism contacts: depth, normal, point (local)
 #pragma unroll
@@ -1517,221 +1778,86 @@ struct TPhys {
       for (int a = 0; a < 3; a++) { cn[s][a] = 0.0f; cx[s][a] = 0.0f; }
     }
     STAGE_MARK(37);
-    // 2. the survivors, one at a time over the half-team (the mask is uniform over it)
-    while (surv) {
-#ifdef DUCK_ASM_MARKS
-      asm volatile("; HF_LOOP_TOP" ::: "memory");
-#endif
-      const int pi = __builtin_ctz(surv);
-      surv &= surv - 1;
-#ifdef DUCK_STAGE_PROF
-      if (threadIdx.x == 0) STAGE_ADD(40, 1ull);  // survivors of one foot (team 0, first half)
-      {
-        const unsigned long long act = __ballot(1);  // iterations the wave runs (any half active)
-        if (threadIdx.x < 64 && (int)threadIdx.x == __ffsll((long long)act) - 1) STAGE_ADD(46, 1ull);
-      }
-#endif
-      float T[3][3], nt[3];
-      int tri;
-      prism_top(pi, T, tri);
-      top_normal(T, nt);
-      float sl[3][3];
-      float smk[3];  // this triangle kind's side normals and the hull's minima along them
-      for (int k = 0; k < 3; k++) {
-        sl[k][0] = tri ? sx_[1][k] : sx_[0][k];
-        sl[k][1] = tri ? sy_[1][k] : sy_[0][k];
-        sl[k][2] = 0.0f;
-        smk[k] = tri ? smin[1][k] : smin[0][k];
-      }
-      // the axes of the prism's faces (uniform): overlap = the prism's support minus the hull's
-      // lowest point along the axis
-      const float ptop = dot3(nt, T[0]);
-      float hm = 1e30f;
+    // 2. the survivors of the wave's 8 feet, one per lane: a queue in the H + constraint-row
+    // storage of the wave's 4 env slices (dead until make_rows()), entry g in slice g & 3; each
+    // lane writes its survivors' descriptors (mesh frame), every active lane runs one entry's SAT
+    // (hf_exec) and writes the contact back, the owners collect them. Rounds of QR entries.
+    const int hw = ((int)threadIdx.x & 63) >> 3, tw = hw >> 1;
+    const unsigned long long act = __ballot(1);
+    int S = 0, g0 = 0;
+    {
+      const int cnt = __popc(surv);
 #pragma unroll
-      for (int i = 0; i < VPL; i++)
-        if (vok[i]) hm = fminf(hm, dot3(nt, xl[i]));
-      hm = hmin8f(hm);
-      float mo = ptop - hm, mu[3];  // this lane's running minimum (overlap, priority, axis (mesh))
-      int mp = 0;
-      mulmtv3(mu, R, nt);
-      float Tm[3][3], sm[3][3], ntm[3], hk[3];
-      for (int k = 0; k < 3; k++) {
-        mulmtv3(Tm[k], R, T[k]);
-        mulmtv3(sm[k], R, sl[k]);
-        hk[k] = T[k][2] - base;
-      }
-      for (int a = 0; a < 3; a++) ntm[a] = mu[a];
-      for (int k = 0; k < 3; k++) {
-        const float osd = sl[k][0] * T[k][0] + sl[k][1] * T[k][1] - smk[k];
-        if (osd < mo) { mo = osd; mp = 1 + k; for (int a = 0; a < 3; a++) mu[a] = sm[k][a]; }
-      }
-      if (obot < mo) { mo = obot; mp = 4; for (int a = 0; a < 3; a++) mu[a] = -zc[a]; }
-      STAGE_MARK(41);
-      // hull faces: the axis -n_f, overlap = offset_f - the prism's lowest point along n_f (a
-      // bottom vertex where n_f leans up)
-#pragma unroll
-      for (int j = 0; j < FPL; j++) {
-        float pm = 1e30f;
-        for (int k = 0; k < 3; k++) pm = fminf(pm, dot3(fnv[j], Tm[k]) - hk[k] * fnz[j]);
-        const float ov = fof[j] - pm;
-        if (ov < mo) { mo = ov; mp = 5 + sub + 8 * j; for (int a = 0; a < 3; a++) mu[a] = -fnv[j][a]; }
-      }
-      STAGE_MARK(42);
-      // vertical-edge pairs: the prism's support along w is the vertical edge at vertex k
-#pragma unroll
-      for (int j = 0; j < EPL; j++) {
-        const int e = sub + 8 * j;
-        const float q0 = dot3(wv[j], Tm[0]), q1 = dot3(wv[j], Tm[1]), q2 = dot3(wv[j], Tm[2]);
-        const int kk = q0 >= q1 ? (q0 >= q2 ? 0 : 2) : (q1 >= q2 ? 1 : 2);
-        const float ov = fmaxf(q0, fmaxf(q1, q2)) - wh[j];
-        const int pr = PRIO_V + 3 * e + kk;
-        if (ov < mo || (ov == mo && pr < mp)) { mo = ov; mp = pr; for (int a = 0; a < 3; a++) mu[a] = wv[j][a]; }
-      }
-      // top-edge pairs (hull edge e = sub + 8j, prism top edge k: faces nt, s_k): Gregorius'
-      // Minkowski-face test, the same enumeration as the oracle's. (A lower bound per arc that skips
-      // arcs which cannot beat the running minimum cost more than it saved: -1.5 % C4 / C5.)
-      float BxA[3][3], Em[3][3];
-      for (int k = 0; k < 3; k++) {
-        cross3(BxA[k], sm[k], ntm);
-        for (int a = 0; a < 3; a++) Em[k][a] = Tm[(k + 1) % 3][a] - Tm[k][a];
-      }
-      // pass 1: the Minkowski-face tests of this lane's (edge, arc) pairs into a bit mask
-#ifdef DUCK_ASM_MARKS
-      asm volatile("; HF_PASS1" ::: "memory");
-#endif
-      unsigned pass = 0;
-      {
-#pragma unroll
-        for (int j = 0; j < EPL; j++) {
-          const int e = sub + 8 * j, ee = e < NE ? e : 0, o = Md::B_HEDGE + 16 * ee;
-          const float C[3] = {th(o), th(o + 1), th(o + 2)}, D[3] = {th(o + 3), th(o + 4), th(o + 5)};
-          const float DxC[3] = {th(o + 6), th(o + 7), th(o + 8)};
-          const float ADC = dot3(ntm, DxC);
-          unsigned bits = 0;
-#pragma unroll
-          for (int k = 0; k < 3; k++) {
-            // the arcs cross when CBA DBA < 0, ADC BDC < 0 and CBA BDC > 0: all three products
-            // negative, i.e. the sign bit of their maximum (branch-free, no condition masks)
-            const float CBA = dot3(C, BxA[k]), DBA = dot3(D, BxA[k]), BDC = dot3(sm[k], DxC);
-            const float mx = fmaxf(fmaxf(CBA * DBA, ADC * BDC), -(CBA * BDC));
-            bits |= (__float_as_uint(mx) >> 31) << k;
-          }
-          if (j == EPL - 1 && NE < 8 * EPL) bits = e < NE ? bits : 0u;
-          pass |= bits << (3 * j);
-        }
-      }
-      // pass 2: the overlap of each passing pair (a few per lane: the wave loops over the most any
-      // lane has, not over all 3 x EPL)
-#ifdef DUCK_ASM_MARKS
-      asm volatile("; HF_PASS2" ::: "memory");
-#endif
-      while (pass) {
-        const int jk = __builtin_ctz(pass);
-        pass &= pass - 1;
-        const int j = jk / 3, k = jk - 3 * j, e = sub + 8 * j, o = Md::B_HEDGE + 16 * e;
-        const float ev[3] = {th(o + 9), th(o + 10), th(o + 11)}, v0[3] = {th(o + 12), th(o + 13), th(o + 14)};
-        float em[3], tm[3], sk[3];
-        for (int a = 0; a < 3; a++) {
-          em[a] = k == 0 ? Em[0][a] : (k == 1 ? Em[1][a] : Em[2][a]);
-          tm[a] = k == 0 ? Tm[0][a] : (k == 1 ? Tm[1][a] : Tm[2][a]);
-          sk[a] = k == 0 ? sm[0][a] : (k == 1 ? sm[1][a] : sm[2][a]);
-        }
-        float u[3];
-        cross3(u, ev, em);
-        const float u2 = dot3(u, u);
-        if (u2 >= 1e-12f * dot3(ev, ev) * dot3(em, em)) {
-          const float sg = (dot3(u, ntm) + dot3(u, sk) < 0.0f ? -1.0f : 1.0f) * __builtin_amdgcn_rsqf(u2);
-          const float ov = sg * (dot3(u, tm) - dot3(u, v0));
-          const int pr = PRIO_T + 3 * e + k;
-          if (ov < mo || (ov == mo && pr < mp)) {
-            mo = ov;
-            mp = pr;
-            for (int a = 0; a < 3; a++) mu[a] = sg * u[a];
-          }
-        }
-      }
-      STAGE_MARK(43);
-      STAGE_MARK(44);
-      // the minimum over the half-team; equal overlaps: the lowest priority
-#ifdef DUCK_ASM_MARKS
-      asm volatile("; HF_AXES_DONE" ::: "memory");
-#endif
-      const float mn = hmin8f(mo);
-      const int wp = hmin8i(mo == mn ? mp : NOPRIO);
-      const int wl = hmin8i(mo == mn && mp == wp ? sub : 8);
-      float um[3];
-      for (int a = 0; a < 3; a++) um[a] = __shfl(mu[a], 8 * h + wl, TEAM);
-      STAGE_MARK(45);
-      if (!(mn > 0.0f)) continue;
-      // the contact point: hull vertices inside the prism and prism top vertices inside the hull,
-      // weighted by their penetration
-      float W = 0.0f, Cx[3] = {0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int i = 0; i < VPL; i++) {
-        float pen = fminf(ptop - dot3(nt, xl[i]), xl[i][2] - base);
-        for (int k = 0; k < 3; k++) pen = fminf(pen, sl[k][0] * (T[k][0] - xl[i][0]) + sl[k][1] * (T[k][1] - xl[i][1]));
-        const float w = vok[i] ? fmaxf(pen, 0.0f) : 0.0f;
-        W += w;
-        for (int a = 0; a < 3; a++) Cx[a] += w * xl[i][a];
-      }
-      float pk[3];
-      for (int k = 0; k < 3; k++) {
-        pk[k] = 1e30f;
-#pragma unroll
-        for (int j = 0; j < FPL; j++) pk[k] = fminf(pk[k], fof[j] - dot3(fnv[j], Tm[k]));
-      }
-      W = hsum8(W);
-      for (int a = 0; a < 3; a++) Cx[a] = hsum8(Cx[a]);
-      for (int k = 0; k < 3; k++) {
-        const float w = fmaxf(hmin8f(pk[k]), 0.0f);
-        W += w;
-        for (int a = 0; a < 3; a++) Cx[a] += w * T[k][a];
-      }
-      float ul[3], pos[3];
-      mulmv3(ul, R, um);
-      if (W > 0.0f) {
-        const float iw = 1.0f / W;
-        for (int a = 0; a < 3; a++) pos[a] = Cx[a] * iw;
-      } else {
-        // crossing edges: the midpoint of the two shapes' support features along u
-        float hmu = 1e30f;
-#pragma unroll
-        for (int i = 0; i < VPL; i++)
-          if (vok[i]) hmu = fminf(hmu, dot3(ul, xl[i]));
-        hmu = hmin8f(hmu);
-        float wh_ = 0.0f, ch[3] = {0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int i = 0; i < VPL; i++) {
-          const float w = vok[i] ? fmaxf(0.0f, 1.0f - (dot3(ul, xl[i]) - hmu) * (1.0f / HF_WITNESS_BAND)) : 0.0f;
-          wh_ += w;
-          for (int a = 0; a < 3; a++) ch[a] += w * xl[i][a];
-        }
-        wh_ = hsum8(wh_);
-        for (int a = 0; a < 3; a++) ch[a] = hsum8(ch[a]);
-        const float q[3] = {dot3(ul, T[0]), dot3(ul, T[1]), dot3(ul, T[2])};
-        const float pmx = fmaxf(q[0], fmaxf(q[1], q[2]));
-        float wp_ = 0.0f, cq[3] = {0.0f, 0.0f, 0.0f};
-        for (int k = 0; k < 3; k++) {
-          const float w = fmaxf(0.0f, 1.0f - (pmx - q[k]) * (1.0f / HF_WITNESS_BAND));
-          wp_ += w;
-          for (int a = 0; a < 3; a++) cq[a] += w * T[k][a];
-        }
-        for (int a = 0; a < 3; a++) pos[a] = 0.5f * (ch[a] / wh_ + cq[a] / wp_);
-      }
-      // kept by lane pi & 7 in slot pi >> 3
-#pragma unroll
-      for (int s = 0; s < PPL; s++) {
-        const bool mine = sub == (pi & 7) && s == (pi >> 3);
-        cd[s] = mine ? mn : cd[s];
-        for (int a = 0; a < 3; a++) {
-          cn[s][a] = mine ? ul[a] : cn[s][a];
-          cx[s][a] = mine ? pos[a] : cx[s][a];
-        }
+      for (int hh = 0; hh < 8; hh++) {
+        const int c = ((act >> (8 * hh)) & 1ull) ? __builtin_amdgcn_readlane(cnt, 8 * hh) : 0;
+        g0 += hh < hw ? c : 0;
+        S += c;
       }
     }
-#ifdef DUCK_ASM_MARKS
-    asm volatile("; HF_LOOP_END" ::: "memory");
+    const int nact = __popcll(act), QRa = nact < HF_QR ? nact : HF_QR;
+#ifdef DUCK_STAGE_PROF
+    if (threadIdx.x == 0) STAGE_ADD(40, (unsigned long long)S);
 #endif
+    const int gi = __popcll(act & ((1ull << ((int)threadIdx.x & 63)) - 1ull));  // this lane among the active
+    auto qent = [&](int g) -> lds_float* { return L + ((g & 3) - tw) * TL::STRIDE + HF_QH0 + HF_ENT * (g >> 2); };
+    for (int r0 = 0; r0 < S; r0 += QRa) {
+#ifdef DUCK_STAGE_PROF
+      if (threadIdx.x == 0) STAGE_ADD(46, 1ull);
+#endif
+#pragma unroll
+      for (int j = 0; j < PPL; j++) {
+        const int q = sub + 8 * j;
+        const int g = g0 + __popc(surv & ((1u << q) - 1u)) - r0;
+        if (((surv >> q) & 1u) && g >= 0 && g < QRa) {
+          // the prism's top (local) as the screen had it, then the mesh frame
+          const int rr = q / (2 * ncx), rem = q - rr * 2 * ncx, cc = rem >> 1, tri = rem & 1;
+          const int dcs[2][3] = {{0, 0, 1}, {0, 1, 1}}, drs[2][3] = {{0, 1, 0}, {1, 0, 1}};
+          float T[3][3], nt[3], ntm[3], Tm[3][3];
+          for (int k = 0; k < 3; k++) {
+            T[k][0] = X0 + (float)(cc + (tri ? dcs[1][k] : dcs[0][k])) * DXC;
+            T[k][1] = Y0 + (float)(rr + (tri ? drs[1][k] : drs[0][k])) * DYC;
+            T[k][2] = szt[j][k];
+          }
+          top_normal(T, nt);
+          mulmtv3(ntm, R, nt);
+          for (int k = 0; k < 3; k++) mulmtv3(Tm[k], R, T[k]);
+          lds_f4* E4 = (lds_f4*)qent(g);
+          E4[0] = f4v{Tm[0][0], Tm[0][1], Tm[0][2], base};
+          E4[1] = f4v{Tm[1][0], Tm[1][1], Tm[1][2], smo[j]};
+          E4[2] = f4v{Tm[2][0], Tm[2][1], Tm[2][2], __int_as_float(smp[j])};
+          E4[3] = f4v{ntm[0], ntm[1], ntm[2], __int_as_float(tri | (2 * tw + h) << 1)};
+          E4[4] = f4v{zc[0], zc[1], zc[2], 0.0f};
+          E4[5] = f4v{R[0], R[1], R[2], 0.0f};
+          E4[6] = f4v{R[3], R[4], R[5], 0.0f};
+        }
+      }
+      TSYNC();
+      STAGE_MARK(41);
+#ifdef DUCK_ASM_MARKS
+      asm volatile("; HF_EXEC_BEGIN" ::: "memory");
+#endif
+      if (gi < QRa && r0 + gi < S) hf_exec(qent(gi), L, tw);
+#ifdef DUCK_ASM_MARKS
+      asm volatile("; HF_EXEC_END" ::: "memory");
+#endif
+      TSYNC();
+      STAGE_MARK(42);
+#pragma unroll
+      for (int j = 0; j < PPL; j++) {
+        const int q = sub + 8 * j;
+        const int g = g0 + __popc(surv & ((1u << q) - 1u)) - r0;
+        if (((surv >> q) & 1u) && g >= 0 && g < QRa) {
+          const lds_f4* O = (const lds_f4*)qent(g);
+          const f4v o0 = O[0], o1 = O[1];
+          const float um[3] = {o0.y, o0.z, o0.w}, pm[3] = {o1.x, o1.y, o1.z};
+          cd[j] = o0.x > 0.0f ? o0.x : -1.0f;
+          mulmv3(cn[j], R, um);
+          mulmv3(cx[j], R, pm);
+        }
+      }
+      TSYNC();
+      STAGE_MARK(43);
+    }
     STAGE_MARK(38);
     // 4 slots by mjx's _manifold_points over the prism contacts, from the deepest (the first prism
     // within HF_DEPTH_TIE of it: prisms sharing a grid vertex or edge often tie exactly); index

@@ -22,9 +22,8 @@ TOP = {0: "kinematics", 1: "com_pos", 2: "rne", 3: "crb", 28: "smooth (actuation
 SUB = {24: "kinematics:local", 21: "rne:A vel/acc", 22: "rne:A+B forces", 35: "rne:C limb sums", 36: "rne:C root sums", 19: "crb:inertia sums",
        26: "collision:floor", 25: "solve:warm J,M products", 9: "solve:warm costs+select", 10: "solve:newton_dir", 16: "  newton:grad+diag",
        17: "  newton:+J'DJ", 18: "  newton:+factor_solve", 11: "solve:(dense fallback)", 12: "solve:jmul+mulM",
-       13: "solve:linesearch", 37: "hfield: setup+screen", 38: "hfield: survivor SAT loop", 39: "hfield: slots",
-       41: "  prism: top/sides", 42: "  prism: hull faces", 43: "  prism: top-edge pairs", 44: "  prism: vertical pairs",
-       45: "  prism: axis reduction"}
+       13: "solve:linesearch", 37: "hfield: setup+screen+silhouettes", 38: "hfield: survivor queue", 39: "hfield: slots",
+       41: "  queue: descriptors", 42: "  queue: per-lane SAT", 43: "  queue: gather"}
 NSTAGE = 48  # DUCK_NSTAGE
 ENV = {32: "env: hot state load", 33: "env: rng draws", 29: "env: pre-physics (per env-step)", 30: "env: contacts+obs",
        31: "env: termination+rewards+state", 34: "env: obs/priv stores", 15: "env: hot state store"}
@@ -87,8 +86,8 @@ def main():
     print(f"{'dense Newton fallbacks':28s} {buf[23] / steps:10.1f} per env-step (all {n} envs)")
     print(f"{'foot/foot SAT runs':28s} {buf[27] / steps:10.1f} per env-step (all {n} envs)")
     if buf[40]:
-        print(f"{'hfield survivors':28s} {buf[40] / (nwg * steps * 10):10.2f} per substep (foot 0 of team 0)")
-        print(f"{'hfield loop iterations':28s} {buf[46] / (nwg * steps * 10):10.2f} per substep (wave 0: max over its 8 feet)")
+        print(f"{'hfield survivors':28s} {buf[40] / (nwg * steps * 10):10.2f} per substep (wave 0 of each workgroup: 8 feet)")
+        print(f"{'hfield queue rounds':28s} {buf[46] / (nwg * steps * 10):10.2f} per substep (wave 0)")
     outside = per(14) + sum(per(k) for k in ENV)
     kern = outside + tot / (nwg * steps)
     if per(14) == 0:
