@@ -287,9 +287,9 @@ def team_tables(m: Model, rows, adr, pre: str, floor: int):
         for e, (a, b) in enumerate(hull.edge):
             C_, D_ = -np.asarray(hull.face_normal[hef[e][0]]), -np.asarray(hull.face_normal[hef[e][1]])
             v0, v1 = np.asarray(hull.vert[a]), np.asarray(hull.vert[b])
-            for v in (C_, D_, np.cross(D_, C_), v1 - v0, v0):
-                rec += [f2i(x) for x in v] + [f2i(0.0)]
-        put("hedge", rec)  # stride 20: C, D, D x C, edge, v0 (each + pad)
+            for v, w in ((C_, 0.0), (D_, 0.0), (np.cross(D_, C_), 0.0), (v1 - v0, float(np.sum((v1 - v0) ** 2))), (v0, 0.0)):
+                rec += [f2i(x) for x in v] + [f2i(w)]
+        put("hedge", rec)  # stride 20: C, D, D x C, edge (+ |edge|^2), v0 (each padded to 16 B)
         put("hvert", [f2i(x) for v in np.asarray(hull.vert) for x in list(v) + [0.0]])  # stride 4
         boff["hend"] = len(blob)
     else:

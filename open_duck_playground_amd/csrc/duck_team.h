@@ -1404,6 +1404,7 @@ struct TPhys {
   // inside the other, or the midpoint of the support features). Writes (depth, normal, point)
   // over the entry's first 8 floats; depth -1 when separated.
   static DK void hf_exec(lds_float* E, LP L, int tw) {
+    STAGE_T0();
     constexpr int NH = Md::NHV, NF = Md::NHF, NE = Md::NHE;
     constexpr int NPW = (3 * NE + 63) / 64;
     static_assert(NPW <= 3, "top-edge pair masks");
@@ -1447,6 +1448,7 @@ struct TPhys {
         take(fmaxf(q0, fmaxf(q1, q2)) - w.w, HF_PRIO_V + 3 * e + kk, wv);
       }
     }
+    STAGE_MARK(44);
     // top-edge pairs (hull edge e, prism top edge k: faces ntm, sm_k). Pass 1: the arcs cross when
     // CBA DBA < 0, ADC BDC < 0 and CBA BDC > 0 (C = -n_a, D = -n_b, B x A = sm_k x ntm: CBA =
     // -phi_a), all three products negative: the sign bit of their maximum, bit 3 e + k of pm
@@ -1470,6 +1472,7 @@ struct TPhys {
         });
       }
     }
+    STAGE_MARK(45);
     // pass 2: each crossing pair's overlap along ev x em (lowest pair first)
     while (pm[0] | pm[1] | pm[2]) {
       const bool z0 = pm[0] == 0ull, z1 = pm[1] == 0ull;
@@ -1492,12 +1495,13 @@ struct TPhys {
       float u[3];
       cross3(u, ev, em);
       const float u2 = dot3(u, u);
-      if (u2 >= 1e-12f * dot3(ev, ev) * dot3(em, em)) {
-        const float sg = (dot3(u, ntm) + dot3(u, sk) < 0.0f ? -1.0f : 1.0f) * __builtin_amdgcn_rsqf(u2);
-        const float un[3] = {sg * u[0], sg * u[1], sg * u[2]};
-        take(sg * (dot3(u, tm) - dot3(u, v0)), HF_PRIO_T + p, un);
-      }
+      const float sg = (dot3(u, ntm) + dot3(u, sk) < 0.0f ? -1.0f : 1.0f) * __builtin_amdgcn_rsqf(u2);
+      const float un[3] = {sg * u[0], sg * u[1], sg * u[2]};
+      // (a degenerate pair, ev parallel to em, gives no axis; ev4.w = |ev|^2)
+      const float ov = u2 >= 1e-12f * ev4.w * dot3(em, em) ? sg * (dot3(u, tm) - dot3(u, v0)) : 1e30f;
+      take(ov, HF_PRIO_T + p, un);
     }
+    STAGE_MARK(47);
     if (!(mo > 0.0f)) {
       E4[0] = f4v{-1.0f, 0.0f, 0.0f, 0.0f};
       return;
@@ -1694,6 +1698,11 @@ struct TPhys {
 #pragma unroll
     for (int j = 0; j < PPL; j++) {
       const int q = sub + 8 * j;
+      smo[j] = 0.0f;
+      smp[j] = 0;
+      for (int k = 0; k < 3; k++) szt[j][k] = 0.0f;
+      // (a wave-uniform skip of the slots no foot of the wave has: most sub-grids hold <= 12 prisms)
+      if (j > 0 && __ballot(q < np) == 0ull) continue;
       float T[3][3], nt[3];
       int tri;
       prism_top(q < np ? q : 0, T, tri);
@@ -1808,7 +1817,9 @@ struct TPhys {
       for (int j = 0; j < PPL; j++) {
         const int q = sub + 8 * j;
         const int g = g0 + __popc(surv & ((1u << q) - 1u)) - r0;
-        if (((surv >> q) & 1u) && g >= 0 && g < QRa) {
+        const bool mine = ((surv >> q) & 1u) && g >= 0 && g < QRa;
+        if (__ballot(mine) == 0ull) continue;
+        if (mine) {
           // the prism's top (local) as the screen had it, then the mesh frame
           const int rr = q / (2 * ncx), rem = q - rr * 2 * ncx, cc = rem >> 1, tri = rem & 1;
           const int dcs[2][3] = {{0, 0, 1}, {0, 1, 1}}, drs[2][3] = {{0, 1, 0}, {1, 0, 1}};
@@ -1846,7 +1857,9 @@ struct TPhys {
       for (int j = 0; j < PPL; j++) {
         const int q = sub + 8 * j;
         const int g = g0 + __popc(surv & ((1u << q) - 1u)) - r0;
-        if (((surv >> q) & 1u) && g >= 0 && g < QRa) {
+        const bool mine = ((surv >> q) & 1u) && g >= 0 && g < QRa;
+        if (__ballot(mine) == 0ull) continue;
+        if (mine) {
           const lds_f4* O = (const lds_f4*)qent(g);
           const f4v o0 = O[0], o1 = O[1];
           const float um[3] = {o0.y, o0.z, o0.w}, pm[3] = {o1.x, o1.y, o1.z};

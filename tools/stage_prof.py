@@ -23,7 +23,8 @@ SUB = {24: "kinematics:local", 21: "rne:A vel/acc", 22: "rne:A+B forces", 35: "r
        26: "collision:floor", 25: "solve:warm J,M products", 9: "solve:warm costs+select", 10: "solve:newton_dir", 16: "  newton:grad+diag",
        17: "  newton:+J'DJ", 18: "  newton:+factor_solve", 11: "solve:(dense fallback)", 12: "solve:jmul+mulM",
        13: "solve:linesearch", 37: "hfield: setup+screen+silhouettes", 38: "hfield: survivor queue", 39: "hfield: slots",
-       41: "  queue: descriptors", 42: "  queue: per-lane SAT", 43: "  queue: gather"}
+       41: "  queue: descriptors", 42: "  queue: per-lane SAT", 43: "  queue: gather",
+       44: "    sat: vertical pairs", 45: "    sat: pass 1 (arc tests)", 47: "    sat: pass 2 (crossing pairs)"}
 NSTAGE = 48  # DUCK_NSTAGE
 ENV = {32: "env: hot state load", 33: "env: rng draws", 29: "env: pre-physics (per env-step)", 30: "env: contacts+obs",
        31: "env: termination+rewards+state", 34: "env: obs/priv stores", 15: "env: hot state store"}
