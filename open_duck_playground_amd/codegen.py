@@ -519,13 +519,22 @@ def model_header(m: Model, variant: str) -> str:
     else:
         hf_cells = (1, 1)
     pre = f"DuckModel_{variant}"
-    dev = [f"__device__ const float {pre}_hull_vert_d[{len(hull.vert)}][3] = {_arr('x', hull.vert, 'float').split('= ', 1)[1]}",
+    maxfv = max(len(f) for f in hull.face_vert)
+    fvert = np.full((len(hull.face_vert), maxfv), -1, dtype=np.int64)
+    for j, f in enumerate(hull.face_vert):
+        fvert[j, :len(f)] = f
+    dev = [f"__device__ const int {pre}_hull_face_vert_d[{len(hull.face_vert)}][{maxfv}] = {_arr('x', fvert, 'int').split('= ', 1)[1]}",
+           f"__device__ const int {pre}_hull_face_nv_d[{len(hull.face_vert)}] = {_arr('x', [len(f) for f in hull.face_vert], 'int').split('= ', 1)[1]}",
+f"__device__ const float {pre}_hull_vert_d[{len(hull.vert)}][3] = {_arr('x', hull.vert, 'float').split('= ', 1)[1]}",
            f"__device__ const float {pre}_hull_face_normal_d[{len(hull.face_normal)}][3] = {_arr('x', hull.face_normal, 'float').split('= ', 1)[1]}",
            f"__device__ const float {pre}_hull_face_offset_d[{len(hull.face_offset)}] = {_arr('x', hull.face_offset, 'float').split('= ', 1)[1]}",
            f"__device__ const int {pre}_hull_edge_d[{len(hull.edge)}][2] = {_arr('x', hull.edge, 'int').split('= ', 1)[1]}",
            f"__device__ const int {pre}_hull_edge_face_d[{len(hef)}][2] = {_arr('x', hef, 'int').split('= ', 1)[1]}",
            f"__device__ const int {pre}_chain_d[{nb}][{maxchain}] = {_arr('x', chain_arr, 'int').split('= ', 1)[1]}"]
-    acc = [f"  static __device__ __forceinline__ const float (*hull_vert_d())[3] {{ return {pre}_hull_vert_d; }}\n",
+    acc = [f"  static constexpr int HULL_MAXFV = {maxfv};  // most vertices of a hull face polygon\n",
+           f"  static __device__ __forceinline__ const int (*hull_face_vert_d())[{maxfv}] {{ return {pre}_hull_face_vert_d; }}\n",
+           f"  static __device__ __forceinline__ const int* hull_face_nv_d() {{ return {pre}_hull_face_nv_d; }}\n",
+           f"  static __device__ __forceinline__ const float (*hull_vert_d())[3] {{ return {pre}_hull_vert_d; }}\n",
            f"  static __device__ __forceinline__ const float (*hull_face_normal_d())[3] {{ return {pre}_hull_face_normal_d; }}\n",
            f"  static __device__ __forceinline__ const float* hull_face_offset_d() {{ return {pre}_hull_face_offset_d; }}\n",
            f"  static __device__ __forceinline__ const int (*hull_edge_d())[2] {{ return {pre}_hull_edge_d; }}\n",

@@ -1475,6 +1475,9 @@ struct TPhys {
     STAGE_MARK(45);
     // pass 2: each crossing pair's overlap along ev x em (lowest pair first)
     while (pm[0] | pm[1] | pm[2]) {
+#ifdef DUCK_STAGE_PROF
+      if (threadIdx.x < 64 && (int)threadIdx.x == __ffsll((long long)__ballot(1)) - 1) STAGE_ADD(48, 1ull);
+#endif
       const bool z0 = pm[0] == 0ull, z1 = pm[1] == 0ull;
       const unsigned long long w = z0 ? (z1 ? pm[2] : pm[1]) : pm[0];
       const int p = (z0 ? (z1 ? 128 : 64) : 0) + __builtin_ctzll(w);
@@ -2039,7 +2042,7 @@ struct TPhys {
   }
 
   // Hull/hull (foot/foot) SAT with the team: mjx / oracle collide_convex_convex semantics, the
-  // axes split over the lanes. Face axes (both hulls, 60) then edge-pair axes (45 x 45); a
+  // axes split over the lanes, then mjx's clipped face manifold or the edge pair's closest points. Face axes (both hulls, 60) then edge-pair axes (45 x 45); a
   // separating axis anywhere means no contact (the 4 slots stay inactive); otherwise the best
   // face (largest separation, first index among equal ones) unless the best edge pair beats it
   // by 1e-9 (declared deviation: the single-lane scan applies that margin per step, here it is
@@ -2218,34 +2221,95 @@ struct TPhys {
       if (lane == 0) P1::store_contact(Ls, slot0, best, pos, fr);
       return;
     }
-    const float* Rr = btype == 0 ? R1 : R2;
-    const float* pr = btype == 0 ? p1 : p2;
+    // face contact, mjx's clipped manifold (oracle collide_convex_convex): the incident face (the
+    // other hull's face most anti-parallel to the reference normal, the first among equal ones)
+    // clipped by the reference face's side planes (Sutherland-Hodgman in the reference polygon's
+    // order; every lane runs the same clip through the dead edge scratch), the clipped points below
+    // the reference plane, 4 of them by _manifold_points, each midway to the reference plane
+    const bool ref1 = btype == 0;
+    const float* Rr = ref1 ? R1 : R2;
+    const float* Ri = ref1 ? R2 : R1;
+    const float* pr = ref1 ? p1 : p2;
     float fn[3];
     mulmv3(fn, Rr, HN[bi]);
     const float off = Md::hull_face_offset_d()[bi] + dot3(fn, pr);
-    float support[NH];
-    bool mask[NH];
-    float smax = -1e30f;
-#pragma unroll
-    for (int k = 0; k < NH; k++) {
-      const float* v = btype == 0 ? V2[k] : V1[k];
-      support[k] = off - dot3(fn, v);
-      smax = fmaxf(smax, support[k]);
+    int finc = 0;
+    float dmin = 1e30f;
+    for (int f = 0; f < NF; f++) {
+      float ni[3];
+      mulmv3(ni, Ri, HN[f]);
+      const float dd = dot3(ni, fn);
+      finc = dd < dmin ? f : finc;
+      dmin = fminf(dmin, dd);
     }
-    const float thr = fmaxf(smax - 1e-3f, 0.0f);
+    constexpr int MFV = Md::HULL_MAXFV, CLIPMAX = 2 * MFV;
+    constexpr int PA = EA, PB = EA + 3 * CLIPMAX;
+    static_assert(PB + 3 * CLIPMAX <= FA, "clip scratch must fit in the edge storage");
+    const int(*FV)[MFV] = Md::hull_face_vert_d();
+    const int* FNV = Md::hull_face_nv_d();
+    auto vtx = [&](bool h1, int k, float* out) {
+      float o1[3], o2[3];
+      pick3<NH>(V1, k, o1);
+      pick3<NH>(V2, k, o2);
+      for (int q = 0; q < 3; q++) out[q] = h1 ? o1[q] : o2[q];
+    };
+    int np = FNV[finc];
+    for (int i = 0; i < np; i++) {
+      float v[3];
+      vtx(!ref1, FV[finc][i], v);
+      for (int q = 0; q < 3; q++) L[PA + 3 * i + q] = v[q];
+    }
+    int src = PA, dst = PB;
+    const int nr = FNV[bi];
+    for (int i = 0; i < nr && np > 0; i++) {
+      float a[3], b[3], ab[3], sd[3];
+      vtx(ref1, FV[bi][i], a);
+      vtx(ref1, FV[bi][i + 1 < nr ? i + 1 : 0], b);
+      for (int q = 0; q < 3; q++) ab[q] = b[q] - a[q];
+      cross3(sd, ab, fn);  // outward side normal of the reference polygon's edge a -> b
+      int nt = 0;
+      for (int j = 0; j < np; j++) {
+        const int jn = j + 1 < np ? j + 1 : 0;
+        const float P[3] = {L[src + 3 * j], L[src + 3 * j + 1], L[src + 3 * j + 2]};
+        const float Q[3] = {L[src + 3 * jn], L[src + 3 * jn + 1], L[src + 3 * jn + 2]};
+        const float dp = sd[0] * (P[0] - a[0]) + sd[1] * (P[1] - a[1]) + sd[2] * (P[2] - a[2]);
+        const float dq = sd[0] * (Q[0] - a[0]) + sd[1] * (Q[1] - a[1]) + sd[2] * (Q[2] - a[2]);
+        if (dp <= 0.0f && nt < CLIPMAX) {
+          for (int q = 0; q < 3; q++) L[dst + 3 * nt + q] = P[q];
+          nt++;
+        }
+        if ((dp <= 0.0f) != (dq <= 0.0f) && nt < CLIPMAX) {
+          const float tt = dp / (dp - dq);
+          for (int q = 0; q < 3; q++) L[dst + 3 * nt + q] = P[q] + tt * (Q[q] - P[q]);
+          nt++;
+        }
+      }
+      TSYNC();
+      np = nt;
+      const int sw = src;
+      src = dst;
+      dst = sw;
+    }
+    float poly[CLIPMAX][3], depth[CLIPMAX];
+    bool mask[CLIPMAX], any = false;
 #pragma unroll
-    for (int k = 0; k < NH; k++) mask[k] = support[k] > thr;
+    for (int k = 0; k < CLIPMAX; k++) {
+      const bool ok = k < np;
+      for (int q = 0; q < 3; q++) poly[k][q] = ok ? L[src + 3 * k + q] : 0.0f;
+      depth[k] = off - dot3(fn, poly[k]);
+      mask[k] = ok && depth[k] > 0.0f;
+      any = any || mask[k];
+    }
+    if (!any) return;
     int idx[4];
-    if (btype == 0) manifold_points<NH>(V2, mask, fn, idx);
-    else manifold_points<NH>(V1, mask, fn, idx);
+    manifold_points<CLIPMAX>(poly, mask, fn, idx);
     if (lane < 4) {
       const int c = lane;
       bool unique = true;
       for (int e = 0; e < 4; e++) unique = unique && !(e < c && idx[e] == idx[c]);
-      const float dist = unique ? -pick1<NH>(support, idx[c]) : 1.0f;
+      const float dist = unique ? -pick1<CLIPMAX>(depth, idx[c]) : 1.0f;
       float v[3], pos[3];
-      if (btype == 0) pick3<NH>(V2, idx[c], v);
-      else pick3<NH>(V1, idx[c], v);
+      pick3<CLIPMAX>(poly, idx[c], v);
       for (int a = 0; a < 3; a++) pos[a] = v[a] - 0.5f * dist * fn[a];
       P1::store_contact(Ls, slot0 + c, dist, pos, fr);
     }

@@ -48,6 +48,7 @@ struct oracle_model {
   double hull_vert[DUCK_MAXHULLV][3], hull_face_normal[DUCK_MAXHULLF][3], hull_face_offset[DUCK_MAXHULLF];
   int hull_edge[DUCK_MAXHULLE][2];
   int hull_edge_face[DUCK_MAXHULLE][2]; /* the two faces whose planes hold the edge */
+  int hull_face_nv[DUCK_MAXHULLF], hull_face_vert[DUCK_MAXHULLF][DUCK_MAXHULLV]; /* face polygons (CCW) */
   double hull_center[3], hull_radius;
   int hfield_nrow, hfield_ncol;
   double hfield_size[4];
@@ -152,6 +153,40 @@ oracle_model* oracle_model_create(const duck_model_desc* s) {
       }
     }
     if (n != 2) { free(m); return NULL; }
+  }
+  /* face polygons: the vertices on the face plane, counter-clockwise about the outward normal,
+   * ordered as mjcf.convex_hull orders them (angle from the lowest-index vertex about the
+   * centroid, atan2 ascending), so that codegen's hull_face_vert table and this agree */
+  for (int f = 0; f < s->hull_nface; f++) {
+    const double* fnm = m->hull_face_normal[f];
+    int nfv = 0, vid[DUCK_MAXHULLV];
+    double cf[3] = {0, 0, 0};
+    for (int k = 0; k < s->hull_nvert; k++) {
+      const double* v = m->hull_vert[k];
+      if (fabs(fnm[0] * v[0] + fnm[1] * v[1] + fnm[2] * v[2] - m->hull_face_offset[f]) < 1e-7) {
+        vid[nfv++] = k;
+        for (int a = 0; a < 3; a++) cf[a] += v[a];
+      }
+    }
+    if (nfv < 3) { free(m); return NULL; }
+    for (int a = 0; a < 3; a++) cf[a] /= nfv;
+    double u[3], w[3], ang[DUCK_MAXHULLV];
+    for (int a = 0; a < 3; a++) u[a] = m->hull_vert[vid[0]][a] - cf[a];
+    const double un = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    for (int a = 0; a < 3; a++) u[a] /= un;
+    w[0] = fnm[1] * u[2] - fnm[2] * u[1]; w[1] = fnm[2] * u[0] - fnm[0] * u[2]; w[2] = fnm[0] * u[1] - fnm[1] * u[0];
+    for (int i = 0; i < nfv; i++) {
+      const double* v = m->hull_vert[vid[i]];
+      const double d[3] = {v[0] - cf[0], v[1] - cf[1], v[2] - cf[2]};
+      ang[i] = atan2(d[0] * w[0] + d[1] * w[1] + d[2] * w[2], d[0] * u[0] + d[1] * u[1] + d[2] * u[2]);
+    }
+    for (int i = 1; i < nfv; i++) /* insertion sort by angle (stable) */
+      for (int j = i; j > 0 && ang[j - 1] > ang[j]; j--) {
+        const double ta = ang[j]; ang[j] = ang[j - 1]; ang[j - 1] = ta;
+        const int tv = vid[j]; vid[j] = vid[j - 1]; vid[j - 1] = tv;
+      }
+    m->hull_face_nv[f] = nfv;
+    for (int i = 0; i < nfv; i++) m->hull_face_vert[f][i] = vid[i];
   }
   m->hfield_nrow = s->hfield_nrow; m->hfield_ncol = s->hfield_ncol; CP(m->hfield_size, s->hfield_size, 4);
   if (s->hfield_nrow > 0) {
@@ -1023,8 +1058,8 @@ int oracle_hfield_prisms(const oracle_model* m, const oracle_data* d, int g_hf, 
 }
 
 /* convex hull (g1) vs convex hull (g2): separating-axis test over face normals and edge
- * pairs; on overlap, a 4-point manifold against the reference face (or one edge-edge
- * point). Declared simplification of mjx's convex-convex clipping. */
+ * pairs; on overlap, mjx's clipped 4-point manifold on the reference face, or one edge-edge
+ * point (mjx collision_convex: SAT over the Gauss map, then _clip + _manifold_points). */
 static void collide_convex_convex(const oracle_model* m, oracle_data* d, int g1, int g2, int slot0) {
   for (int c = 0; c < 4; c++) set_inactive(d, slot0 + c, g1, g2);
   const double *p1 = d->geom_xpos[g1], *R1 = d->geom_xmat[g1], *p2 = d->geom_xpos[g2], *R2 = d->geom_xmat[g2];
@@ -1127,29 +1162,70 @@ static void collide_convex_convex(const oracle_model* m, oracle_data* d, int g1,
     memcpy(d->con_frame[slot0], fr, sizeof(fr));
     return;
   }
-  /* face contact: vertices of the incident hull past the reference face plane */
-  double (*Vi)[3] = btype == 0 ? V2 : V1;
+  /* face contact, mjx's clipped manifold: the incident face (the other hull's face most
+   * anti-parallel to the reference face's normal; the first among equal ones) clipped by the
+   * reference face's side planes (Sutherland-Hodgman, planes in the reference polygon's order),
+   * the clipped points below the reference plane, 4 of them by _manifold_points. Each contact
+   * sits midway between its point and the reference plane. */
+  const int inc_hull = btype == 0 ? 1 : 0;
+  double (*Vi)[3] = inc_hull == 1 ? V2 : V1;
+  double (*Vr)[3] = inc_hull == 1 ? V1 : V2;
   const double* Rr = btype == 0 ? R1 : R2;
+  const double* Ri = btype == 0 ? R2 : R1;
   const double* pr = btype == 0 ? p1 : p2;
   double fn[3], off;
   mulmv3(fn, Rr, m->hull_face_normal[bi]);
   off = m->hull_face_offset[bi] + dot3(fn, pr);  /* world plane: fn . x = off (fn outward of ref hull) */
-  double support[DUCK_MAXHULLV], smax = -1e30;
-  for (int k = 0; k < nv; k++) {
-    support[k] = off - dot3(fn, Vi[k]);  /* depth of incident vertex inside the reference face */
-    if (support[k] > smax) smax = support[k];
+  int finc = 0;
+  double dmin = 1e300;
+  for (int f = 0; f < nf; f++) {
+    double ni[3];
+    mulmv3(ni, Ri, m->hull_face_normal[f]);
+    const double dd = dot3(ni, fn);
+    if (dd < dmin) { dmin = dd; finc = f; }
   }
-  double thr = smax - 1e-3 > 0 ? smax - 1e-3 : 0;
-  int mask[DUCK_MAXHULLV], idx[4];
-  for (int k = 0; k < nv; k++) mask[k] = support[k] > thr;
-  manifold_points((const double(*)[3])Vi, mask, nv, fn, idx);
+  enum { CLIPMAX = 2 * DUCK_MAXHULLV };
+  double poly[CLIPMAX][3], tmpp[CLIPMAX][3];
+  int np = m->hull_face_nv[finc];
+  for (int i = 0; i < np; i++) memcpy(poly[i], Vi[m->hull_face_vert[finc][i]], sizeof(double) * 3);
+  const int nr = m->hull_face_nv[bi];
+  for (int i = 0; i < nr && np > 0; i++) {
+    const double *a = Vr[m->hull_face_vert[bi][i]], *b = Vr[m->hull_face_vert[bi][(i + 1) % nr]];
+    double ab[3], sd[3];
+    for (int q = 0; q < 3; q++) ab[q] = b[q] - a[q];
+    cross3(sd, ab, fn); /* outward side normal of the reference polygon's edge a -> b */
+    int nt = 0;
+    for (int j = 0; j < np; j++) {
+      const double *P = poly[j], *Q = poly[(j + 1) % np];
+      const double dp = sd[0] * (P[0] - a[0]) + sd[1] * (P[1] - a[1]) + sd[2] * (P[2] - a[2]);
+      const double dq = sd[0] * (Q[0] - a[0]) + sd[1] * (Q[1] - a[1]) + sd[2] * (Q[2] - a[2]);
+      if (dp <= 0) memcpy(tmpp[nt++], P, sizeof(double) * 3);
+      if ((dp <= 0) != (dq <= 0)) {
+        const double tt = dp / (dp - dq);
+        for (int q = 0; q < 3; q++) tmpp[nt][q] = P[q] + tt * (Q[q] - P[q]);
+        nt++;
+      }
+      if (nt > CLIPMAX - 2) abort(); /* fixed capacity: a convex clip never grows past np + nr */
+    }
+    np = nt;
+    memcpy(poly, tmpp, sizeof(double) * 3 * (size_t)nt);
+  }
+  double depth[CLIPMAX];
+  int mask[CLIPMAX], idx[4], any = 0;
+  for (int k = 0; k < np; k++) {
+    depth[k] = off - dot3(fn, poly[k]);
+    mask[k] = depth[k] > 0;
+    any |= mask[k];
+  }
+  if (!any) return;
+  manifold_points((const double(*)[3])poly, mask, np, fn, idx);
   for (int c = 0; c < 4; c++) {
     int k = idx[c], unique = 1;
     for (int e = 0; e < c; e++)
       if (idx[e] == k) unique = 0;
-    double dist = unique ? -support[k] : 1.0;
+    double dist = unique ? -depth[k] : 1.0;
     int s = slot0 + c;
-    for (int a = 0; a < 3; a++) d->con_pos[s][a] = Vi[k][a] - 0.5 * dist * fn[a];
+    for (int a = 0; a < 3; a++) d->con_pos[s][a] = poly[k][a] - 0.5 * dist * fn[a];
     d->con_dist[s] = dist;
     memcpy(d->con_frame[s], fr, sizeof(fr));
   }

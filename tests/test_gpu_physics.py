@@ -143,9 +143,9 @@ def test_flight_obeys_newton_euler(task, gpu):
 
 def test_foot_foot_contacts_match_oracle(gpu):
     """Foot/foot (hull/hull) contacts at 4096 robots in flight (flight_states seed 7: feet touch
-    in a few dozen): the HIP path (bounding sphere, then box/box SAT prefilter, then the hull SAT)
-    reports the same active contacts as the oracle's hull SAT, at the same point, and the dense
-    Newton direction those rows need gives the oracle's qacc."""
+    in a few dozen): the HIP path (bounding sphere, then box/box SAT prefilter, then the hull SAT
+    and mjx's clipped face manifold) reports the same active contacts as the oracle's, at the same
+    points (all 4 slots), and the dense Newton direction those rows need gives the oracle's qacc."""
     from tests.physics_laws import flight_states
     n = 4096
     env = Joystick("flat_terrain", num_envs=1, device=gpu, use_imitation=False)
@@ -166,7 +166,7 @@ def test_foot_foot_contacts_match_oracle(gpu):
         om.forward(d)
         r.append(d.arr("con_dist", 4 * m.npair)[:4].copy())
         rq.append(d.arr("qacc", m.nv).copy())
-        rp.append(np.array(d.arr("con_pos", 4 * m.npair)[0]))
+        rp.append(np.array(d.arr("con_pos", 4 * m.npair)[:4]).reshape(-1))
     r, rq, rp = np.array(r), np.array(rq), np.array(rp)
     act_r, act_g = (r < 0).any(axis=1), (g < 0).any(axis=1)
     assert act_r.sum() >= 10
@@ -174,9 +174,11 @@ def test_foot_foot_contacts_match_oracle(gpu):
     both = act_r & act_g
     np.testing.assert_allclose(np.where(r[both] < 0, r[both], 0), np.where(g[both] < 0, g[both], 0), atol=1e-5)
     # the Newton step with the foot/foot rows active (dense H: the pair's rows couple the legs);
-    # same contact axis and point as the oracle (tie-tolerant SAT, Minkowski-face edge pairs)
+    # same contact axis and points as the oracle (tie-tolerant SAT, Minkowski-face edge pairs,
+    # mjx's clipped face manifold: every active slot)
     rel = np.abs(ga["qacc"] - rq).max(axis=1) / (1 + np.abs(rq).max(axis=1))
-    np.testing.assert_allclose(ga["con_pos"][both, :3], rp[both], atol=2e-5)
+    slot_act = np.repeat(r[both] < 0, 3, axis=1)
+    np.testing.assert_allclose(np.where(slot_act, ga["con_pos"][both, :12], 0), np.where(slot_act, rp[both], 0), atol=2e-5)
     assert rel[both].max() < 1e-3, np.sort(rel[both])[-5:]
     assert np.median(rel[~both]) < 1e-5
 

@@ -246,3 +246,47 @@ def test_hfield_contacts_match_brute_force_prisms():
     w = r["axis_wins"]
     assert w["bottom_edge"] == 0 and w["bottom"] == 0, w
     assert all(w[k] > 0 for k in ("top", "side", "hull_face", "top_edge", "vertical_edge")), w
+
+
+def test_oracle_hull_hull_clipped_manifold():
+    """Foot/foot contacts (oracle collide_convex_convex, mjx's clipped face manifold) of robots in
+    flight whose feet touch (physics_laws.flight_states seed 7, the states of the GPU foot/foot
+    test): 1-4 distinct points per touching pair, each the midpoint between a point of the incident
+    face (on one foot hull's surface) and its projection on the reference plane, no deeper than
+    the SAT penetration, all on the plane of the contact normal's face."""
+    from tests.physics_laws import flight_states
+    m = Model.load(constants.task_to_xml("flat_terrain"))
+    om = OracleModel(m)
+    hull = m.hulls[0]
+    feet = [m.id("geom", g) for g in constants.FEET_GEOMS]
+    p = [k for k in range(m.npair) if {int(m.pair_geom1[k]), int(m.pair_geom2[k])} == set(feet)][0]
+    qpos, qvel, ctrl = flight_states(m, 4096, seed=7)
+    touching = 0
+    for e in range(len(qpos)):
+        d = om.new_data(qpos=qpos[e], qvel=qvel[e], ctrl=ctrl[e])
+        om.forward(d)
+        dist = d.arr("con_dist", 4 * m.npair)[4 * p:4 * p + 4]
+        if not (dist < 0).any():
+            continue
+        touching += 1
+        pos = np.ctypeslib.as_array(d.con_pos)[4 * p:4 * p + 4]
+        fr = np.ctypeslib.as_array(d.con_frame)[4 * p:4 * p + 4]
+        act = dist < 0
+        assert 1 <= act.sum() <= 4
+        pts = pos[act]
+        assert len(np.unique(np.round(pts, 12), axis=0)) == act.sum()
+        n = fr[act][0][:3]
+        assert np.allclose(fr[act][:, :3], n)
+        gx = np.ctypeslib.as_array(d.geom_xpos)
+        gm = np.ctypeslib.as_array(d.geom_xmat)
+        for k in np.nonzero(act)[0]:
+            q = pos[k] + 0.5 * dist[k] * n  # the clipped point on the incident face
+            on = []
+            for g in feet:
+                R = gm[g].reshape(3, 3)
+                v = R.T @ (q - gx[g])  # mesh frame
+                on.append(np.max(hull.face_normal @ v - hull.face_offset))
+            assert min(abs(x) for x in on) < 1e-9, on  # on one foot's surface
+        # no point deeper than the SAT penetration (the deepest incident vertex along n)
+        assert -dist[act].min() <= -dist.min() + 1e-12
+    assert touching >= 10

@@ -25,7 +25,7 @@ SUB = {24: "kinematics:local", 21: "rne:A vel/acc", 22: "rne:A+B forces", 35: "r
        13: "solve:linesearch", 37: "hfield: setup+screen+silhouettes", 38: "hfield: survivor queue", 39: "hfield: slots",
        41: "  queue: descriptors", 42: "  queue: per-lane SAT", 43: "  queue: gather",
        44: "    sat: vertical pairs", 45: "    sat: pass 1 (arc tests)", 47: "    sat: pass 2 (crossing pairs)"}
-NSTAGE = 48  # DUCK_NSTAGE
+NSTAGE = 56  # DUCK_NSTAGE
 ENV = {32: "env: hot state load", 33: "env: rng draws", 29: "env: pre-physics (per env-step)", 30: "env: contacts+obs",
        31: "env: termination+rewards+state", 34: "env: obs/priv stores", 15: "env: hot state store"}
 
@@ -89,6 +89,7 @@ def main():
     if buf[40]:
         print(f"{'hfield survivors':28s} {buf[40] / (nwg * steps * 10):10.2f} per substep (wave 0 of each workgroup: 8 feet)")
         print(f"{'hfield queue rounds':28s} {buf[46] / (nwg * steps * 10):10.2f} per substep (wave 0)")
+        print(f"{'hfield pass-2 iterations':28s} {buf[48] / (nwg * steps * 10):10.2f} per substep (wave 0: the most crossing pairs of a lane)")
     outside = per(14) + sum(per(k) for k in ENV)
     kern = outside + tot / (nwg * steps)
     if per(14) == 0:
