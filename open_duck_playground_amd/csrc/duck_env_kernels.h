@@ -561,7 +561,7 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
     F[Lo.swing_peak + k] = fmaxf(F[Lo.swing_peak + k], L[Ly::FOOTZ + k]);
   }
   if constexpr (STAGE_OBS) {
-    static_assert(DUCK_OBS_SIZE(NU) + 15 + 3 * NU + 1 + 2 + 6 + 2 + 40 + 1 + 2 <= Md::NM + 4 * Ly::NROW,
+    static_assert(DUCK_OBS_SIZE(NU) + 15 + 3 * NU + 1 + 2 + 6 + 2 + 40 + 1 + 2 <= Ly::SCR_OBS && Ly::SCR_OBS <= Ly::HSZ + 4 * Ly::NROW,
                   "privileged row must fit in the H/row storage");
     write_obs_team<Md>(A, lane, L, F, SObs<SW>{L, Ly::H}, r, imitation_i);
     TSYNC();

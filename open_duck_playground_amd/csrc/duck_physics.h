@@ -89,15 +89,23 @@ struct Lay {
   // M, then one word kept at zero (crb writes it with M): the register column
   // loads of M read it for the entries outside the tree pattern (codegen mcolz table)
   static constexpr int M = CDD1 + 18, MZERO = M + Md::NM, H = MZERO + 1;
+  // H: scratch in front of the constraint rows, dead outside the stage that uses it together with
+  // the rows (the Newton Hessian itself is assembled in registers, never stored). Its users, each
+  // from H on: the tree passes' scratch (rne: 12 NB + 6 NV), the hull/hull SAT's edge tables (6 per
+  // hull edge and face), the height-field survivor queue (16 entries of 28 per env slice + 16-B
+  // alignment), the staged privileged observation row (env code, 86 + 9 NU). H is sized so that
+  // H + rows covers the largest of them: the rows alone cover most, so H is short (the backlash
+  // scenes' slices then leave LDS for the model blob: TLay::TAB_LDS).
+  static constexpr int SCR_TREE = 12 * NB + 6 * NV, SCR_SAT = 6 * (Md::NHE + Md::NHF);
+  static constexpr int SCR_HF = Md::FLOOR_TYPE == 1 ? 3 + 28 * 16 : 0, SCR_OBS = 86 + 9 * NU;
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  static constexpr int SCR_NEED = cmax(cmax(SCR_TREE, SCR_SAT), cmax(SCR_HF, SCR_OBS));
+  static constexpr int NROWS = NROW;
+  static constexpr int HSZ = ((cmax(SCR_NEED - 4 * NROWS - Md::NLIM, 0) + 3) / 4) * 4;
   // RNE accumulators live in the H + row storage (dead until smooth()/make_rows())
   static constexpr int CACC = H, CFRC = CACC + 6 * NB;
-  static_assert(12 * NB <= Md::NM + 4 * NROW, "RNE scratch must fit in H + rows");
-  // constraint rows, NROWS apart: the rows, or more when the hull/hull SAT scratch that reuses the
-  // H + row storage (6 floats per hull edge and face) needs it (a model without dof friction rows)
-  static constexpr int SAT_SCRATCH = 6 * (Md::NHE + Md::NHF);
-  static constexpr int NROWS =
-      (Md::NM + 4 * NROW + Md::NLIM >= SAT_SCRATCH) ? NROW : (SAT_SCRATCH - Md::NM - Md::NLIM + 3) / 4;
-  static constexpr int JA = H + Md::NM, JV = JA + NROWS, RD = JV + NROWS, AREF = RD + NROWS;
+  static_assert(12 * NB <= HSZ + 4 * NROW, "RNE scratch must fit in H + rows");
+  static constexpr int JA = H + HSZ, JV = JA + NROWS, RD = JV + NROWS, AREF = RD + NROWS;
   static constexpr int LSGN = AREF + NROWS;
   static constexpr int CR = LSGN + Md::NLIM, CFR = CR + 3 * NCON, CDIST = CFR + 9 * NCON;
   // Newton 6x6 foot blocks live in CIN's storage (composite inertias are dead after crb())

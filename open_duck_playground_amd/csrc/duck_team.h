@@ -146,15 +146,20 @@ constexpr float HF_DEPTH_TIE = 1e-6f;
 template <class Md>
 struct TLay {
   using Ly = Lay<Md>;
-  static constexpr int KC = Ly::TOTAL;                 // K.cdof per chain dof (6 x MAXCHAIN)
-  static constexpr int USED = KC + 6 * Md::MAXCHAIN;
+  // per-lane dump slots (SINK, 2 x TEAM words; debug line-search dumps use 136 words from here)
+  static constexpr int KC = Ly::TOTAL;
+#ifdef DUCK_LS_DUMP
+  static constexpr int USED = KC + 136;
+#else
+  static constexpr int USED = KC + 2 * TEAM;
+#endif
   static constexpr int STRIDE = ((USED + 15) / 32) * 32 + 16;  // = 16 (mod 32), >= USED
   static_assert(STRIDE >= USED && STRIDE % 32 == 16, "stride");
   static constexpr int FTMP = Ly::JA;                  // crb: F_i = I_b cdof_i (dead row storage)
   // per-lane dump slots for branchless conditional stores (L[ok ? addr : SINK + lane] = v): a
   // lane-divergent `if` leaves a join block whose exec restore the register allocator may put
   // live-range split copies in front of (tools/isa_exec_check.py), so the hot
-  // path avoids such regions where a select does the job. KC is dead storage in the fused solver.
+  // path avoids such regions where a select does the job.
   static constexpr int SINK = KC;
   // scratch of the flattened tree passes: the H + constraint-row storage is dead until the
   // constraint stage (kinematics / rne / crb run before it)
@@ -162,7 +167,7 @@ struct TLay {
   static constexpr int KLOC = TMP;                               // local body transforms (7 per body)
   static constexpr int RCS = TMP, RCF = TMP + 6 * Md::NB, RCDD = TMP + 12 * Md::NB;  // rne
   static constexpr int CRB = TMP, FT = TMP + 10 * Md::NB;        // crb
-  static_assert(12 * Md::NB + 6 * Md::NV <= Md::NM + 4 * Ly::NROW, "tree scratch must fit in H + rows");
+  static_assert(12 * Md::NB + 6 * Md::NV <= Ly::HSZ + 4 * Ly::NROW, "tree scratch must fit in H + rows");
   // the model blob (lane-indexed tables, constraint-row records) follows the env slices in
   // LDS when it fits, else it is read from global memory
   static constexpr int TAB = STRIDE * TEAM_WG;
@@ -1391,7 +1396,7 @@ struct TPhys {
   static constexpr int HF_QE = (Ly::CR - HF_QH0) / HF_ENT, HF_QR = 4 * HF_QE < 64 ? 4 * HF_QE : 64;
   static constexpr int HF_CINQ = (Ly::CIN + 3) & ~3, HF_SLF = (1 + Md::HF_SILCAP + 3) & ~3;
   static constexpr int HF_SLSZ = HF_SLF + 4 * Md::HF_SILCAP;
-  static_assert(Md::FLOOR_TYPE != 1 || (HF_QE >= 2 && HF_CINQ + 2 * HF_SLSZ <= Ly::CIN + 10 * Md::NB),
+  static_assert(Md::FLOOR_TYPE != 1 || (HF_QE >= 16 && HF_CINQ + 2 * HF_SLSZ <= Ly::CIN + 10 * Md::NB),
                 "height-field SAT queue / silhouette lists must fit their LDS storage");
 
   // One prism's separating-axis test against the hull for the lane that runs queue entry E

@@ -9,8 +9,8 @@ Mirrors ``playground/common/poly_reference_motion.py`` (``PolyReferenceMotion``)
 * ``get_reference_motion`` (:163-168) evaluates the 40 degree-15 polynomials at
   ``t = (i % nb_steps_in_period) / nb_steps_in_period``.
 
-The kernel evaluates the same thing on the GPU (``csrc/duck_env.hip``); this module bakes
-the table once. The reference stores the table as a pickle. Pickles that ship with the
+This module evaluates the polynomials once per phase (fp64) into a phase table; the step
+kernel (``csrc/duck_env_kernels.h``) looks the table up by grid cell and phase. The reference stores the table as a pickle. Pickles that ship with the
 reference are never unpickled here: :func:`read_poly_pkl` walks the opcode stream with
 ``pickletools.genops`` and interprets only inert data opcodes (dict/list/str/float/bytes
 and the two numpy scalar reconstructors, whose raw bytes are decoded with ``struct``),

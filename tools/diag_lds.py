@@ -24,18 +24,21 @@ gen = os.path.join(os.path.dirname(__file__), "..", "open_duck_playground_amd", 
                     "rough_terrain": "duck_model_rough.h",
                     "rough_terrain_backlash": "duck_model_rough_backlash.h"}[task])
 txt = open(gen).read()
-C = {k: int(v) for k, v in re.findall(r"\b(NB|NQ|NV|NU|NM|MAXCHAIN|NSENSORDATA|NPAIR|NFRIC|NLIM) = (\d+)", txt)}
+C = {k: int(v) for k, v in re.findall(r"\b(NB|NQ|NV|NU|NM|MAXCHAIN|NSENSORDATA|NPAIR|NFRIC|NLIM|NHE|NHF|FLOOR_TYPE) = (\d+)", txt)}
 NB, NQ, NV, NU, NM = C["NB"], C["NQ"], C["NV"], C["NU"], C["NM"]
 NCON = 4 * C["NPAIR"]
 NROW = C["NFRIC"] + C["NLIM"] + 4 * NCON
+# Lay::HSZ: the scratch in front of the rows, sized for its largest user
+need = max(12 * NB + 6 * NV, 6 * (C["NHE"] + C["NHF"]), 3 + 28 * 16 if C["FLOOR_TYPE"] == 1 else 0, 86 + 9 * NU)
+HSZ = (max(need - 4 * NROW - C["NLIM"], 0) + 3) // 4 * 4
 # Lay<Md> (csrc/duck_physics.h) in order
 fields = [("QPOS", NQ), ("QVEL", NV), ("WARM", NV), ("CTRL", NU), ("QACC", NV), ("QSM", NV), ("FSM", NV),
           ("SRCH", NV), ("GRAD", NV), ("MA", NV), ("DMASS", NB), ("DIPOS", 3), ("DARM", NV), ("DFRIC", NV),
           ("DQ0", NQ), ("DKP", NU), ("XPOS", 3 * NB), ("XQ", 4 * NB), ("XMAT", 9 * NB), ("CIN", 10 * NB),
-          ("CVEL", 6 * NB), ("COM", 3), ("CDOF", 6 * NV), ("CDD1", 18), ("M", NM), ("H", NM), ("JA", NROW),
+          ("CVEL", 6 * NB), ("COM", 3), ("CDOF", 6 * NV), ("CDD1", 18), ("M", NM), ("MZERO", 1), ("H", HSZ), ("JA", NROW),
           ("JV", NROW), ("RD", NROW), ("AREF", NROW), ("LSGN", C["NLIM"]), ("CR", 3 * NCON), ("CFR", 9 * NCON),
           ("CDIST", NCON), ("AF", NU), ("SENS", C["NSENSORDATA"]), ("OCON", 2), ("IMUR", 3), ("FOOTZ", 2),
-          ("FLAGS", 2), ("KC", 6 * C["MAXCHAIN"]), ("TSP", 6 * C["MAXCHAIN"] + 24)]
+          ("FLAGS", 2), ("SINK", 32)]
 total = sum(k for _, k in fields)
 
 env = Joystick(task, num_envs=1, device="cuda:0", use_imitation=False)
