@@ -646,6 +646,9 @@ struct TPhys {
     constexpr int BL = Md::T_BRLEN, MC = Md::MAXCHAIN;
     // (the composite inertias were summed in rne's subtree pass)
     STAGE_MARK(19);
+#ifdef DUCK_ASM_MARKS
+    asm volatile("; CRB_BEGIN" ::: "memory");
+#endif
     L[lane == 0 ? Ly::MZERO : TL::SINK + lane] = 0.0f;  // the zero word load_cols reads (LDS is not
                                                           // initialised by the launch)
     // M row i (lane i, i + 16): F_i = crb_{body(i)} cdof_i stays in registers;
@@ -730,6 +733,9 @@ struct TPhys {
 
   // ---------------- actuation + passive; H = M ----------------
   static DK void smooth(LP L, int lane) {
+#ifdef DUCK_ASM_MARKS
+    asm volatile("; SMOOTH_BEGIN" ::: "memory");
+#endif
     for (int i = lane; i < NV; i += TEAM) L[Ly::FSM + i] += -tf(Md::B_DAMP + i) * L[Ly::QVEL + i];
     TSYNC();
     if (lane < NU) {
@@ -1478,6 +1484,21 @@ struct TPhys {
       }
     }
     STAGE_MARK(45);
+#ifdef DUCK_STAGE_PROF
+    if (threadIdx.x < 64) {
+      // crossing top-edge pairs: all of the wave's survivors (49), hull edges crossing in any of them (50)
+      STAGE_ADD(49, (unsigned long long)(__popcll(pm[0]) + __popcll(pm[1]) + __popcll(pm[2])));
+      int uni = 0;
+      for (int e = 0; e < NE; e++) {
+        const int p0 = 3 * e;
+        const unsigned long long b3 = ((p0 >> 6) == ((p0 + 2) >> 6))
+                                          ? (pm[p0 >> 6] >> (p0 & 63)) & 7ull
+                                          : ((pm[p0 >> 6] >> (p0 & 63)) | (pm[(p0 >> 6) + 1] << (64 - (p0 & 63)))) & 7ull;
+        uni += __ballot(b3 != 0ull) != 0ull;
+      }
+      if ((int)threadIdx.x == __ffsll((long long)__ballot(1)) - 1) STAGE_ADD(50, (unsigned long long)uni);
+    }
+#endif
     // pass 2: each crossing pair's overlap along ev x em (lowest pair first)
     while (pm[0] | pm[1] | pm[2]) {
 #ifdef DUCK_STAGE_PROF

@@ -90,6 +90,8 @@ def main():
         print(f"{'hfield survivors':28s} {buf[40] / (nwg * steps * 10):10.2f} per substep (wave 0 of each workgroup: 8 feet)")
         print(f"{'hfield queue rounds':28s} {buf[46] / (nwg * steps * 10):10.2f} per substep (wave 0)")
         print(f"{'hfield pass-2 iterations':28s} {buf[48] / (nwg * steps * 10):10.2f} per substep (wave 0: the most crossing pairs of a lane)")
+        print(f"{'hfield crossing pairs':28s} {buf[49] / (nwg * steps * 10):10.2f} per substep (wave 0: all survivors)")
+        print(f"{'hfield crossing edges':28s} {buf[50] / (nwg * steps * 10):10.2f} per substep (wave 0: hull edges crossing in any survivor)")
     outside = per(14) + sum(per(k) for k in ENV)
     kern = outside + tot / (nwg * steps)
     if per(14) == 0:
