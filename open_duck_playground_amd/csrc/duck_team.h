@@ -26,6 +26,12 @@ typedef __attribute__((address_space(3))) f4v lds_f4;
 
 // fp32 reciprocal as one v_rcp_f32 (1 ulp; operands here are never denormal or zero)
 DK float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// m's lane bit ? t : f, as one v_cndmask the compiler cannot turn back into an indexed load
+DK float vsel(unsigned long long m, float t, float f) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+  return r;
+}
 
 // impedance of a constraint at violation pos (mjx constraint._kbi, imp part)
 DK float imp_of(const float* solimp, float pos) {
@@ -1434,11 +1440,28 @@ struct TPhys {
     // the prism's side normals (triangle kind A: -x, (g_x, g_y), -y; B: -(g_x, g_y), +x, +y)
     float sm[3][3];
     {
-      const float sx[3] = {tri ? -GX : -1.0f, tri ? 1.0f : GX, 0.0f};
-      const float sy[3] = {tri ? -GY : 0.0f, tri ? 0.0f : GY, tri ? 1.0f : -1.0f};
-      for (int k = 0; k < 3; k++)
-        for (int a = 0; a < 3; a++) sm[k][a] = sx[k] * xc[a] + sy[k] * yc[a];
+      const float sx0 = tri ? -GX : -1.0f, sx1 = tri ? 1.0f : GX;
+      const float sy0 = tri ? -GY : 0.0f, sy1 = tri ? 0.0f : GY, sy2 = tri ? 1.0f : -1.0f;
+      for (int a = 0; a < 3; a++) {
+        sm[0][a] = sx0 * xc[a] + sy0 * yc[a];
+        sm[1][a] = sx1 * xc[a] + sy1 * yc[a];
+        sm[2][a] = 0.0f * xc[a] + sy2 * yc[a];
+      }
     }
+    // selects by a runtime index k (pass 2, the winning axis) as v_cndmask on lane masks the
+    // compiler cannot see through: written as selects over elements of the Tm / sm arrays they were
+    // folded into indexed loads from scratch-memory copies of the arrays, a memory round trip per pair
+    auto side = [&](int k, float* o) {  // side normal k
+      const unsigned long long m0 = __ballot(k == 0), m1 = __ballot(k == 1);
+      for (int a = 0; a < 3; a++) o[a] = vsel(m0, sm[0][a], vsel(m1, sm[1][a], sm[2][a]));
+    };
+    auto top_edge = [&](int k, float* tm, float* em) {  // top vertex k and the edge to vertex k + 1
+      const unsigned long long m0 = __ballot(k == 0), m1 = __ballot(k == 1);
+      for (int a = 0; a < 3; a++) {
+        tm[a] = vsel(m0, Tm[0][a], vsel(m1, Tm[1][a], Tm[2][a]));
+        em[a] = vsel(m0, Tm[1][a], vsel(m1, Tm[2][a], Tm[0][a])) - tm[a];
+      }
+    };
     float mu[3] = {0.0f, 0.0f, 0.0f};
     auto take = [&](float ov, int pr, const float* u) {
       const bool b = (ov < mo) | ((ov == mo) & (pr < mp));
@@ -1470,18 +1493,20 @@ struct TPhys {
       // (one prism edge at a time: 30 face products live, not 90)
       float ADC[NE];
       static_for<0, NE>([&](auto eI) { ADC[eI.value] = dxc_dot<eI.value>(ntm); });
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
+      // (k a compile-time constant too, so that every pm index is one: a runtime index kept pm in
+      // scratch memory, and pass 2's word selects became indexed scratch loads)
+      static_for<0, 3>([&](auto kI) {
+        constexpr int k = kI.value;
         float phi[NF];
         static_for<0, NF>([&](auto fI) { phi[fI.value] = nf_dot<fI.value>(hx[k]); });
         static_for<0, NE>([&](auto eI) {
           constexpr int e = eI.value, fa = Md::hull_edge_face[e][0], fb = Md::hull_edge_face[e][1];
           const float BDC = dxc_dot<e>(sm[k]);
           const float mx = fmaxf(fmaxf(phi[fa] * phi[fb], ADC[e] * BDC), phi[fa] * BDC);
-          const int p = 3 * e + k;
+          constexpr int p = 3 * e + k;
           pm[p >> 6] |= (unsigned long long)(__float_as_uint(mx) >> 31) << (p & 63);
         });
-      }
+      });
     }
     STAGE_MARK(45);
 #ifdef DUCK_STAGE_PROF
@@ -1515,12 +1540,8 @@ struct TPhys {
       const f4v ev4 = ht4(o + 12), v04 = ht4(o + 16);
       const float ev[3] = {ev4.x, ev4.y, ev4.z}, v0[3] = {v04.x, v04.y, v04.z};
       float em[3], tm[3], sk[3];
-      for (int a = 0; a < 3; a++) {
-        const float t0 = Tm[0][a], t1 = Tm[1][a], t2 = Tm[2][a];
-        tm[a] = k == 0 ? t0 : (k == 1 ? t1 : t2);
-        em[a] = (k == 0 ? t1 : (k == 1 ? t2 : t0)) - tm[a];
-        sk[a] = k == 0 ? sm[0][a] : (k == 1 ? sm[1][a] : sm[2][a]);
-      }
+      side(k, sk);
+      top_edge(k, tm, em);
       float u[3];
       cross3(u, ev, em);
       const float u2 = dot3(u, u);
@@ -1540,10 +1561,9 @@ struct TPhys {
       const int f = mp - 5;
       const f4v n4 = ht4(Md::B_HFACE + 4 * (f > 0 ? f : 0));
       const float nf[3] = {-n4.x, -n4.y, -n4.z};
-      for (int a = 0; a < 3; a++) {
-        const float s = mp == 1 ? sm[0][a] : (mp == 2 ? sm[1][a] : sm[2][a]);
-        mu[a] = mp == 0 ? ntm[a] : (mp < 4 ? s : (mp == 4 ? -zc[a] : nf[a]));
-      }
+      float sv[3];
+      side(mp - 1, sv);
+      for (int a = 0; a < 3; a++) mu[a] = mp == 0 ? ntm[a] : (mp < 4 ? sv[a] : (mp == 4 ? -zc[a] : nf[a]));
     }
     // the contact point: hull vertices inside the prism and prism top vertices inside the hull,
     // weighted by their penetration
