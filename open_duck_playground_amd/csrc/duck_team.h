@@ -2951,20 +2951,34 @@ struct TPhys {
     rne(L, lane);
     STAGE_MARK(2);
     crb(L, lane);
+    // DUCK_DOUBLE (measurement builds, tools/gpu_stage_double.sh): one idempotent stage runs twice,
+    // and the launch-time difference to the normal build is that stage's cost, unperturbed by markers
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 1
+    crb(L, lane);
+#endif
     STAGE_MARK(3);
     smooth(L, lane);
     STAGE_MARK(28);
     // collision and the constraint rows depend on the kinematics only: they run before the
     // smooth acceleration so that M is loaded into registers once for both solves
     collision(L, lane, hf);
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 2
+    collision(L, lane, hf);
+#endif
     STAGE_MARK(5);
     make_rows(L, lane);
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 3
+    make_rows(L, lane);
+#endif
     STAGE_MARK(6);
     {
       float Mc[NC][NV];
       load_cols(L, lane, Mc, false);
       STAGE_MARK(20);
       smooth_acc(L, lane, Mc);
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 4
+      smooth_acc(L, lane, Mc);
+#endif
       STAGE_MARK(4);
       solve(L, lane, scratch, sstride, Mc);
     }
