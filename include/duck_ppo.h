@@ -1,7 +1,10 @@
 /* duck_ppo.h — C ABI of the learner-side kernels of the PPO outer loop (libduck.so).
  *
- *   duck_gae   brax losses.compute_gae (the advantage/value-target recursion brax PPO runs in
- *                its loss; the reference reaches it through ppo.train at common/runner.py:104-118)
+ *   duck_gae       brax losses.compute_gae (the advantage/value-target recursion brax PPO runs in
+ *                  its loss; the reference reaches it through ppo.train at common/runner.py:104-118)
+ *   duck_ppo_loss  brax losses.compute_ppo_loss after GAE: clipped surrogate + value loss + entropy
+ *                  bonus of one minibatch and its gradient w.r.t. the policy logits and the value
+ *                  baseline (open_duck_playground_amd/ppo.py:ppo_loss is the same computation in torch)
  *
  * Same conventions as duck.h: DEVICE pointers, float32, time-major [T][B] arrays (B = number of
  * trajectories, contiguous), `stream` a hipStream_t, negative return codes on error.
@@ -20,6 +23,23 @@ extern "C" {
 int duck_gae(int T, int B, const float* truncation, const float* termination, const float* reward,
              const float* value, const float* bootstrap, float lambda_, float discount, float* vs, float* adv,
              void* stream);
+
+/* The PPO loss of a minibatch of N samples, action size A (three launches; deterministic sums):
+ *   logits [N][2A] (loc | pre-softplus scale), raw_action [N][A] (pre-tanh), old_logprob [N],
+ *   advantage [N] (GAE, normalised inside when normalize_advantage: (a - mean) / (std + 1e-8)),
+ *   value_target [N] (GAE vs), baseline [N] (value head), eps [N][A] (standard normal draws of the
+ *   entropy estimate). scale = softplus(pre) + 1e-3; lp = sum_j log N(raw; loc, scale) - log|tanh'(raw)|;
+ *   rho = exp(lp - old_logprob); policy = -mean(min(rho a, clip(rho, 1 - clip_eps, 1 + clip_eps) a));
+ *   value = 0.25 mean((value_target - baseline)^2); entropy = mean sum_j (0.5 + 0.5 log 2 pi + log scale
+ *   + log|tanh'(loc + scale eps)|). out[4] = {policy + value - entropy_cost entropy, policy, value,
+ *   entropy}; grad_logits [N][2A], grad_baseline [N] = d out[0] / d logits, d out[0] / d baseline.
+ *   out must hold duck_ppo_loss_out_size(N) floats (the rest is the launches' scratch). */
+int duck_ppo_loss(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
+                  const float* advantage, const float* value_target, const float* baseline, const float* eps,
+                  float clip_eps, float entropy_cost, int normalize_advantage, float* out, float* grad_logits,
+                  float* grad_baseline, void* stream);
+/* 4 + 2 + 3 ceil(N / 256): the length of duck_ppo_loss's out array */
+int duck_ppo_loss_out_size(int N);
 
 #ifdef __cplusplus
 }

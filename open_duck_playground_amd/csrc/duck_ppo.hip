@@ -32,6 +32,147 @@ __global__ __launch_bounds__(256) void gae_kernel(int T, int B, const float* __r
     }
 }
 
+
+// Block-wide sum over the 1024 threads of one workgroup (wave DPP-free: LDS tree, 16 waves).
+__device__ float block_sum(float v, float* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+    if (threadIdx.x < 64) {
+        t = threadIdx.x < (blockDim.x >> 6) ? red[threadIdx.x] : 0.f;
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_down(t, o, 64);
+        if (threadIdx.x == 0) red[0] = t;
+    }
+    __syncthreads();
+    const float r = red[0];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ float softplusf(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
+// log |d tanh(x)/dx| = 2 (log 2 - x - softplus(-2x)) and its derivative -2 tanh(x)
+__device__ __forceinline__ float ldjf(float x) { return 2.f * (0.69314718055994531f - x - softplusf(-2.f * x)); }
+
+// The PPO loss of one minibatch and its gradient with respect to the policy logits and the value
+// baseline in three launches: the advantage statistics (one workgroup, two-pass mean / population
+// std), then one thread per sample (the NormalTanh log-probability ratio, the clipped surrogate, the
+// value error and the entropy estimate at loc + scale eps, with their derivatives; per-workgroup
+// partial sums), then the sums of the partials (one workgroup): deterministic, and it replaces ~150
+// small autograd kernels per minibatch. Gradients follow torch's rules: minimum() splits a tie
+// evenly, clamp() passes the gradient on its closed interval.
+__global__ __launch_bounds__(1024) void adv_stats_kernel(int N, const float* __restrict__ adv, int normalize,
+                                                         float* __restrict__ stats) {
+    __shared__ float red[16];
+    const float invN = 1.f / (float)N;
+    float mean = 0.f, inv_std = 1.f;
+    if (normalize) {
+        float s = 0.f;
+        for (int i = threadIdx.x; i < N; i += blockDim.x) s += adv[i];
+        mean = block_sum(s, red) * invN;
+        float q = 0.f;
+        for (int i = threadIdx.x; i < N; i += blockDim.x) {
+            const float d = adv[i] - mean;
+            q += d * d;
+        }
+        inv_std = 1.f / (sqrtf(block_sum(q, red) * invN) + 1e-8f);
+    }
+    if (threadIdx.x == 0) {
+        stats[0] = mean;
+        stats[1] = inv_std;
+    }
+}
+
+constexpr int PPO_TPB = 256;
+
+__global__ __launch_bounds__(PPO_TPB) void ppo_loss_kernel(int N, int A, const float* __restrict__ logits,
+                                                            const float* __restrict__ raw_action,
+                                                            const float* __restrict__ old_logprob,
+                                                            const float* __restrict__ adv,
+                                                            const float* __restrict__ vs,
+                                                            const float* __restrict__ baseline,
+                                                            const float* __restrict__ eps, float clip_eps,
+                                                            float entropy_cost, const float* __restrict__ stats,
+                                                            float* __restrict__ partial, float* __restrict__ g_logits,
+                                                            float* __restrict__ g_baseline) {
+    __shared__ float red[3][PPO_TPB / 64];
+    const float invN = 1.f / (float)N;
+    const float HL2PI = 0.91893853320467274f;  // 0.5 log(2 pi)
+    const int i = blockIdx.x * PPO_TPB + threadIdx.x;
+    float spl = 0.f, svl = 0.f, sent = 0.f;
+    if (i < N) {
+        const float mean = stats[0], inv_std = stats[1];
+        const float* lg = logits + (size_t)i * 2 * A;
+        const float* ra = raw_action + (size_t)i * A;
+        const float* ep = eps + (size_t)i * A;
+        float lp = 0.f, ent = 0.f;
+        for (int j = 0; j < A; j++) {
+            const float loc = lg[j], sc = softplusf(lg[A + j]) + 1e-3f, a = ra[j];
+            const float z = (a - loc) / sc, ls = logf(sc);
+            lp += -0.5f * z * z - ls - HL2PI - ldjf(a);
+            ent += 0.5f + HL2PI + ls + ldjf(loc + sc * ep[j]);
+        }
+        const float rho = expf(lp - old_logprob[i]);
+        const float an = (adv[i] - mean) * inv_std;
+        const float lo = 1.f - clip_eps, hi = 1.f + clip_eps;
+        const float s1 = rho * an, s2 = fminf(fmaxf(rho, lo), hi) * an;
+        const bool inr = rho >= lo && rho <= hi;
+        // d(-min(s1, s2))/d lp
+        const float gmin = s1 < s2 ? rho * an : (s1 > s2 ? (inr ? rho * an : 0.f) : 0.5f * rho * an * (inr ? 2.f : 1.f));
+        const float g_lp = -gmin * invN, g_ent = -entropy_cost * invN;
+        spl = -fminf(s1, s2);
+        const float dv = vs[i] - baseline[i];
+        svl = dv * dv;
+        sent = ent;
+        g_baseline[i] = -0.5f * dv * invN;
+        float* gl = g_logits + (size_t)i * 2 * A;
+        for (int j = 0; j < A; j++) {
+            const float loc = lg[j], r = lg[A + j], sc = softplusf(r) + 1e-3f, a = ra[j], e = ep[j];
+            const float isc = 1.f / sc, z = (a - loc) * isc;
+            const float dldj = -2.f * tanhf(loc + sc * e);
+            gl[j] = g_lp * z * isc + g_ent * dldj;
+            gl[A + j] = sigmoidf(r) * (g_lp * (z * z - 1.f) * isc + g_ent * (isc + dldj * e));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        spl += __shfl_down(spl, o, 64);
+        svl += __shfl_down(svl, o, 64);
+        sent += __shfl_down(sent, o, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][w] = spl;
+        red[1][w] = svl;
+        red[2][w] = sent;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        float t = 0.f;
+        for (int k = 0; k < PPO_TPB / 64; k++) t += red[threadIdx.x][k];
+        partial[(size_t)blockIdx.x * 3 + threadIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(1024) void ppo_loss_sum_kernel(int N, int nblk, const float* __restrict__ partial,
+                                                             float entropy_cost, float* __restrict__ out) {
+    __shared__ float red[16];
+    const float invN = 1.f / (float)N;
+    float s[3] = {0.f, 0.f, 0.f};
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x)
+        for (int k = 0; k < 3; k++) s[k] += partial[(size_t)b * 3 + k];
+    const float pl = block_sum(s[0], red) * invN, vl = 0.25f * block_sum(s[1], red) * invN;
+    const float en = block_sum(s[2], red) * invN;
+    if (threadIdx.x == 0) {
+        out[0] = pl + vl - entropy_cost * en;
+        out[1] = pl;
+        out[2] = vl;
+        out[3] = en;
+    }
+}
+
 }  // namespace
 
 extern "C" int duck_gae(int T, int B, const float* truncation, const float* termination, const float* reward,
@@ -46,3 +187,27 @@ extern "C" int duck_gae(int T, int B, const float* truncation, const float* term
     HIPCHECK(hipGetLastError());
     return DUCK_OK;
 }
+
+extern "C" int duck_ppo_loss(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
+                             const float* advantage, const float* value_target, const float* baseline,
+                             const float* eps, float clip_eps, float entropy_cost, int normalize_advantage,
+                             float* out, float* grad_logits, float* grad_baseline, void* stream) {
+    if (N <= 0 || A <= 0) return duck_fail(DUCK_EINVAL, "duck_ppo_loss: empty batch");
+    if (!logits || !raw_action || !old_logprob || !advantage || !value_target || !baseline || !eps || !out ||
+        !grad_logits || !grad_baseline)
+        return duck_fail(DUCK_EINVAL, "duck_ppo_loss: null pointer");
+    const int nblk = (N + PPO_TPB - 1) / PPO_TPB;
+    // scratch: out[4 ..) of the caller's 4 + 2 + 3 nblk floats holds the statistics and the partial sums
+    float* stats = out + 4;
+    float* partial = out + 6;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(adv_stats_kernel, dim3(1), dim3(1024), 0, st, N, advantage, normalize_advantage, stats);
+    hipLaunchKernelGGL(ppo_loss_kernel, dim3(nblk), dim3(PPO_TPB), 0, st, N, A, logits, raw_action, old_logprob,
+                       advantage, value_target, baseline, eps, clip_eps, entropy_cost, stats, partial, grad_logits,
+                       grad_baseline);
+    hipLaunchKernelGGL(ppo_loss_sum_kernel, dim3(1), dim3(1024), 0, st, N, nblk, partial, entropy_cost, out);
+    HIPCHECK(hipGetLastError());
+    return DUCK_OK;
+}
+
+extern "C" int duck_ppo_loss_out_size(int N) { return 4 + 2 + 3 * (((N > 0 ? N : 0) + PPO_TPB - 1) / PPO_TPB); }

@@ -21,7 +21,8 @@ BUILD = os.path.join(HERE, "build")  # libraries compiled for other models (mode
 
 EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get", "duck_aux_size", "duck_create", "duck_destroy",
            "duck_debug_stage_cycles", "duck_model_fingerprint", "duck_model_supported",
-           "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae"]
+           "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae", "duck_ppo_loss",
+           "duck_ppo_loss_out_size"]
 
 
 class DuckError(RuntimeError):
@@ -223,6 +224,10 @@ def lib(path: str = None):
         L.duck_model_supported.argtypes = [C.POINTER(DuckModelDesc)]
         if hasattr(L, "duck_gae"):
             L.duck_gae.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp]
+        if hasattr(L, "duck_ppo_loss"):
+            L.duck_ppo_loss.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_int,
+                                        vp, vp, vp, vp]
+            L.duck_ppo_loss_out_size.argtypes = [C.c_int]
         _libs[path] = L
     return _libs[path]
 

@@ -206,14 +206,57 @@ def compute_gae(truncation: torch.Tensor, termination: torch.Tensor, rewards: to
     return vs, adv
 
 
-def ppo_loss(net: ActorCritic, batch: Dict[str, torch.Tensor], cfg: PPOConfig, gen: Optional[torch.Generator]):
-    """batch tensors are time-major [T, B, ...]; returns (loss, metrics)."""
+class _FusedLoss(torch.autograd.Function):
+    """The PPO loss after GAE as one ``duck_ppo_loss`` HIP launch (csrc/duck_ppo.hip): the forward
+    returns [loss, policy_loss, v_loss, entropy] and the kernel's gradients w.r.t. the logits and
+    the baseline, which the backward scales by d loss (the three metrics are detached)."""
+
+    @staticmethod
+    def forward(ctx, logits, baseline, raw_action, old_logprob, adv, vs, eps, clip_eps, entropy_cost, normalize):
+        from .native import check, lib
+        args = [t.detach().contiguous() for t in (logits, raw_action, old_logprob, adv, vs, baseline, eps)]
+        if any(a.dtype != torch.float32 for a in args):
+            raise TypeError("the fused PPO loss takes float32 tensors")
+        lg, ra, olp, ad, v, bl, ep = args
+        A = ra.shape[-1]
+        N = ra.numel() // A
+        out = torch.empty(lib().duck_ppo_loss_out_size(N), dtype=torch.float32, device=lg.device)  # + scratch
+        g_lg, g_bl = torch.empty_like(lg), torch.empty_like(bl)
+        check(lib().duck_ppo_loss(N, A, lg.data_ptr(), ra.data_ptr(), olp.data_ptr(), ad.data_ptr(), v.data_ptr(),
+                                  bl.data_ptr(), ep.data_ptr(), float(clip_eps), float(entropy_cost), int(normalize),
+                                  out.data_ptr(), g_lg.data_ptr(), g_bl.data_ptr(),
+                                  torch.cuda.current_stream(lg.device).cuda_stream))
+        ctx.save_for_backward(g_lg, g_bl)
+        return out[:4]
+
+    @staticmethod
+    def backward(ctx, g_out):
+        g_lg, g_bl = ctx.saved_tensors
+        return g_lg * g_out[0], g_bl * g_out[0], None, None, None, None, None, None, None, None
+
+
+def ppo_loss(net: ActorCritic, batch: Dict[str, torch.Tensor], cfg: PPOConfig, gen: Optional[torch.Generator],
+             fused: Optional[bool] = None):
+    """batch tensors are time-major [T, B, ...]; returns (loss, metrics). On the GPU the part after
+    the networks and GAE runs as the fused ``duck_ppo_loss`` kernel (one launch instead of ~150 small
+    autograd kernels per minibatch; ``fused=False`` or DUCK_PPO_FUSED=0 keeps the torch expression
+    below, which is also its test reference)."""
     logits = net.policy_logits(batch["obs"])
     baseline = net.value_of(batch["priv"])
     bootstrap = net.value_of(batch["next_priv"][-1])
     rewards = batch["reward"] * cfg.reward_scaling
     truncation = batch["truncation"]
     termination = batch["done"] * (1.0 - truncation)
+    if fused is None:
+        fused = logits.is_cuda and os.environ.get("DUCK_PPO_FUSED", "1") != "0"
+    if fused:
+        vs, adv = compute_gae(truncation, termination, rewards, baseline.detach(), bootstrap.detach(), cfg.gae_lambda,
+                              cfg.discounting)
+        loc = logits[..., : logits.shape[-1] // 2]
+        eps = torch.randn(loc.shape, device=loc.device, generator=gen)  # the entropy sample, as NormalTanh draws it
+        out = _FusedLoss.apply(logits, baseline, batch["raw_action"], batch["log_prob"], adv, vs, eps,
+                               cfg.clipping_epsilon, cfg.entropy_cost, bool(cfg.normalize_advantage))
+        return out[0], {"policy_loss": out[1].detach(), "v_loss": out[2].detach(), "entropy": out[3].detach()}
     dist_ = NormalTanh(logits)
     target_lp = dist_.log_prob(batch["raw_action"])
     vs, adv = compute_gae(truncation, termination, rewards, baseline.detach(), bootstrap.detach(), cfg.gae_lambda,

@@ -135,6 +135,16 @@ def test_cabi_exports_every_declared_symbol():
     assert set(native.EXPORTS) >= syms
 
 
+def test_ppo_loss_sizes_and_argument_checks():
+    """Host-side contract of duck_ppo_loss (no GPU call): the out array's length and the refusals."""
+    lib = native.lib()
+    assert [lib.duck_ppo_loss_out_size(n) for n in (0, 1, 256, 257, 5120)] == [6, 9, 9, 12, 66]
+    assert lib.duck_ppo_loss(0, 14, *([None] * 7), 0.2, 0.005, 1, None, None, None, None) < 0
+    assert b"empty batch" in lib.duck_last_error()
+    assert lib.duck_ppo_loss(8, 14, *([None] * 7), 0.2, 0.005, 1, None, None, None, None) < 0
+    assert b"null pointer" in lib.duck_last_error()
+
+
 @pytest.mark.parametrize("nq,nv,nu,imit,task", [(21, 20, 14, 0, 0), (21, 20, 14, 1, 0), (31, 30, 14, 1, 0),
                                                 (21, 20, 14, 0, 1), (31, 30, 14, 1, 1)])
 def test_layout_matches_c(nq, nv, nu, imit, task):

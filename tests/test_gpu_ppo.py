@@ -89,3 +89,39 @@ def test_runner_standing_env(gpu, tmp_path, monkeypatch):
     runner.main(["--output_dir", "ck", "--env", "standing", "--num_timesteps", str(20 * 256)])
     line = json.loads(open(tmp_path / "ck" / "metrics.jsonl").readline())
     assert line["step"] == 20 * 256 and np.isfinite(line["train/loss"])
+
+
+@pytest.mark.parametrize("normalize", [True, False])
+def test_fused_loss_matches_torch(gpu, normalize):
+    """duck_ppo_loss (one HIP launch) against the torch expression of ppo_loss on the same minibatch:
+    loss, the three metrics and every parameter gradient, with the entropy sample drawn from the same
+    generator state; ratios pushed across the clip range on some samples (both sides of the clamp,
+    and exact ties where rho is inside it)."""
+    torch.manual_seed(0)
+    T, B, A = 20, 64, 14
+    cfg = ppo.PPOConfig(normalize_advantage=normalize)
+    net = ppo.ActorCritic(101, 172, A, cfg).to(gpu)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    r = lambda *s: torch.randn(*s, generator=g).to(gpu)
+    batch = {"obs": r(T, B, 101), "priv": r(T, B, 172), "next_priv": r(T, B, 172),
+             "reward": r(T, B), "truncation": (torch.rand(T, B, generator=g) < 0.05).float().to(gpu),
+             "done": (torch.rand(T, B, generator=g) < 0.1).float().to(gpu), "raw_action": 1.5 * r(T, B, A)}
+    with torch.no_grad():
+        lp = ppo.NormalTanh(net.policy_logits(batch["obs"])).log_prob(batch["raw_action"])
+    # old log-probs: the current ones shifted so that rho spans [0.5, 1.6] (clip range 0.8 .. 1.2)
+    batch["log_prob"] = lp - torch.log(torch.linspace(0.5, 1.6, T * B, device=gpu)).view(T, B)
+    res = []
+    for fused in (False, True):
+        net.zero_grad(set_to_none=True)
+        gen = torch.Generator(device=gpu).manual_seed(7)
+        loss, m = ppo.ppo_loss(net, batch, cfg, gen, fused=fused)
+        loss.backward()
+        res.append((float(loss), {k: float(v) for k, v in m.items()},
+                    [p.grad.detach().clone() for p in net.parameters()]))
+    (l0, m0, g0), (l1, m1, g1) = res
+    assert abs(l1 - l0) <= 1e-5 * (1 + abs(l0)), (l0, l1)
+    for k in m0:
+        assert abs(m1[k] - m0[k]) <= 1e-5 * (1 + abs(m0[k])), (k, m0[k], m1[k])
+    for a, b in zip(g0, g1):
+        err = float((a - b).abs().max()) / (1e-6 + float(a.abs().max()))
+        assert err < 1e-4, err
