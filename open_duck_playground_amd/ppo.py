@@ -125,7 +125,20 @@ class RunningStatistics(nn.Module):
         self.register_buffer("mean", torch.zeros(size, dtype=torch.float64))
         self.register_buffer("summed_var", torch.zeros(size, dtype=torch.float64))
         self.register_buffer("std", torch.ones(size, dtype=torch.float64))
+        # fp32 copies for normalize(): the same conversions, made once per update instead of per call
+        # (two conversion kernels less in every policy / value evaluation; not checkpointed)
+        self.register_buffer("mean32", torch.zeros(size), persistent=False)
+        self.register_buffer("std32", torch.ones(size), persistent=False)
         self.std_eps, self.std_min, self.std_max = std_eps, std_min, std_max
+
+    @torch.no_grad()
+    def _refresh(self) -> None:
+        self.mean32.copy_(self.mean)
+        self.std32.copy_(self.std)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        super()._load_from_state_dict(*args, **kwargs)
+        self._refresh()
 
     @torch.no_grad()
     def update(self, x: torch.Tensor) -> None:
@@ -146,8 +159,11 @@ class RunningStatistics(nn.Module):
         self.count.copy_(tot)
         var = self.summed_var / self.count
         self.std.copy_(torch.clamp(torch.sqrt(var + self.std_eps), self.std_min, self.std_max))
+        self._refresh()
 
     def normalize(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dtype == torch.float32:
+            return (x - self.mean32) / self.std32
         return (x - self.mean.to(x.dtype)) / self.std.to(x.dtype)
 
 
@@ -242,8 +258,10 @@ def ppo_loss(net: ActorCritic, batch: Dict[str, torch.Tensor], cfg: PPOConfig, g
     autograd kernels per minibatch; ``fused=False`` or DUCK_PPO_FUSED=0 keeps the torch expression
     below, which is also its test reference)."""
     logits = net.policy_logits(batch["obs"])
-    baseline = net.value_of(batch["priv"])
-    bootstrap = net.value_of(batch["next_priv"][-1])
+    # the baseline [T, B] and the bootstrap value [B] in one pass of the value network
+    priv, nxt = batch["priv"], batch["next_priv"][-1]
+    v_all = net.value_of(torch.cat([priv.reshape(-1, priv.shape[-1]), nxt], 0))
+    baseline, bootstrap = v_all[: priv.shape[0] * priv.shape[1]].view(priv.shape[:2]), v_all[priv.shape[0] * priv.shape[1]:]
     rewards = batch["reward"] * cfg.reward_scaling
     truncation = batch["truncation"]
     termination = batch["done"] * (1.0 - truncation)
