@@ -66,12 +66,47 @@ class PPOConfig:
 # ---------------------------------------------------------------------------------------
 # networks (brax ppo/networks.py: MLP with swish, NormalTanhDistribution)
 # ---------------------------------------------------------------------------------------
+class _SplitKLinearFn(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient dW = dY^T X is formed as SPLITK partial products over
+    row blocks of the batch and their sum: the learner's minibatches are K = 5120 rows deep and only
+    a few 32 x 32 output tiles wide, which one GEMM runs on a fraction of the chip (31 us -> 14-20 us
+    per layer on MI355X, `tools/bench_dw.py`)."""
+
+    SPLITK = 4
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        ctx.save_for_backward(x2, w)
+        ctx.xshape = x.shape
+        return torch.addmm(b, x2, w.t()).view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w = ctx.saved_tensors
+        g2 = gy.reshape(-1, gy.shape[-1])
+        n, S = g2.shape[0], _SplitKLinearFn.SPLITK
+        gx = g2.mm(w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        if g2.shape[1] >= 8 and n % S == 0 and n >= 64 * S:
+            gw = torch.bmm(g2.view(S, n // S, -1).transpose(1, 2), x2.view(S, n // S, -1)).sum(0)
+        else:
+            gw = g2.t().mm(x2)
+        return gx, gw, g2.sum(0)
+
+
+class SplitKLinear(nn.Linear):
+    """nn.Linear (same parameters, state dict and export) with the split-K weight gradient."""
+
+    def forward(self, x):
+        return _SplitKLinearFn.apply(x, self.weight, self.bias)
+
+
 def mlp(sizes: Sequence[int], out: int) -> nn.Sequential:
     layers, prev = [], sizes[0]
     for h in sizes[1:]:
-        layers += [nn.Linear(prev, h), nn.SiLU()]
+        layers += [SplitKLinear(prev, h), nn.SiLU()]
         prev = h
-    layers.append(nn.Linear(prev, out))
+    layers.append(SplitKLinear(prev, out))
     for m in layers:  # brax: lecun_uniform kernels, zero bias
         if isinstance(m, nn.Linear):
             bound = math.sqrt(3.0 / m.in_features)

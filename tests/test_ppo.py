@@ -221,3 +221,23 @@ def test_two_rank_data_parallel_stays_in_sync():
     assert np.array_equal(p0, p1)  # identical init (broadcast) + all-reduced grads -> identical params
     assert np.array_equal(m0, m1) and c0 == c1 == 3 * 8 * 64  # normaliser saw both ranks' batches
     assert s0 == s1 == 3 * 8 * 64
+
+
+@pytest.mark.parametrize("n,out", [(5120, 256), (4096, 28), (100, 64), (5120, 1)])
+def test_split_k_linear_matches_linear(n, out):
+    """SplitKLinear: the same outputs and gradients as nn.Linear (split-K weight gradient for deep
+    batches, the plain product otherwise)."""
+    torch.manual_seed(0)
+    a = ppo.SplitKLinear(37, out)
+    b = torch.nn.Linear(37, out)
+    b.load_state_dict(a.state_dict())
+    x1 = torch.randn(n, 37, requires_grad=True)
+    x2 = x1.detach().clone().requires_grad_(True)
+    gy = torch.randn(n, out)
+    ya, yb = a(x1), b(x2)
+    assert torch.allclose(ya, yb, atol=1e-6)
+    ya.backward(gy)
+    yb.backward(gy)
+    assert torch.allclose(x1.grad, x2.grad, atol=1e-5)
+    assert torch.allclose(a.weight.grad, b.weight.grad, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(a.bias.grad, b.bias.grad, rtol=1e-5, atol=1e-4)
