@@ -38,7 +38,7 @@ int duck_ppo_loss(int N, int A, const float* logits, const float* raw_action, co
                   const float* advantage, const float* value_target, const float* baseline, const float* eps,
                   float clip_eps, float entropy_cost, int normalize_advantage, float* out, float* grad_logits,
                   float* grad_baseline, void* stream);
-/* 4 + 2 + 3 ceil(N / 256): the length of duck_ppo_loss's out array */
+/* 4 + 2 + 3 ceil(N / 128): the length of duck_ppo_loss's out array (A <= 31) */
 int duck_ppo_loss_out_size(int N);
 
 #ifdef __cplusplus

@@ -86,8 +86,12 @@ __global__ __launch_bounds__(1024) void adv_stats_kernel(int N, const float* __r
     }
 }
 
-constexpr int PPO_TPB = 256;
+constexpr int PPO_TPB = 128;
 
+// One thread per sample; the workgroup's rows of logits / raw actions / entropy draws are staged in
+// LDS by coalesced loads (a thread's own row is 2A or A consecutive floats: read directly, a wave's
+// accesses would be 64 rows apart) and the logits gradient leaves the same way. Row strides in LDS are
+// odd, so the per-sample reads of a wave fall on distinct banks.
 __global__ __launch_bounds__(PPO_TPB) void ppo_loss_kernel(int N, int A, const float* __restrict__ logits,
                                                             const float* __restrict__ raw_action,
                                                             const float* __restrict__ old_logprob,
@@ -98,16 +102,32 @@ __global__ __launch_bounds__(PPO_TPB) void ppo_loss_kernel(int N, int A, const f
                                                             float entropy_cost, const float* __restrict__ stats,
                                                             float* __restrict__ partial, float* __restrict__ g_logits,
                                                             float* __restrict__ g_baseline) {
+    extern __shared__ float sh[];
+    const int SL = 2 * A + 1, SA = A + 1;  // odd LDS row strides
+    float* s_lg = sh;                      // [PPO_TPB][SL]: logits in, their gradient out
+    float* s_ra = s_lg + PPO_TPB * SL;     // [PPO_TPB][SA]
+    float* s_ep = s_ra + PPO_TPB * SA;     // [PPO_TPB][SA]
     __shared__ float red[3][PPO_TPB / 64];
+    const int i0 = blockIdx.x * PPO_TPB, nr = min(PPO_TPB, N - i0);
+    for (int k = threadIdx.x; k < nr * 2 * A; k += PPO_TPB) {
+        const int r = k / (2 * A);
+        s_lg[r * SL + (k - r * 2 * A)] = logits[(size_t)i0 * 2 * A + k];
+    }
+    for (int k = threadIdx.x; k < nr * A; k += PPO_TPB) {
+        const int r = k / A, c = k - r * A;
+        s_ra[r * SA + c] = raw_action[(size_t)i0 * A + k];
+        s_ep[r * SA + c] = eps[(size_t)i0 * A + k];
+    }
+    __syncthreads();
     const float invN = 1.f / (float)N;
     const float HL2PI = 0.91893853320467274f;  // 0.5 log(2 pi)
-    const int i = blockIdx.x * PPO_TPB + threadIdx.x;
+    const int i = i0 + threadIdx.x;
     float spl = 0.f, svl = 0.f, sent = 0.f;
-    if (i < N) {
+    if (threadIdx.x < nr) {
         const float mean = stats[0], inv_std = stats[1];
-        const float* lg = logits + (size_t)i * 2 * A;
-        const float* ra = raw_action + (size_t)i * A;
-        const float* ep = eps + (size_t)i * A;
+        float* lg = s_lg + threadIdx.x * SL;
+        const float* ra = s_ra + threadIdx.x * SA;
+        const float* ep = s_ep + threadIdx.x * SA;
         float lp = 0.f, ent = 0.f;
         for (int j = 0; j < A; j++) {
             const float loc = lg[j], sc = softplusf(lg[A + j]) + 1e-3f, a = ra[j];
@@ -128,14 +148,18 @@ __global__ __launch_bounds__(PPO_TPB) void ppo_loss_kernel(int N, int A, const f
         svl = dv * dv;
         sent = ent;
         g_baseline[i] = -0.5f * dv * invN;
-        float* gl = g_logits + (size_t)i * 2 * A;
-        for (int j = 0; j < A; j++) {
+        for (int j = 0; j < A; j++) {  // the gradient overwrites the staged logits row (j and A + j read first)
             const float loc = lg[j], r = lg[A + j], sc = softplusf(r) + 1e-3f, a = ra[j], e = ep[j];
             const float isc = 1.f / sc, z = (a - loc) * isc;
             const float dldj = -2.f * tanhf(loc + sc * e);
-            gl[j] = g_lp * z * isc + g_ent * dldj;
-            gl[A + j] = sigmoidf(r) * (g_lp * (z * z - 1.f) * isc + g_ent * (isc + dldj * e));
+            lg[j] = g_lp * z * isc + g_ent * dldj;
+            lg[A + j] = sigmoidf(r) * (g_lp * (z * z - 1.f) * isc + g_ent * (isc + dldj * e));
         }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nr * 2 * A; k += PPO_TPB) {
+        const int r = k / (2 * A);
+        g_logits[(size_t)i0 * 2 * A + k] = s_lg[r * SL + (k - r * 2 * A)];
     }
     for (int o = 32; o > 0; o >>= 1) {
         spl += __shfl_down(spl, o, 64);
@@ -193,6 +217,8 @@ extern "C" int duck_ppo_loss(int N, int A, const float* logits, const float* raw
                              const float* eps, float clip_eps, float entropy_cost, int normalize_advantage,
                              float* out, float* grad_logits, float* grad_baseline, void* stream) {
     if (N <= 0 || A <= 0) return duck_fail(DUCK_EINVAL, "duck_ppo_loss: empty batch");
+    const size_t lds = sizeof(float) * PPO_TPB * (4 * A + 3);
+    if (lds > 64 * 1024) return duck_fail(DUCK_EINVAL, "duck_ppo_loss: action size too large");
     if (!logits || !raw_action || !old_logprob || !advantage || !value_target || !baseline || !eps || !out ||
         !grad_logits || !grad_baseline)
         return duck_fail(DUCK_EINVAL, "duck_ppo_loss: null pointer");
@@ -202,7 +228,7 @@ extern "C" int duck_ppo_loss(int N, int A, const float* logits, const float* raw
     float* partial = out + 6;
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(adv_stats_kernel, dim3(1), dim3(1024), 0, st, N, advantage, normalize_advantage, stats);
-    hipLaunchKernelGGL(ppo_loss_kernel, dim3(nblk), dim3(PPO_TPB), 0, st, N, A, logits, raw_action, old_logprob,
+    hipLaunchKernelGGL(ppo_loss_kernel, dim3(nblk), dim3(PPO_TPB), lds, st, N, A, logits, raw_action, old_logprob,
                        advantage, value_target, baseline, eps, clip_eps, entropy_cost, stats, partial, grad_logits,
                        grad_baseline);
     hipLaunchKernelGGL(ppo_loss_sum_kernel, dim3(1), dim3(1024), 0, st, N, nblk, partial, entropy_cost, out);

@@ -81,7 +81,7 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no
         inc = gen_dir
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
         [os.path.join(inc, f) for f in os.listdir(inc)] + \
-        [os.path.join(ROOT, "include", f) for f in ("duck.h", "duck_env.h", "duck_model.h")] + \
+        [os.path.join(ROOT, "include", f) for f in sorted(os.listdir(os.path.join(ROOT, "include"))) if f.endswith(".h")] + \
         [os.path.abspath(__file__)]  # the compile flags live here
     if not defines and not extra_flags and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
