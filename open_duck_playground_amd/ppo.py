@@ -178,10 +178,13 @@ class RunningStatistics(nn.Module):
     @torch.no_grad()
     def update(self, x: torch.Tensor) -> None:
         """Fold a batch [..., size] in (parallel-variance merge; one all-reduce across ranks)."""
-        x = x.reshape(-1, x.shape[-1]).to(torch.float64)
+        x = x.reshape(-1, x.shape[-1])
         k = x.shape[-1]
+        # sums accumulated in fp64 by the reductions themselves (no fp64 copy of the batch: a rollout
+        # batch is 163,840 rows, and the copies made this the slowest step of an update)
         stats = torch.cat([torch.full((1,), float(x.shape[0]), dtype=torch.float64, device=x.device),
-                           x.sum(0), (x * x).sum(0)])
+                           x.sum(0, dtype=torch.float64),
+                           torch.linalg.vector_norm(x, 2, dim=0, dtype=torch.float64) ** 2])
         if dist.is_available() and dist.is_initialized():
             dist.all_reduce(stats)
         n, s, ss = stats[0], stats[1:1 + k], stats[1 + k:]
