@@ -852,6 +852,7 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
     r.k1 = (uint32_t)A.is[(size_t)(Lo.rng_key + 1) * n + e];
     r.ctr = (uint32_t)A.is[(size_t)Lo.rng_ctr * n + e];
     step_env<Md, Col<0>, true>(A, e, lane, L, G, G, r, step_prefetch<Md>(A, e, lane));
+    STAGE_RESET();  // (no staged hot state to store: mark 15 counts nothing on this path)
   }
   STAGE_MARK(15);
 #ifdef DUCK_ANY_PROF
