@@ -1446,6 +1446,11 @@ static lspt ls_eval(const oracle_model* m, const fwd_ws* w, const sctx* c, const
   return p;
 }
 
+/* test aid (oracle_set_ls_floor): the HIP kernel's declared fp32 line-search stop,
+ * a bracket end whose slope is below floor x the starting slope; 0 (default) = MJX's rule alone */
+static _Thread_local double g_ls_floor;
+void oracle_set_ls_floor(double floor) { g_ls_floor = floor; }
+
 static void linesearch(const oracle_model* m, const oracle_data* d, const fwd_ws* w, sctx* c) {
   int nv = m->nv;
   double snorm = 0;
@@ -1469,6 +1474,7 @@ static void linesearch(const oracle_model* m, const oracle_data* d, const fwd_ws
   lspt lo = ls_eval(m, w, c, jv, qg, p0.alpha - p0.d0 / p0.d1);
   lspt hi;
   if (lo.d0 < p0.d0) { hi = p0; } else { hi = lo; lo = p0; }
+  if (g_ls_floor > 0 && g_ls_floor * fabs(p0.d0) > gtol) gtol = g_ls_floor * fabs(p0.d0);
   int swap = 1, iter = 0;
   for (;;) {
     int done = iter >= m->ls_iterations;

@@ -26,9 +26,7 @@ from tests.teacher_forcing import CASES, explain, explain_reset, run_case
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("case", list(CASES))
-def test_teacher_forced_step_parity(case, gpu):
-    rep = run_case(case, gpu, n=256, steps=6, keep_states=True)
+def _check(case, rep):
     s = rep.summary()
     print(case, {k: v for k, v in s.items()})
     # the reset itself, strictly: every fstate row, obs, privileged obs and istate word of every env
@@ -53,6 +51,18 @@ def test_teacher_forced_step_parity(case, gpu):
             if x["kind"] != "sensitive":
                 unexplained.append((t, int(e), x))
     assert not unexplained, unexplained
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_teacher_forced_step_parity(case, gpu):
+    _check(case, run_case(case, gpu, n=256, steps=6, keep_states=True))
+
+
+@pytest.mark.parametrize("case", ["rough_dr"])
+def test_teacher_forced_rough_long(case, gpu):
+    """The height-field scenes (C4, C5) at 1024 envs x 10 env-steps: 10,240 teacher-forced env-steps
+    each, at the same bar and with every outlier explained."""
+    _check(case, run_case(case, gpu, n=1024, steps=10, keep_states=True))
 
 
 def test_teacher_forced_paths_are_exercised(gpu):

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Locate teacher-forcing defects at substep resolution and dump what the GPU computed there.
 
-GPU: python tools/diag_tf_substep.py run <case> [max]   -> gpurun_out/diag_tf_<case>.npz
+GPU: python tools/diag_tf_substep.py run <case> [max] [envs] [steps] [thr]  -> gpurun_out/diag_tf_<case>.npz
 CPU: python tools/diag_tf_substep.py show <case>        (oracle forward at the same inputs)
 """
 import os
@@ -13,11 +13,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(case, mx=6):
+def run(case, mx=6, n=256, steps=6, thr=1e-3):
     import torch
     from tests.helpers import parse_aux
     from tests.teacher_forcing import _split, _state_rel, gpu_substep, oracle_substep, run_case, substep_trace
-    rep = run_case(case, "cuda:0", n=256, steps=6, keep_states=True)
+    rep = run_case(case, "cuda:0", n=n, steps=steps, keep_states=True)
     env, m = rep.env, rep.env.mj_model
     out = {"x": [], "aux": [], "env": [], "gnext": [], "rnext": [], "dr": []}
     for t, st in enumerate(rep.steps):
@@ -29,7 +29,7 @@ def run(case, mx=6):
             for s in range(env.n_substeps):
                 g = gpu_substep(env, int(e), x)
                 r = oracle_substep(om, x)
-                if _state_rel(m, g, r) > 1e-3:
+                if _state_rel(m, g, r) > thr:
                     n = env.num_envs
                     T = lambda y: torch.tensor(np.tile(y.astype(np.float32)[:, None], (1, n)), device=env.device).contiguous()  # noqa: E731
                     tq, tv, tw, tc = (T(y) for y in _split(m, x))
@@ -81,5 +81,5 @@ def show(case):
 
 
 if __name__ == "__main__":
-    {"run": lambda: run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 6),
+    {"run": lambda: run(sys.argv[2], *[f(a) for f, a in zip((int, int, int, float), sys.argv[3:])]),
      "show": lambda: show(sys.argv[2])}[sys.argv[1]]()
