@@ -1450,6 +1450,12 @@ static lspt ls_eval(const oracle_model* m, const fwd_ws* w, const sctx* c, const
  * a bracket end whose slope is below floor x the starting slope; 0 (default) = MJX's rule alone */
 static _Thread_local double g_ls_floor;
 void oracle_set_ls_floor(double floor) { g_ls_floor = floor; }
+/* test aid (oracle_set_force_start): 1 start the Newton solve from qacc_warmstart, 2 from qacc_smooth,
+ * 0 (default) the lower-cost one (mjx solver._init); for explaining a near-tie of the two costs */
+static _Thread_local int g_force_start;
+void oracle_set_force_start(int mode) { g_force_start = mode; }
+static _Thread_local double g_start_costs[2];
+void oracle_last_start_costs(double out[2]) { out[0] = g_start_costs[0]; out[1] = g_start_costs[1]; }
 
 static void linesearch(const oracle_model* m, const oracle_data* d, const fwd_ws* w, sctx* c) {
   int nv = m->nv;
@@ -1527,7 +1533,10 @@ static void solve(const oracle_model* m, oracle_data* d, const fwd_ws* w) {
   sctx warm, smth, *c;
   ctx_init(m, d, w, &warm, d->qacc_warmstart);
   ctx_init(m, d, w, &smth, d->qacc_smooth);
+  g_start_costs[0] = warm.cost;
+  g_start_costs[1] = smth.cost;
   c = warm.cost < smth.cost ? &warm : &smth;
+  if (g_force_start) c = g_force_start == 1 ? &warm : &smth; /* test aid */
   update_gradient(m, d, w, c);
   for (int i = 0; i < nv; i++) c->search[i] = -c->Mgrad[i];
   int it = 0;

@@ -78,6 +78,8 @@ int oracle_hfield_prisms(const oracle_model* m, const oracle_data* d, int g_hf, 
 void oracle_hfield_axis_wins(long long out[14], int reset);
 void oracle_set_trace(double* buf); /* test aid: record substep inputs of oracle_env_step */
 void oracle_set_ls_floor(double floor); /* test aid: the HIP line search's fp32 stop rule (0 = off) */
+void oracle_set_force_start(int mode);  /* test aid: Newton start 1 warm, 2 smooth, 0 the cheaper */
+void oracle_last_start_costs(double out[2]); /* test aid: costs at qacc_warmstart, qacc_smooth */
 int oracle_env_step(const oracle_model* m, const duck_env_config* cfg, const duck_refmotion* ref,
                     double* fstate, int32_t* istate, const double* action, double* obs, double* priv,
                     double* reward, double* done, oracle_data* d_out);

@@ -82,6 +82,8 @@ def lib():
                                       dp, C.POINTER(OracleData)]
         L.oracle_set_trace.argtypes = [dp]
         L.oracle_set_ls_floor.argtypes = [C.c_double]
+        L.oracle_set_force_start.argtypes = [C.c_int]
+        L.oracle_last_start_costs.argtypes = [C.POINTER(C.c_double)]
         L.oracle_hfield_axis_wins.argtypes = [C.POINTER(C.c_longlong), C.c_int]
         L.oracle_hfield_prisms.argtypes = [vp, C.POINTER(OracleData), C.c_int, C.c_int, C.c_int, dp, dp, dp, ip]
         L.oracle_reference_motion.argtypes = [C.POINTER(DuckRefMotion), C.c_double, C.c_double, C.c_double, C.c_int, dp]
