@@ -704,6 +704,12 @@ void oracle_hfield_axis_wins(long long out[14], int reset) {
   for (int i = 0; i < 14; i++) { out[i] = hf_axis_wins[i]; if (reset) hf_axis_wins[i] = 0; }
 }
 
+/* test aid (oracle_set_hf_tie_last): a prism's overlaps within this band of the minimum resolve to the
+ * LAST such axis of the priority order (0, default: the first, the declared rule). Used to explain an
+ * fp32 near-tie of two separating axes: the kernel's fp32 overlaps may order them the other way. */
+static _Thread_local double g_hf_tie_last;
+void oracle_set_hf_tie_last(double band) { g_hf_tie_last = band; }
+
 /* the hull in the local frame (the height field's axes, origin at the hull's frame) */
 typedef struct {
   int nv, nf, ne;
@@ -831,6 +837,9 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
   }
   int w = 0;
   while (ov[w] > mn) w++;
+  if (g_hf_tie_last > 0) /* test aid: the last axis within the tie band instead of the first */
+    for (int i = 0; i < na; i++)
+      if (ov[i] <= mn + g_hf_tie_last) w = i;
   {
     /* which class of axis won (hf_axis_wins: prism top, sides, bottom, hull faces, top-edge,
      * vertical-edge, bottom-edge pairs) */
@@ -1231,6 +1240,12 @@ static void collide_convex_convex(const oracle_model* m, oracle_data* d, int g1,
   }
 }
 
+/* test aid (oracle_set_con_override): after collision, every slot s takes dist buf[7s], pos
+ * buf[7s+1..3] and the frame of normal buf[7s+4..6] (a contact set computed elsewhere, e.g. the
+ * kernel's), so that the rest of the substep can be compared from identical contacts; NULL = off */
+static _Thread_local const double* g_con_override;
+void oracle_set_con_override(const double* buf) { g_con_override = buf; }
+
 static void collision(const oracle_model* m, oracle_data* d) {
   d->ncon = m->npair * DUCK_CON_PER_PAIR;
   for (int p = 0; p < m->npair; p++) {
@@ -1398,6 +1413,12 @@ static void update_constraint(const oracle_model* m, const oracle_data* d, const
   c->cost = gauss + cost;
 }
 
+/* test aid (oracle_set_hdump): buf[0] = nefc, buf[1..NV*NV] the first Newton Hessian (row stride NV) of
+ * the next solve, then per row (Jaref, |J||qacc| + |aref|, friction band R*f or 0) at that point */
+static _Thread_local double* g_hdump;
+static _Thread_local int g_hdump_done;
+void oracle_set_hdump(double* buf) { g_hdump = buf; g_hdump_done = 0; }
+
 /* _update_gradient (Newton): grad and H^-1 grad with H = M + J' diag(D*active) J */
 static void update_gradient(const oracle_model* m, const oracle_data* d, const fwd_ws* w, sctx* c) {
   int nv = m->nv;
@@ -1415,6 +1436,18 @@ static void update_gradient(const oracle_model* m, const oracle_data* d, const f
       if (w->J[r][i] == 0) continue;
       double a = w->D[r] * w->J[r][i];
       for (int j = 0; j < nv; j++) H[i * NV + j] += a * w->J[r][j];
+    }
+  }
+  if (g_hdump && !g_hdump_done) { /* test aid: the first Newton Hessian and the rows' margins at its point */
+    g_hdump_done = 1;
+    g_hdump[0] = w->nefc;
+    memcpy(g_hdump + 1, H, sizeof(double) * NV * NV);
+    for (int r = 0; r < w->nefc; r++) {
+      double sc = fabs(w->aref[r]);
+      for (int i = 0; i < nv; i++) sc += fabs(w->J[r][i] * c->qacc[i]);
+      g_hdump[1 + NV * NV + 3 * r] = c->Jaref[r];
+      g_hdump[2 + NV * NV + 3 * r] = sc;
+      g_hdump[3 + NV * NV + 3 * r] = w->ineq[r] ? 0 : w->R[r] * w->frictionloss[r];
     }
   }
   cholesky(H, nv);
@@ -1632,6 +1665,13 @@ static void forward_ws(const oracle_model* m, oracle_data* d, fwd_ws* w) {
   com_pos(m, d, w);
   crb(m, d, w);
   collision(m, d);
+  if (g_con_override)
+    for (int c = 0; c < d->ncon; c++) {
+      const double* o = g_con_override + 7 * c;
+      d->con_dist[c] = o[0];
+      memcpy(d->con_pos[c], o + 1, 3 * sizeof(double));
+      make_frame(d->con_frame[c], o + 4);
+    }
   make_constraint(m, d, w);
   com_vel(m, d, w);
   sensors(m, d, w, 0);

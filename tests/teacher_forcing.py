@@ -308,6 +308,24 @@ def oracle_substep(om, x: np.ndarray) -> np.ndarray:
                            d.arr("ctrl", m.nu)])
 
 
+def oracle_substep_with_contacts(om, x: np.ndarray, ga: dict) -> np.ndarray:
+    """oracle_substep with the contact set replaced, after collision, by the GPU's (parse_aux dict ga
+    of one env: con_dist, con_pos, con_normal; oracle_set_con_override)."""
+    import ctypes as C
+    from tests.oracle_ffi import lib
+    ncon = 4 * om.m.npair
+    buf = np.zeros((ncon, 7))
+    buf[:, 0] = ga["con_dist"][0][:ncon]
+    buf[:, 1:4] = np.asarray(ga["con_pos"][0]).reshape(-1, 3)[:ncon]
+    buf[:, 4:7] = np.asarray(ga["con_normal"][0]).reshape(-1, 3)[:ncon]
+    buf = np.ascontiguousarray(buf.ravel())
+    lib().oracle_set_con_override(buf.ctypes.data_as(C.POINTER(C.c_double)))
+    try:
+        return oracle_substep(om, x)
+    finally:
+        lib().oracle_set_con_override(None)
+
+
 def _state_rel(m, a, b):
     """max relative error over qvel and qacc (qacc_warmstart) of two trace rows."""
     sl = slice(m.nq, m.nq + 2 * m.nv)
@@ -340,9 +358,14 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     one of the kernel's declared fp32 behaviours, or None:
     "ls_floor": the oracle with the kernel's line-search stop (slope below 1e-6 of the start; DESIGN.md
     §5 item 7) lands on the GPU's result (within sub_tol);
+    "sat_tie": the oracle resolving height-field SAT near-ties (overlaps within 1e-6 m of the minimum)
+    to the last tied axis instead of the first lands on the GPU's result -- two separating axes of one
+    prism tie below fp32 resolution and the kernel ordered them the other way;
     "onset": the two contact sets differ only in slots that are, on each side, inactive or active
     within `onset` (m) of zero depth -- which prisms of a height field touch at the onset is decided
     below fp32 resolution;
+    "onset_cascade": every pair whose slots differ holds an active contact at the onset depth on
+    either side, and the oracle continued from the GPU's contact set lands on the GPU's result;
     "conditioning": the oracle's own substep moves by at least the GPU's difference (median over random
     1e-6 relative input perturbations): the state amplifies fp32-sized differences that much."""
     from tests.helpers import parse_aux
@@ -355,6 +378,15 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
         lib().oracle_set_ls_floor(0.0)
     if _state_rel(m, g, r) <= sub_tol:
         return "ls_floor"
+    # a height-field prism whose two best separating axes overlap within 1e-6 m of each other (fp32's
+    # resolution of the overlaps): the oracle resolving such ties to the other axis lands on the GPU
+    lib().oracle_set_hf_tie_last(1e-6)
+    try:
+        r = oracle_substep(om, x)
+    finally:
+        lib().oracle_set_hf_tie_last(0.0)
+    if _state_rel(m, g, r) <= sub_tol:
+        return "sat_tie"
     n = env.num_envs
     T = lambda y: torch.tensor(np.tile(y.astype(np.float32)[:, None], (1, n)), device=env.device).contiguous()  # noqa: E731
     tq, tv, tw, tc = (T(y) for y in _split(m, x))
@@ -372,6 +404,17 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     at_onset = ((gd >= 0) | (np.abs(gd) <= onset)) & ((od >= 0) | (np.abs(od) <= onset))
     if differ.any() and at_onset[differ].all():
         return "onset"
+    # an onset-depth prism's cascade: every pair whose slots differ holds, on either side, an active
+    # contact at the onset depth (its penetration-weighted point has ~onset weights, so fp32 and fp64
+    # place it centimetres apart and _manifold_points picks differently from there), and the oracle
+    # continued from the GPU's own contact set lands on the GPU's result (everything after collision
+    # agrees; the difference is the manifold's choice at the onset)
+    pair_differs = differ.reshape(m.npair, 4).any(axis=1)
+    pair_onset = (((gd < 0) & (np.abs(gd) <= onset)) |
+                  ((od < 0) & (np.abs(od) <= onset))).reshape(m.npair, 4).any(axis=1)
+    if pair_differs.any() and pair_onset[pair_differs].all() and \
+            _state_rel(m, g, oracle_substep_with_contacts(om, x, ga)) <= sub_tol:
+        return "onset_cascade"
     # the state's own conditioning: the oracle's substep moves, under random 1e-6 relative input
     # perturbations (flip_level's fp32-sized level), by a median at least the GPU's difference
     r0 = oracle_substep(om, x)

@@ -58,9 +58,7 @@ def test_teacher_forced_step_parity(case, gpu):
     _check(case, run_case(case, gpu, n=256, steps=6, keep_states=True))
 
 
-@pytest.mark.parametrize("case", ["rough_dr", pytest.param("rough_backlash_dr", marks=pytest.mark.xfail(
-    reason="2 of 27 outliers in 10,240 env-steps not explained by the automatic rules (DESIGN.md §5: an "
-           "onset-prism manifold cascade, and one Newton step that differs at identical contacts)", strict=False))])
+@pytest.mark.parametrize("case", ["rough_dr", "rough_backlash_dr"])
 def test_teacher_forced_rough_long(case, gpu):
     """The height-field scenes (C4, C5) at 1024 envs x 10 env-steps: 10,240 teacher-forced env-steps
     each, at the same bar and with every outlier explained."""
