@@ -70,8 +70,23 @@ def build(verbose: bool = False, defines=(), out: str = None, extra_flags=(), no
 
     One translation unit per model variant (variant_*.hip) plus the C ABI (duck_capi.hip),
     compiled in parallel and linked into one shared library. ``gen_dir`` (model_library) holds
-    the units, headers and variant registry of other models instead of the four shipped scenes."""
+    the units, headers and variant registry of other models instead of the four shipped scenes.
+    One builder per output at a time (torchrun ranks importing the package together): the others
+    wait on a file lock and then find the library fresh, so N ranks run one hipcc build, not N."""
+    import fcntl
     out = os.path.abspath(out or LIB_PATH)
+    os.makedirs(BUILD, exist_ok=True)
+    with open(os.path.join(BUILD, os.path.basename(out) + ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        try:
+            # the freshness check runs under the lock: a rank never scans a library another rank
+            # is still replacing
+            return _build_unlocked(verbose, defines, out, extra_flags, no_ilp, isa_check, gen_dir)
+        finally:
+            fcntl.flock(lock, fcntl.LOCK_UN)
+
+
+def _build_unlocked(verbose, defines, out, extra_flags, no_ilp, isa_check, gen_dir) -> str:
     if gen_dir is None:
         srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
         inc = os.path.join(CSRC, "generated")

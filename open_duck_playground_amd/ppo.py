@@ -274,6 +274,14 @@ class _FusedLoss(torch.autograd.Function):
         lg, ra, olp, ad, v, bl, ep = args
         A = ra.shape[-1]
         N = ra.numel() // A
+        # the kernel indexes every operand by (N, A) unchecked: a mismatch must be an error here,
+        # not an out-of-bounds device read (the torch expression would raise on it too)
+        if A < 1 or lg.shape[-1] != 2 * A or lg.numel() != 2 * N * A or ep.numel() != N * A:
+            raise ValueError(f"fused PPO loss: logits {tuple(lg.shape)} / eps {tuple(ep.shape)} do not match "
+                             f"raw_action {tuple(ra.shape)} (N={N}, A={A})")
+        for name, t in (("old_logprob", olp), ("adv", ad), ("vs", v), ("baseline", bl)):
+            if t.numel() != N:
+                raise ValueError(f"fused PPO loss: {name} holds {t.numel()} values, expected N={N}")
         out = torch.empty(lib().duck_ppo_loss_out_size(N), dtype=torch.float32, device=lg.device)  # + scratch
         g_lg, g_bl = torch.empty_like(lg), torch.empty_like(bl)
         check(lib().duck_ppo_loss(N, A, lg.data_ptr(), ra.data_ptr(), olp.data_ptr(), ad.data_ptr(), v.data_ptr(),

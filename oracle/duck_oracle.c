@@ -695,20 +695,23 @@ static void collide_plane_convex(const oracle_model* m, oracle_data* d, int g1, 
  * shape's vertices within HF_WITNESS_BAND of its support plane along the normal, weighted 1 at the
  * plane to 0 at the band edge; the prism's top vertices only). */
 #define HF_WITNESS_BAND 1e-3 /* m; = TPhys HF_WITNESS_BAND */
+#define HF_TIE_BAND 1e-4     /* m; = TPhys HF_TIE_BAND: the second-smallest overlap within this of the smallest blends its axis into the normal */
+#define HF_POINT_BAND 1e-4   /* m; = TPhys HF_POINT_BAND: a total penetration weight below this blends the point towards the support midpoint */
 #define HF_DEPTH_TIE 1e-6    /* m; = TPhys HF_DEPTH_TIE: prisms sharing a grid vertex or edge often tie exactly */
 #define HF_MAXPRISM 128      /* prisms under one hull (the sub-grid of a 0.11 m foot: <= 18) */
 
 /* test aid: how often each class of separating axis gave a prism's penetration (oracle_hfield_axis_wins) */
-static long long hf_axis_wins[14];
-void oracle_hfield_axis_wins(long long out[14], int reset) {
-  for (int i = 0; i < 14; i++) { out[i] = hf_axis_wins[i]; if (reset) hf_axis_wins[i] = 0; }
+static long long hf_axis_wins[17];
+void oracle_hfield_axis_wins(long long out[17], int reset) {
+  for (int i = 0; i < 17; i++) { out[i] = hf_axis_wins[i]; if (reset) hf_axis_wins[i] = 0; }
 }
 
-/* test aid (oracle_set_hf_tie_last): a prism's overlaps within this band of the minimum resolve to the
- * LAST such axis of the priority order (0, default: the first, the declared rule). Used to explain an
- * fp32 near-tie of two separating axes: the kernel's fp32 overlaps may order them the other way. */
-static _Thread_local double g_hf_tie_last;
-void oracle_set_hf_tie_last(double band) { g_hf_tie_last = band; }
+
+/* test aid (oracle_set_hf_band_scale): scales HF_TIE_BAND and HF_POINT_BAND (default 1; 0 = the exact
+ * SAT's axis and the plain weighted centroid). Only the brute-force check of the prism SAT's depth and
+ * axis (tools/hfield_deviation.py, blend=False) turns the blend off. */
+static _Thread_local double g_hf_band_scale = 1.0;
+void oracle_set_hf_band_scale(double s) { g_hf_band_scale = s; }
 
 /* the hull in the local frame (the height field's axes, origin at the hull's frame) */
 typedef struct {
@@ -835,26 +838,61 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
     }
     return 0;
   }
+  /* the smallest overlap (the first axis in priority order among equal ones) and the second smallest
+   * (likewise, over the other axes) */
   int w = 0;
-  while (ov[w] > mn) w++;
-  if (g_hf_tie_last > 0) /* test aid: the last axis within the tie band instead of the first */
-    for (int i = 0; i < na; i++)
-      if (ov[i] <= mn + g_hf_tie_last) w = i;
+  while (w < na - 1 && ov[w] > mn) w++;
+  int w2 = -1;
+  for (int i = 0; i < na; i++)
+    if (i != w && (w2 < 0 || ov[i] < ov[w2])) w2 = i;
   {
     /* which class of axis won (hf_axis_wins: prism top, sides, bottom, hull faces, top-edge,
-     * vertical-edge, bottom-edge pairs) */
+     * vertical-edge, bottom-edge pairs); 14-16: prisms with a second / third axis inside the tie band */
     int cls = w == 0 ? 0 : (w < 4 ? 1 : (w == 4 ? 2 : (w < 5 + H->nf ? 3 : 4)));
     if (cls == 4) cls = 4 + kind_of_axis[w];
+    int inband = 0;
+    for (int i = 0; i < na; i++) inband += ov[i] < mn + HF_TIE_BAND * g_hf_band_scale;
 #ifdef _OPENMP
 #pragma omp atomic
 #endif
     hf_axis_wins[cls]++;
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+    hf_axis_wins[14]++;
+    if (inband >= 2) {
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+      hf_axis_wins[15]++;
+    }
+    if (inband >= 3) {
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+      hf_axis_wins[16]++;
+    }
   }
-  const double* u = ax[w];
-  /* the contact point: the centroid of the vertices of each shape inside the other (hull
-   * vertices inside the prism, prism top vertices inside the hull), each weighted by its
-   * penetration (distance to the nearest face of the other shape); when no vertex is inside
-   * (crossing edges), the midpoint of the two shapes' support features along u */
+  /* the normal: the smallest overlap's axis, blended with the second smallest's by a weight that
+   * falls linearly from 1 at equal overlaps to 0 at HF_TIE_BAND apart (declared):
+   * the exact SAT's normal jumps between two axes whose overlaps cross, which fp32 and fp64 decide
+   * differently within ~1e-7 m; the blend is continuous there, and is the exact SAT's axis whenever
+   * no other axis comes within the band */
+  double u[3];
+  {
+    const double band = HF_TIE_BAND * g_hf_band_scale;
+    const double beta = w2 < 0 || band <= 0 ? 0.0 : fmax(0.0, 1.0 - (ov[w2] - ov[w]) / band);
+    for (int a = 0; a < 3; a++) u[a] = ax[w][a] + (beta > 0 ? beta * ax[w2][a] : 0.0);
+    const double un = norm3(u);
+    for (int a = 0; a < 3; a++) u[a] = un > 1e-9 ? u[a] / un : ax[w][a];
+  }
+  /* the contact point: the centroid of the vertices of each shape inside the other (hull vertices
+   * inside the prism, prism top vertices inside the hull), each weighted by its penetration (distance
+   * to the nearest face of the other shape), blended towards the midpoint of the two shapes' support
+   * features along u when the total weight W is below HF_POINT_BAND: pos = C / W for W >= band, else
+   * C / band + (1 - W / band) mid (continuous at W = band; mid alone when no vertex is inside, i.e.
+   * crossing edges). The plain centroid of ~1e-7 m weights is ill-conditioned: fp32 and fp64 put an
+   * onset prism's point centimetres apart. */
   double wsum = 0, c[3] = {0, 0, 0};
   const double ptop = dot3(nt, T[0]);
   for (int k = 0; k < H->nv; k++) {
@@ -868,7 +906,8 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
     for (int f = 0; f < H->nf; f++) pen = fmin(pen, m->hull_face_offset[f] - dot3(H->FN[f], T[j]));
     if (pen > 0) { wsum += pen; for (int a = 0; a < 3; a++) c[a] += pen * T[j][a]; }
   }
-  if (wsum > 0) {
+  const double pband = HF_POINT_BAND * g_hf_band_scale;
+  if (wsum > 0 && wsum >= pband) {
     for (int a = 0; a < 3; a++) pos[a] = c[a] / wsum;
   } else {
     const double hmin = pts_min(u, (const double(*)[3])H->V, H->nv), pmax = pts_max(u, T, 3);
@@ -883,10 +922,12 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
       wp += wk;
       for (int a = 0; a < 3; a++) cp[a] += wk * T[k][a];
     }
-    for (int a = 0; a < 3; a++) pos[a] = 0.5 * (ch[a] / wh + cp[a] / wp);
+    /* (wsum == 0 when the band is off: the midpoint alone) */
+    const double f = pband > 0 ? 1.0 - wsum / pband : 1.0;
+    for (int a = 0; a < 3; a++) pos[a] = (pband > 0 ? c[a] / pband : 0.0) + f * 0.5 * (ch[a] / wh + cp[a] / wp);
   }
   memcpy(u_out, u, sizeof(double) * 3);
-  *depth = ov[w];
+  *depth = mn;
   return 1;
 }
 
@@ -2131,7 +2172,7 @@ int oracle_env_reset(const oracle_model* m, const duck_env_config* cfg, const du
   return 0;
 }
 
-/* test aid (tools/tf_outliers.py): when set, oracle_env_step on this thread records every substep's
+/* test aid (tests/teacher_forcing.py substep_trace): when set, oracle_env_step on this thread records every substep's
  * input state (qpos, qvel, qacc_warmstart, ctrl) into the buffer, n_substeps records */
 static _Thread_local double* g_trace;
 void oracle_set_trace(double* buf) { g_trace = buf; }

@@ -21,12 +21,13 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional
 
 import numpy as np
 import torch
 
 from open_duck_playground_amd.joystick import Joystick, domain_randomize, wrap_for_brax_training
+from open_duck_playground_amd.mjcf import Hull, Model
 from tests.oracle_ffi import OracleBatch, OracleModel
 
 # per-env error = max over a field group of |gpu - oracle| / (1 + |oracle|)
@@ -97,7 +98,9 @@ def _fs_err(L, fa, fb, n):
 def run(task: str, imitation: bool, n: int, steps: int, device, seed: int = 7, dr: bool = False,
         auto_reset: bool = False, episode_length: int = 1000, overrides: Optional[dict] = None,
         force_push: bool = False, force_resample: bool = False, env_cls=Joystick, action_seed: int = 0,
-        keep_states: bool = False) -> Report:
+        keep_states: bool = False, oracle_edit: Optional[Callable[[Model], Model]] = None) -> Report:
+    """``oracle_edit`` hands the oracle a deliberately wrong model (a copy of the GPU's, edited; the
+    GPU keeps the nominal one): the injected-defect test of ``explain`` (DEFECTS)."""
     kw = {} if env_cls is not Joystick else {"use_imitation": imitation}
     env = env_cls(task, num_envs=n, device=device, config_overrides=overrides, **kw)
     if auto_reset:
@@ -106,8 +109,9 @@ def run(task: str, imitation: bool, n: int, steps: int, device, seed: int = 7, d
     elif dr:
         domain_randomize(env, rng=seed + 1)
     st = env.reset(rng=seed)
-    base = OracleModel(env.mj_model)
-    models = [OracleModel(env.mj_model, dr=base.dr_sample(seed + 1, e)) for e in range(n)] if dr else base
+    om_model = oracle_edit(copy_model(env.mj_model)) if oracle_edit is not None else env.mj_model
+    base = OracleModel(om_model)
+    models = [OracleModel(om_model, dr=base.dr_sample(seed + 1, e)) for e in range(n)] if dr else base
     cfg = env._cfg_struct                      # the exact struct duck_create received
     L = env._layout
     ob = OracleBatch(models, cfg, n)
@@ -245,6 +249,43 @@ CASES = {
 }
 
 
+def copy_model(m: Model) -> Model:
+    return Model(name=m.name, arrays={k: v.copy() for k, v in m.arrays.items()}, names=dict(m.names),
+                 hulls=[Hull(vert=h.vert.copy(), face_normal=h.face_normal.copy(), face_offset=h.face_offset.copy(),
+                             face_vert=[list(f) for f in h.face_vert], edge=h.edge.copy()) for h in m.hulls])
+
+
+def _floor_friction(m: Model) -> Model:      # the contact pairs' sliding friction x 1.02
+    m.arrays["pair_friction"][:, :2] *= 1.02
+    return m
+
+
+def _one_kp(m: Model) -> Model:              # the left knee servo's kp x 1.005
+    m.arrays["actuator_kp"][3] *= 1.005
+    return m
+
+
+def _solref(m: Model) -> Model:              # the contact pairs' solref time constant x 1.02
+    m.arrays["pair_solref"][:, 0] *= 1.02
+    return m
+
+
+def _foot_hull(m: Model) -> Model:           # the foot hull scaled by 1.0005 about its mesh origin (~25 um)
+    m.hulls = [Hull(vert=h.vert * 1.0005, face_normal=h.face_normal, face_offset=h.face_offset * 1.0005,
+                    face_vert=h.face_vert, edge=h.edge) for h in m.hulls]
+    return m
+
+
+# injected defects (name -> (case, oracle model edit)): the oracle runs a deliberately wrong model
+# while the GPU runs the nominal one, so every outlier IS a defect and explain() must say so
+DEFECTS = {
+    "floor_friction_x1.02": ("flat", _floor_friction),
+    "actuator_kp_x1.005": ("flat", _one_kp),
+    "contact_solref_x1.02": ("flat", _solref),
+    "foot_hull_x1.0005_hfield": ("rough_dr", _foot_hull),
+}
+
+
 def run_case(name: str, device, n: int = 256, steps: int = 6, **extra) -> Report:
     kw = dict(CASES[name], **extra)
     if kw.pop("standing", False):
@@ -349,6 +390,36 @@ def flip_level(om, x: np.ndarray, target: np.ndarray, rng, levels=(1e-6, 1e-5)) 
     return None
 
 
+def backward_error_landing(om, x: np.ndarray, target: np.ndarray, level: float = 1e-6) -> Optional[dict]:
+    """Backward error of the GPU's substep: is there an input within `level` of x -- every qpos,
+    qvel and qacc_warmstart coordinate moved by at most level * |x_i| + 1e-3 level, the size
+    flip_level perturbs by -- from which the oracle's substep lands on target (closer than a quarter
+    of the unperturbed distance)? Found by a bounded least-squares fit of target - f(x) to the
+    oracle's finite-difference Jacobian (one column per input coordinate), then checked by running
+    the oracle at the fitted input (the landing is real, not a linear prediction). A continuous
+    sensitivity of the state (no branch flips) passes it; a model defect -- a systematic force error
+    no fp32-sized input change produces -- does not (test_explain_has_teeth). Returns the fit or None."""
+    from scipy.optimize import lsq_linear
+    m = om.m
+    k = m.nq + 2 * m.nv
+    sl = slice(m.nq, m.nq + 2 * m.nv)
+    base = oracle_substep(om, x)
+    d0 = _state_rel(m, base, target)
+    h = level * np.abs(x[:k]) + 1e-3 * level
+    J = np.empty((2 * m.nv, k))
+    for i in range(k):
+        y = x.copy()
+        y[i] += h[i]
+        J[:, i] = oracle_substep(om, y)[sl] - base[sl]
+    fit = lsq_linear(J, target[sl] - base[sl], bounds=(-1.0, 1.0))
+    y = x.copy()
+    y[:k] += fit.x * h
+    d = _state_rel(m, oracle_substep(om, y), target)
+    if d < 0.25 * d0:
+        return {"landed": d, "unperturbed": d0, "max_coord": float(np.abs(fit.x).max())}
+    return None
+
+
 def _contacts(m, dist, pos):
     return np.asarray(dist, dtype=np.float64)[:4 * m.npair], np.asarray(pos, dtype=np.float64).reshape(-1, 3)[:4 * m.npair]
 
@@ -358,16 +429,16 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     one of the kernel's declared fp32 behaviours, or None:
     "ls_floor": the oracle with the kernel's line-search stop (slope below 1e-6 of the start; DESIGN.md
     §5 item 7) lands on the GPU's result (within sub_tol);
-    "sat_tie": the oracle resolving height-field SAT near-ties (overlaps within 1e-6 m of the minimum)
-    to the last tied axis instead of the first lands on the GPU's result -- two separating axes of one
-    prism tie below fp32 resolution and the kernel ordered them the other way;
+    "backward_error": the oracle from an input within 1e-6 of the GPU's input lands on the GPU's result
+    (backward_error_landing: the kernel's fp32 substep is the exact substep of a nearby input);
     "onset": the two contact sets differ only in slots that are, on each side, inactive or active
     within `onset` (m) of zero depth -- which prisms of a height field touch at the onset is decided
-    below fp32 resolution;
-    "onset_cascade": every pair whose slots differ holds an active contact at the onset depth on
-    either side, and the oracle continued from the GPU's contact set lands on the GPU's result;
-    "conditioning": the oracle's own substep moves by at least the GPU's difference (median over random
-    1e-6 relative input perturbations): the state amplifies fp32-sized differences that much."""
+    below fp32 resolution.
+    (Round 3's "sat_tie" and "onset_cascade" rules -- the oracle re-run with the other tied SAT axis,
+    or continued from the GPU's own contact set -- are gone: round 4's contact model is continuous at
+    SAT ties and onset prisms. Round 3's "conditioning" rule -- the oracle merely moving by the GPU's difference under 1e-6
+    perturbations, without landing on it -- is gone: a rule that does not require landing cannot tell
+    a defect from a sensitive state, tests/test_gpu_teacher_forced.py::test_explain_has_teeth.)"""
     from tests.helpers import parse_aux
     from tests.oracle_ffi import lib
     m = om.m
@@ -378,15 +449,9 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
         lib().oracle_set_ls_floor(0.0)
     if _state_rel(m, g, r) <= sub_tol:
         return "ls_floor"
-    # a height-field prism whose two best separating axes overlap within 1e-6 m of each other (fp32's
-    # resolution of the overlaps): the oracle resolving such ties to the other axis lands on the GPU
-    lib().oracle_set_hf_tie_last(1e-6)
-    try:
-        r = oracle_substep(om, x)
-    finally:
-        lib().oracle_set_hf_tie_last(0.0)
-    if _state_rel(m, g, r) <= sub_tol:
-        return "sat_tie"
+    # backward error: the oracle from an fp32-sized perturbation of the input lands on the GPU's result
+    if backward_error_landing(om, x, g) is not None:
+        return "backward_error"
     n = env.num_envs
     T = lambda y: torch.tensor(np.tile(y.astype(np.float32)[:, None], (1, n)), device=env.device).contiguous()  # noqa: E731
     tq, tv, tw, tc = (T(y) for y in _split(m, x))
@@ -404,32 +469,19 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     at_onset = ((gd >= 0) | (np.abs(gd) <= onset)) & ((od >= 0) | (np.abs(od) <= onset))
     if differ.any() and at_onset[differ].all():
         return "onset"
-    # an onset-depth prism's cascade: every pair whose slots differ holds, on either side, an active
-    # contact at the onset depth (its penetration-weighted point has ~onset weights, so fp32 and fp64
-    # place it centimetres apart and _manifold_points picks differently from there), and the oracle
-    # continued from the GPU's own contact set lands on the GPU's result (everything after collision
-    # agrees; the difference is the manifold's choice at the onset)
-    pair_differs = differ.reshape(m.npair, 4).any(axis=1)
-    pair_onset = (((gd < 0) & (np.abs(gd) <= onset)) |
-                  ((od < 0) & (np.abs(od) <= onset))).reshape(m.npair, 4).any(axis=1)
-    if pair_differs.any() and pair_onset[pair_differs].all() and \
-            _state_rel(m, g, oracle_substep_with_contacts(om, x, ga)) <= sub_tol:
-        return "onset_cascade"
-    # the state's own conditioning: the oracle's substep moves, under random 1e-6 relative input
-    # perturbations (flip_level's fp32-sized level), by a median at least the GPU's difference
-    r0 = oracle_substep(om, x)
-    err = _state_rel(m, g, r0)
-    rng = np.random.default_rng(1)
-    k = m.nq + 2 * m.nv
-    moved = []
-    for _ in range(24):
-        y = x.copy()
-        y[:k] *= 1 + 1e-6 * rng.choice([-1.0, 1.0], size=k)
-        y[:k] += 1e-9 * rng.choice([-1.0, 1.0], size=k)
-        moved.append(_state_rel(m, oracle_substep(om, y), r0))
-    if float(np.median(moved)) >= err:
-        return "conditioning"
     return None
+
+
+def rule_of(x: dict) -> List[str]:
+    """The rules an explain() result used: one per flipped substep ("flip1e-06", "ls_floor", ...),
+    plus "gpu_flip1e-07" when step_kernel's result needed the chain ensemble, or ["agree"] when every
+    substep agreed to sub_tol; ["defect"] for a defect."""
+    if x["kind"] != "sensitive":
+        return ["defect"]
+    out = [lev if isinstance(lev, str) else f"flip{lev:.0e}" for _, lev in x.get("flips", [])]
+    if "gpu_flip" in x:
+        out.append(f"gpu_flip{x['gpu_flip'][0]:.0e}")
+    return out or ["agree"]
 
 
 def gpu_chain_ensemble(env, e: int, x: np.ndarray, rel: float, seed: int = 0) -> np.ndarray:

@@ -159,9 +159,10 @@ def test_env_offset_shards_are_bit_identical(gpu):
     assert torch.equal(torch.cat([s.reward for s in sp]), sf.reward)
 
 
-@pytest.mark.parametrize("cfg", ["C2", "C4", "C5"])
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C4", "C5"])
 def test_full_size_runs_are_deterministic(cfg, gpu):
-    """At the bench's sizes (C2 4096 flat, C4 8192 rough + DR, C5 4096 rough + DR + backlash), two
+    """At the bench's sizes (C2 4096 flat, C3 4096 flat + imitation, C4 8192 rough + DR, C5 4096
+    rough + DR + backlash), two
     runs from the same seeds give bit-identical obs, privileged obs, rewards and dones: no races
     between the team's lanes or the workgroup's staging, no order-dependent reductions."""
     from bench import CONFIGS

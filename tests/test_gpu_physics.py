@@ -217,8 +217,9 @@ def test_hfield_prism_contacts_match_oracle(task, height, gpu):
 def test_hfield_kernel_matches_brute_force_prisms(task, gpu):
     """The kernel's height-field contacts against the brute-force prism reference (every axis of
     every prism, fp64; tools/hfield_deviation.py --gpu) at oracle rollout states of rough + DR: the
-    feet's contact flags agree, the deepest depth to fp32 (1e-6 m at p99) and its normal to 0.1 deg
-    at p99 (fp32 ties of equal-depth prisms aside)."""
+    feet's contact flags agree, the deepest depth to fp32 (1e-6 m at p99), and its normal -- the
+    declared tie-band blend of the two smallest overlaps' axes -- the oracle's to 0.1 deg at p99
+    (fp32 ties of equal-depth prisms aside)."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))

@@ -13,15 +13,18 @@ branch the oracle also takes under a 1e-6/1e-5 input perturbation; and that subs
 reproduces step_kernel's own result for the env-step). The reset before step 0 is compared
 strictly: every fstate row (incl. the auto-reset snapshot), obs, privileged obs and istate word of
 every env at the same bar (teacher_forcing.reset_stats), >= 99.5 % of envs, the rest explained as a
-contact branch of the reset's forward (explain_reset). Measured on MI355X: median
-errors 1e-7 (qpos) .. 4e-6 (obs), p99 <= 3e-4, at most 2 outliers in 1536 env-steps per case, all
-explained (tools/tf_outliers.py).
+contact branch of the reset's forward (explain_reset). Every case prints how many outliers each
+explanation rule accepted ("rules:"; teacher_forcing.rule_of), and test_explain_has_teeth shows the
+classifier says "defect" when the oracle is handed a deliberately wrong model (teacher_forcing.DEFECTS).
+Measured on MI355X (profiles/r04_gpu_tests.log): median errors 1e-7 (qpos) .. 9e-6 (obs), a handful of
+outliers per 1536 env-steps, all explained.
 """
+from collections import Counter
 
 import numpy as np
 import pytest
 
-from tests.teacher_forcing import CASES, explain, explain_reset, run_case
+from tests.teacher_forcing import CASES, DEFECTS, explain, explain_reset, rule_of, run_case
 
 pytestmark = pytest.mark.gpu
 
@@ -42,14 +45,17 @@ def _check(case, rep):
         assert x["kind"] == "sensitive", (int(e), x)
     assert s["good_frac"] >= 0.995, s
     unexplained = []
+    rules = Counter()
     for t, st in enumerate(rep.steps):
         out = rep.outliers(st) | st.done_mismatch | st.int_mismatch
         for e in out.nonzero()[0]:
             x = explain(rep, t, int(e))
             print(f"  outlier step {t} env {e}: {x['kind']} max substep err {max(x['substep_err']):.2e} "
                   f"flips {x.get('flips')} gpu_flip {x.get('gpu_flip')} chain_vs_step {x.get('chain_vs_step', 0):.2e}")
+            rules.update(rule_of(x))
             if x["kind"] != "sensitive":
                 unexplained.append((t, int(e), x))
+    print(f"  rules: {dict(sorted(rules.items()))}")
     assert not unexplained, unexplained
 
 
@@ -85,3 +91,24 @@ def test_teacher_forced_paths_are_exercised(gpu):
     fs3 = rep.pre[3][0].reshape(L.nfloat, 64)
     assert (fs3[L.off["done"]] == 1).all() and (is3[L.ioff["ep_steps"]] == 3).all()   # every env restored at 3
     assert rep.summary()["good_frac"] >= 0.995
+
+
+@pytest.mark.parametrize("defect", list(DEFECTS))
+def test_explain_has_teeth(defect, gpu):
+    """The classifier can say "defect": the oracle runs a deliberately wrong model (floor friction
+    x 1.02, one servo's kp x 1.005, contact solref x 1.02, the foot hull scaled by 1.0005 on the
+    height field) while the GPU runs the nominal one, so every outlier is a real model difference.
+    Outliers must appear, and explain() must return "defect" for >= 90 % of them (up to 40 checked)."""
+    case, edit = DEFECTS[defect]
+    rep = run_case(case, gpu, n=256, steps=2, keep_states=True, oracle_edit=edit)
+    outl = [(t, int(e)) for t, st in enumerate(rep.steps)
+            for e in (rep.outliers(st) | st.done_mismatch | st.int_mismatch).nonzero()[0]]
+    assert len(outl) >= 20, f"the injected defect gave only {len(outl)} outliers"
+    pick = [outl[i] for i in np.linspace(0, len(outl) - 1, min(40, len(outl))).astype(int)]
+    rules = Counter()
+    for t, e in pick:
+        rules.update(rule_of(explain(rep, t, e)))
+    n_def = rules["defect"]
+    print(f"{defect}: {len(outl)} outliers of {sum(len(s.done_mismatch) for s in rep.steps)}, "
+          f"{len(pick)} explained: {dict(sorted(rules.items()))}")
+    assert n_def >= 0.9 * len(pick), dict(rules)

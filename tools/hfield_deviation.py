@@ -38,7 +38,7 @@ def prisms(om, d, g_hf, g_foot, max_n=64):
     return dep[:n], nrm[:3 * n].reshape(n, 3)
 
 
-def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
+def measure(task: str, n_envs: int, n_steps: int, seed: int = 0, blend: bool = True):
     m = Model.load(constants.task_to_xml(task))
     base = OracleModel(m)
     cfg = env_config_struct(m, default_config(), False, domain_randomize=True)
@@ -50,8 +50,21 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
         pairs[g] = p
     rng = np.random.default_rng(seed)
     rows = []
-    wins = (C.c_longlong * 14)()
+    wins = (C.c_longlong * 17)()
     lib().oracle_hfield_axis_wins(wins, 1)
+    # blend=False: the exact SAT's axis and the plain centroid (oracle_set_hf_band_scale(0)), to check
+    # the Minkowski-filtered SAT against the unfiltered brute force axis for axis
+    lib().oracle_set_hf_band_scale(1.0 if blend else 0.0)
+    try:
+        rows = _rollout(m, base, cfg, pairs, floor, n_envs, n_steps, seed, rng)
+    finally:
+        lib().oracle_set_hf_band_scale(1.0)
+    lib().oracle_hfield_axis_wins(wins, 1)
+    return _summary(task, rows, wins, blend)
+
+
+def _rollout(m, base, cfg, pairs, floor, n_envs, n_steps, seed, rng):
+    rows = []
     for e in range(n_envs):
         om = OracleModel(m, dr=base.dr_sample(seed + 1, e))
         env = OracleEnv(om, cfg)
@@ -71,12 +84,15 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
                     n2 = nrm[int(np.argmax(dep))]
                     ang = float(np.degrees(np.arccos(np.clip(n1 @ n2, -1, 1))))
                 rows.append((ours > 0, ref > 0, max(ours, 0.0), max(ref, 0.0), ang, len(dep)))
-    lib().oracle_hfield_axis_wins(wins, 1)
+    return rows
+
+
+def _summary(task, rows, wins, blend):
     a = np.array(rows, dtype=float)
     flag_o, flag_r, dep_o, dep_r, ang, nprism = a.T
     both = (flag_o > 0) & (flag_r > 0)
     dd = np.abs(dep_o - dep_r)[both]
-    return {"scene": task, "foot_samples": len(a), "contact_ours": int(flag_o.sum()), "contact_prism": int(flag_r.sum()),
+    return {"scene": task, "blend": blend, "foot_samples": len(a), "contact_ours": int(flag_o.sum()), "contact_prism": int(flag_r.sum()),
             "flag_agreement": float((flag_o == flag_r).mean()),
             "flag_disagree_max_depth_m": float(np.max(np.maximum(dep_o, dep_r)[flag_o != flag_r], initial=0.0)),
             "depth_abs_diff_m": {"median": float(np.median(dd)), "p99": float(np.quantile(dd, 0.99)), "max": float(dd.max())},
@@ -87,13 +103,18 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0):
                                   [int(x) for x in wins[:7]])),
             "separated_past_prism_faces_by": dict(zip(("hull_face", "top_edge", "vertical_edge", "bottom_edge"),
                                                       [int(x) for x in wins[10:14]])),
+            "tie_band": {"prisms": int(wins[14]), "second_axis_in_band": int(wins[15]),
+                         "third_axis_in_band": int(wins[16])},
             "penetrating_prisms_per_foot": {"mean": float(nprism[flag_r > 0].mean()), "max": int(nprism.max())}}
 
 
 def measure_gpu(task: str, n_envs: int, n_steps: int, seed: int = 0, device="cuda:0"):
     """The HIP kernel's contacts (TPhys::collide_hfield, through duck_physics_step's forward) against
     the brute-force prisms at the same states: oracle rollouts (rough + DR, U(-1,1) actions) give
-    the states; per foot the contact flag, the deepest depth and its normal are compared."""
+    the states; per foot the contact flag and the deepest depth are compared with the brute force,
+    the deepest slot's normal with the oracle's (the declared tie-band blend of the SAT axes, which
+    the brute force's single minimum axis does not make; normal_angle_vs_brute_deg reports that
+    difference too)."""
     import torch
     from open_duck_playground_amd.joystick import Joystick, domain_randomize
     from tests.helpers import parse_aux
@@ -138,16 +159,19 @@ def measure_gpu(task: str, n_envs: int, n_steps: int, seed: int = 0, device="cud
                 gd = g["con_dist"][e, 4 * p:4 * p + 4]
                 gn = g["con_normal"][e].reshape(-1, 3)[4 * p:4 * p + 4]
                 dep, nrm = prisms(models[e], d, floor, gid)
+                od = d.arr("con_dist", 4 * m.npair)[4 * p:4 * p + 4]
+                on = np.ctypeslib.as_array(d.con_frame)[4 * p:4 * p + 4, :3]
                 ours = -gd.min()
                 ref = dep.max() if len(dep) else -1.0
-                ang = np.nan
+                ang = angb = np.nan
                 if ours > 0 and ref > 0:
-                    n1 = gn[int(np.argmin(gd))]
-                    n2 = nrm[int(np.argmax(dep))]
-                    ang = float(np.degrees(np.arccos(np.clip(n1 @ n2 / np.linalg.norm(n1), -1, 1))))
-                rows.append((ours > 0, ref > 0, max(ours, 0.0), max(ref, 0.0), ang))
+                    n1 = gn[int(np.argmin(gd))] / np.linalg.norm(gn[int(np.argmin(gd))])
+                    angb = float(np.degrees(np.arccos(np.clip(n1 @ nrm[int(np.argmax(dep))], -1, 1))))
+                    if od.min() < 0:
+                        ang = float(np.degrees(np.arccos(np.clip(n1 @ on[int(np.argmin(od))], -1, 1))))
+                rows.append((ours > 0, ref > 0, max(ours, 0.0), max(ref, 0.0), ang, angb))
     a = np.array(rows, dtype=float)
-    flag_o, flag_r, dep_o, dep_r, ang = a.T
+    flag_o, flag_r, dep_o, dep_r, ang, angb = a.T
     both = (flag_o > 0) & (flag_r > 0)
     dd = np.abs(dep_o - dep_r)[both]
     q = lambda x: {"median": float(np.median(x)), "p99": float(np.quantile(x, 0.99)), "max": float(np.max(x))}  # noqa: E731
@@ -155,7 +179,8 @@ def measure_gpu(task: str, n_envs: int, n_steps: int, seed: int = 0, device="cud
             "contact_kernel": int(flag_o.sum()), "contact_prism": int(flag_r.sum()),
             "flag_agreement": float((flag_o == flag_r).mean()),
             "flag_disagree_max_depth_m": float(np.max(np.maximum(dep_o, dep_r)[flag_o != flag_r], initial=0.0)),
-            "depth_abs_diff_m": q(dd), "normal_angle_deg": q(ang[both & np.isfinite(ang)])}
+            "depth_abs_diff_m": q(dd), "normal_angle_deg": q(ang[both & np.isfinite(ang)]),
+            "normal_angle_vs_brute_deg": q(angb[both & np.isfinite(angb)])}
 
 
 def main():

@@ -42,14 +42,14 @@ def main():
     pool = [torch.rand(n, env.action_size, device="cuda:0", generator=g) * 2 - 1 for _ in range(8)] if rand else \
         [torch.zeros(n, env.action_size, device="cuda:0")]
     for i in range(20):
-        env.step(st, pool[i % len(pool)])
+        st = env.step(st, pool[i % len(pool)], inplace=True)
     torch.cuda.synchronize()
     buf = (C.c_ulonglong * (NSTAGE + 3 * 1024))()
     lib = native.lib()
     lib.duck_debug_stage_cycles(env._sim, buf, 1)
     steps = 5
     for i in range(steps):
-        env.step(st, pool[i % len(pool)])
+        st = env.step(st, pool[i % len(pool)], inplace=True)
     torch.cuda.synchronize()
     lib.duck_debug_stage_cycles(env._sim, buf, 1)
     nwg = (n + 15) // 16
