@@ -41,6 +41,24 @@ int duck_ppo_loss(int N, int A, const float* logits, const float* raw_action, co
 /* 4 + 2 + 3 ceil(N / 128): the length of duck_ppo_loss's out array (A <= 31) */
 int duck_ppo_loss_out_size(int N);
 
+/* The policy / value MLP layers (brax ppo/networks.py: Dense + swish; nn.Linear weight layout
+ * W [M][R] row-major, bias [M]) on fp32 MFMA, row-major activations [N][.]:
+ *   mode 0  Y[N][M] = op(A)[N][R] W^T + b                    (the output layer)
+ *   mode 1  Y = Z = op(A) W^T + b,  Y2 = silu(Z)             (a hidden layer: Z kept for the backward)
+ *   mode 2  Y[N][M] = (A[N][R] W[R][M]) * silu'(aux[N][M])    (the data gradient: A = dZ of the layer
+ *           above, W that layer's weight [R][M], aux = this layer's Z; bias, mean, istd unused)
+ * op(A) = (A - mean) * istd per column when mean / istd are given (the observation normaliser), else A. */
+int duck_mlp_gemm(int mode, int N, int R, int M, const float* A, const float* W, const float* bias, const float* aux,
+                  float* Y, float* Y2, const float* mean, const float* istd, void* stream);
+/* The weight gradient of one layer as `splits` partial products over row blocks of the batch:
+ * partial[s][off_w + m K + k] = sum_{n in block s} dZ[n][m] op(H)[n][k], partial[s][off_b + m] =
+ * sum_{n in block s} dZ[n][m]; P = the length of one partial (the network's parameter count), so all
+ * layers of the networks share one partial array and one duck_mlp_wgrad_reduce. */
+int duck_mlp_wgrad(int N, int M, int K, const float* dZ, const float* H, const float* mean, const float* istd,
+                   int splits, float* partial, int P, int off_w, int off_b, void* stream);
+/* grad[i] = sum_{s < splits} partial[s][i] in order (deterministic), i < P */
+int duck_mlp_wgrad_reduce(int P, int splits, const float* partial, float* grad, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

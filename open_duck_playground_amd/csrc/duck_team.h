@@ -240,6 +240,30 @@ DK void load_model_tables(float* lds) {
   }
 }
 
+// the hull's faces in screening order for the prism-vertex-inside-hull test (hf_exec): the six faces
+// whose normals are extreme along -z, +z, +x, -x, +y, -y of the mesh frame first (a grid vertex near
+// a foot is almost always outside one of them: below the sole, above the top or beside the
+// footprint), then the rest in index order. The minimum over the faces does not depend on the order.
+template <class Md>
+struct HullFaceOrder {
+  int f[Md::NHF];
+  constexpr HullFaceOrder() : f{} {
+    bool used[Md::NHF] = {};
+    int n = 0;
+    for (int c = 0; c < 6 && c < Md::NHF; c++) {
+      const int ax = c < 2 ? 2 : (c < 4 ? 0 : 1);
+      const float sg = (c == 0 || c == 3 || c == 5) ? -1.0f : 1.0f;
+      int best = -1;
+      for (int i = 0; i < Md::NHF; i++)
+        if (!used[i] && (best < 0 || sg * Md::hull_face_normal[i][ax] > sg * Md::hull_face_normal[best][ax])) best = i;
+      used[best] = true;
+      f[n++] = best;
+    }
+    for (int i = 0; i < Md::NHF; i++)
+      if (!used[i]) f[n++] = i;
+  }
+};
+
 template <class Md>
 struct TPhys {
   using Ly = Lay<Md>;
@@ -1615,9 +1639,13 @@ struct TPhys {
     const float ptop = dot3(ntm, Tm[0]);
     const float smt[3] = {dot3(sm[0], Tm[0]), dot3(sm[1], Tm[1]), dot3(sm[2], Tm[2])};
     float W = 0.0f, Cx[3] = {0.0f, 0.0f, 0.0f};
+    // (a hull vertex above every lane's prism top weighs 0 everywhere: its other four distances are
+    // skipped by a wave-uniform test; W and Cx are unchanged bit for bit, + 0 and fma(0, .) being exact)
     static_for<0, NH>([&](auto kI) {
       constexpr int k = kI.value;
-      float pen = fminf(ptop - hv_dot<k>(ntm), hv_dot<k>(zc) - base);
+      const float atop = ptop - hv_dot<k>(ntm);
+      if (__ballot(atop > 0.0f) == 0ull) return;
+      float pen = fminf(atop, hv_dot<k>(zc) - base);
       for (int j = 0; j < 3; j++) pen = fminf(pen, smt[j] - hv_dot<k>(sm[j]));
       const float w = fmaxf(pen, 0.0f);
       W += w;
@@ -1625,13 +1653,26 @@ struct TPhys {
       Cx[1] = cfma<fbits(Md::hull_vert[k][1])>(w, Cx[1]);
       Cx[2] = cfma<fbits(Md::hull_vert[k][2])>(w, Cx[2]);
     });
+    {
+      // the prism's top vertices inside the hull: the faces in HullFaceOrder, and once no lane of the
+      // wave has a vertex still inside every face tested so far (checked after the first 6 and 14),
+      // the rest are skipped -- every weight is 0 then, and the minimum is order-independent
+      float pk[3] = {1e30f, 1e30f, 1e30f};
+      bool live = true;
+      static_for<0, NF>([&](auto pI) {
+        constexpr int pos = pI.value;
+        constexpr int f = HullFaceOrder<Md>{}.f[pos];
+        if (pos == 6 || pos == 14) live = live && __ballot(fmaxf(pk[0], fmaxf(pk[1], pk[2])) > 0.0f) != 0ull;
+        if (!live) return;
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
-      float pk = 1e30f;
-      static_for<0, NF>([&](auto fI) { pk = fminf(pk, nf_off_minus<fI.value>(nf_dot<fI.value>(Tm[j]))); });
-      const float w = fmaxf(pk, 0.0f);
-      W += w;
-      for (int a = 0; a < 3; a++) Cx[a] += w * Tm[j][a];
+        for (int j = 0; j < 3; j++) pk[j] = fminf(pk[j], nf_off_minus<f>(nf_dot<f>(Tm[j])));
+      });
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        const float w = fmaxf(pk[j], 0.0f);
+        W += w;
+        for (int a = 0; a < 3; a++) Cx[a] += w * Tm[j][a];
+      }
     }
     float pos[3];
     if (W >= HF_POINT_BAND) {

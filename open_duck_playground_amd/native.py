@@ -22,7 +22,7 @@ BUILD = os.path.join(HERE, "build")  # libraries compiled for other models (mode
 EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get", "duck_aux_size", "duck_create", "duck_destroy",
            "duck_debug_stage_cycles", "duck_model_fingerprint", "duck_model_supported",
            "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae", "duck_ppo_loss",
-           "duck_ppo_loss_out_size"]
+           "duck_ppo_loss_out_size", "duck_mlp_gemm", "duck_mlp_wgrad", "duck_mlp_wgrad_reduce"]
 
 
 class DuckError(RuntimeError):
@@ -243,6 +243,11 @@ def lib(path: str = None):
             L.duck_ppo_loss.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_int,
                                         vp, vp, vp, vp]
             L.duck_ppo_loss_out_size.argtypes = [C.c_int]
+        if hasattr(L, "duck_mlp_gemm"):
+            ci = C.c_int
+            L.duck_mlp_gemm.argtypes = [ci, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+            L.duck_mlp_wgrad.argtypes = [ci, ci, ci, vp, vp, vp, vp, ci, vp, ci, ci, ci, vp]
+            L.duck_mlp_wgrad_reduce.argtypes = [ci, ci, vp, vp, vp]
         _libs[path] = L
     return _libs[path]
 

@@ -164,12 +164,14 @@ class RunningStatistics(nn.Module):
         # (two conversion kernels less in every policy / value evaluation; not checkpointed)
         self.register_buffer("mean32", torch.zeros(size), persistent=False)
         self.register_buffer("std32", torch.ones(size), persistent=False)
+        self.register_buffer("istd32", torch.ones(size), persistent=False)  # 1 / std32 (the fused MLP's loads)
         self.std_eps, self.std_min, self.std_max = std_eps, std_min, std_max
 
     @torch.no_grad()
     def _refresh(self) -> None:
         self.mean32.copy_(self.mean)
         self.std32.copy_(self.std)
+        self.istd32.copy_(1.0 / self.std)
 
     def _load_from_state_dict(self, *args, **kwargs):
         super()._load_from_state_dict(*args, **kwargs)
@@ -337,11 +339,129 @@ def ppo_loss(net: ActorCritic, batch: Dict[str, torch.Tensor], cfg: PPOConfig, g
     return loss, {"policy_loss": policy_loss.detach(), "v_loss": v_loss.detach(), "entropy": entropy.detach()}
 
 
+class FusedGrad:
+    """One minibatch's loss and parameter gradients without autograd: both networks' MLPs forward and
+    backward through the duck_mlp_* HIP kernels (csrc/duck_mlp.hip: fp32 MFMA GEMMs with the observation
+    normaliser, bias, swish and its derivative fused into their loads and stores; weight gradients as
+    split-K partial products summed in fixed order), GAE and the loss through duck_gae /
+    duck_ppo_loss. It computes what ``ppo_loss(..., fused=True)`` + ``loss.backward()`` compute (the
+    test compares the two), in ~40 launches instead of ~100, most of them MFMA GEMMs.
+
+    The parameters' ``.grad`` are views of one flat buffer that the final reduction overwrites (never
+    set to None), so the all-reduce over ranks is a single collective on that buffer."""
+
+    SPLITS = 8
+
+    def __init__(self, net: ActorCritic, rows: int, boot_rows: int, device):
+        from .native import lib
+        self.lib = lib()
+        self.net = net
+        self.params = list(net.parameters())
+        self.P = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(self.P, device=device)
+        self.off, o = {}, 0
+        for p in self.params:
+            self.off[id(p)] = o
+            p.grad = self.flat[o:o + p.numel()].view_as(p)
+            o += p.numel()
+        self.part = torch.empty(self.SPLITS * self.P, device=device)
+        self.pol = [m for m in net.policy if isinstance(m, nn.Linear)]
+        self.val = [m for m in net.value if isinstance(m, nn.Linear)]
+        self.N, self.Nv = rows, rows + boot_rows
+
+        def bufs(layers, n):
+            return {"Z": [torch.empty(n, m.out_features, device=device) for m in layers[:-1]],
+                    "H": [torch.empty(n, m.out_features, device=device) for m in layers[:-1]],
+                    "dZ": [torch.empty(n, m.out_features, device=device) for m in layers[:-1]],
+                    "out": torch.empty(n, layers[-1].out_features, device=device)}
+        self.bp, self.bv = bufs(self.pol, self.N), bufs(self.val, self.Nv)
+        A = self.pol[-1].out_features // 2
+        self.g_lg = torch.empty(self.N, 2 * A, device=device)
+        self.d_val = torch.zeros(self.Nv, 1, device=device)   # rows N.. (the bootstrap) stay 0: detached
+        self.loss_out = torch.empty(self.lib.duck_ppo_loss_out_size(self.N), device=device)
+
+    def _forward(self, layers, b, x, norm, n, stream):
+        from .native import check
+        mean, istd = (norm.mean32.data_ptr(), norm.istd32.data_ptr()) if norm is not None else (None, None)
+        inp = x
+        for i, m in enumerate(layers):
+            last = i == len(layers) - 1
+            y = b["out"] if last else b["Z"][i]
+            check(self.lib.duck_mlp_gemm(0 if last else 1, n, m.in_features, m.out_features, inp.data_ptr(),
+                                         m.weight.data_ptr(), m.bias.data_ptr(), None, y.data_ptr(),
+                                         None if last else b["H"][i].data_ptr(), mean if i == 0 else None,
+                                         istd if i == 0 else None, stream))
+            if not last:
+                inp = b["H"][i]
+        return b["out"]
+
+    def _backward(self, layers, b, x, norm, dout, n, stream):
+        from .native import check
+        d = dout
+        for i in range(len(layers) - 1, -1, -1):
+            m = layers[i]
+            h = x if i == 0 else b["H"][i - 1]
+            mean, istd = (norm.mean32.data_ptr(), norm.istd32.data_ptr()) if (i == 0 and norm is not None) else (None, None)
+            check(self.lib.duck_mlp_wgrad(n, m.out_features, m.in_features, d.data_ptr(), h.data_ptr(), mean, istd,
+                                          self.SPLITS, self.part.data_ptr(), self.P, self.off[id(m.weight)],
+                                          self.off[id(m.bias)], stream))
+            if i > 0:
+                dz = b["dZ"][i - 1]
+                check(self.lib.duck_mlp_gemm(2, n, m.out_features, m.in_features, d.data_ptr(), m.weight.data_ptr(),
+                                             None, b["Z"][i - 1].data_ptr(), dz.data_ptr(), None, None, None, stream))
+                d = dz
+
+    def __call__(self, mb: Dict[str, torch.Tensor], cfg: PPOConfig, gen: Optional[torch.Generator]):
+        from .native import check
+        net = self.net
+        T, B = mb["reward"].shape
+        N = T * B
+        if N != self.N or self.Nv != N + B:
+            raise ValueError(f"FusedGrad was sized for {self.N} rows, got {T} x {B}")
+        st = torch.cuda.current_stream(self.flat.device).cuda_stream
+        on, pn = (net.obs_norm, net.priv_norm) if net.normalize else (None, None)
+        obs = mb["obs"].reshape(N, -1)
+        xv = torch.cat([mb["priv"].reshape(N, -1), mb["next_priv"][-1]], 0)
+        logits = self._forward(self.pol, self.bp, obs, on, N, st)
+        v_all = self._forward(self.val, self.bv, xv, pn, self.Nv, st).view(-1)
+        baseline, bootstrap = v_all[:N].view(T, B), v_all[N:]
+        truncation = mb["truncation"]
+        termination = mb["done"] * (1.0 - truncation)
+        vs, adv = compute_gae(truncation, termination, mb["reward"] * cfg.reward_scaling, baseline, bootstrap,
+                              cfg.gae_lambda, cfg.discounting)
+        A = logits.shape[-1] // 2
+        eps = torch.randn((T, B, A), device=logits.device, generator=gen)  # the entropy sample, as NormalTanh draws it
+        ra, olp = mb["raw_action"].contiguous(), mb["log_prob"].contiguous()
+        check(self.lib.duck_ppo_loss(N, A, logits.data_ptr(), ra.data_ptr(), olp.data_ptr(), adv.data_ptr(),
+                                     vs.data_ptr(), baseline.data_ptr(), eps.data_ptr(), float(cfg.clipping_epsilon),
+                                     float(cfg.entropy_cost), int(bool(cfg.normalize_advantage)),
+                                     self.loss_out.data_ptr(), self.g_lg.data_ptr(), self.d_val.data_ptr(), st))
+        self._backward(self.pol, self.bp, obs, on, self.g_lg, N, st)
+        self._backward(self.val, self.bv, xv, pn, self.d_val, self.Nv, st)
+        check(self.lib.duck_mlp_wgrad_reduce(self.P, self.SPLITS, self.part.data_ptr(), self.flat.data_ptr(), st))
+        o = self.loss_out
+        return {"loss": o[0], "policy_loss": o[1], "v_loss": o[2], "entropy": o[3]}
+
+
+def fused_grad_available(device) -> bool:
+    """the fused learner runs on the GPU when libduck.so exports the duck_mlp_* kernels
+    (DUCK_PPO_FUSED_MLP=0 keeps the autograd learner)"""
+    if torch.device(device).type != "cuda" or os.environ.get("DUCK_PPO_FUSED_MLP", "1") == "0":
+        return False
+    from .native import lib
+    return hasattr(lib(), "duck_mlp_gemm")
+
+
 def allreduce_grads(params: Sequence[torch.nn.Parameter]) -> None:
     """Data-parallel gradient mean over ranks: one flattened RCCL all-reduce (xGMI ring)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return
     grads = [p.grad for p in params if p.grad is not None]
+    base = grads[0]._base if grads and grads[0]._base is not None else None
+    if base is not None and all(g._base is base for g in grads) and base.numel() == sum(g.numel() for g in grads):
+        dist.all_reduce(base)       # FusedGrad: every gradient is a view of one flat buffer
+        base /= dist.get_world_size()
+        return
     flat = torch.cat([g.reshape(-1) for g in grads])
     dist.all_reduce(flat)
     flat /= dist.get_world_size()
@@ -373,9 +493,13 @@ class _Learner:
     WARMUP = 3
 
     def __init__(self, net: ActorCritic, opt, cfg: PPOConfig, data: Dict[str, torch.Tensor], mb: int,
-                 device: torch.device, use_graph: bool):
+                 device: torch.device, use_graph: bool, fused_mlp: Optional[bool] = None):
         self.net, self.opt, self.cfg, self.data = net, opt, cfg, data
         self.params = list(net.parameters())
+        if fused_mlp is None:
+            fused_mlp = fused_grad_available(device)
+        T = cfg.unroll_length
+        self.fused = FusedGrad(net, T * mb, mb, device) if fused_mlp else None
         self.idx = torch.zeros(mb, dtype=torch.long, device=device)
         self.use_graph = use_graph
         self.calls = 0
@@ -384,6 +508,8 @@ class _Learner:
 
     def _fwd_bwd(self):
         mbatch = {k: v[:, self.idx] for k, v in self.data.items()}
+        if self.fused is not None:
+            return self.fused(mbatch, self.cfg, None)   # writes every .grad (views of one flat buffer)
         loss, m = ppo_loss(self.net, mbatch, self.cfg, None)
         # gradients set to None before the backward that is captured: it then writes them instead of
         # zero-filling and accumulating (one fill + one add kernel per parameter tensor saved)

@@ -125,3 +125,68 @@ def test_fused_loss_matches_torch(gpu, normalize):
     for a, b in zip(g0, g1):
         err = float((a - b).abs().max()) / (1e-6 + float(a.abs().max()))
         assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("normalize_obs", [True, False])
+def test_fused_mlp_grads_match_autograd(gpu, normalize_obs):
+    """FusedGrad (both MLPs forward and backward through the duck_mlp_* fp32 MFMA kernels, no
+    autograd) against ppo_loss(fused=True) + loss.backward() on the same minibatch: the loss, the
+    three metrics and every parameter gradient to 1e-4 (relative to the gradient's largest entry),
+    with a fitted observation normaliser (op(X) = (X - mean) / std fused into the first layer's
+    loads) and without one; sizes off the 64-row / 64-column tiles (T x B = 140 rows, obs 101)."""
+    torch.manual_seed(0)
+    T, B, A = 20, 7, 14
+    cfg = ppo.PPOConfig(normalize_observations=normalize_obs)
+    net = ppo.ActorCritic(101, 172, A, cfg).to(gpu)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    r = lambda *s: torch.randn(*s, generator=g).to(gpu)
+    batch = {"obs": 2 + 3 * r(T, B, 101), "priv": r(T, B, 172) - 1, "next_priv": r(T, B, 172),
+             "reward": r(T, B), "truncation": (torch.rand(T, B, generator=g) < 0.05).float().to(gpu),
+             "done": (torch.rand(T, B, generator=g) < 0.1).float().to(gpu), "raw_action": 1.5 * r(T, B, A)}
+    if normalize_obs:
+        net.obs_norm.update(batch["obs"])
+        net.priv_norm.update(batch["priv"])
+    with torch.no_grad():
+        lp = ppo.NormalTanh(net.policy_logits(batch["obs"])).log_prob(batch["raw_action"])
+    batch["log_prob"] = lp - torch.log(torch.linspace(0.5, 1.6, T * B, device=gpu)).view(T, B)
+    net.zero_grad(set_to_none=True)
+    loss, m = ppo.ppo_loss(net, batch, cfg, torch.Generator(device=gpu).manual_seed(7), fused=True)
+    loss.backward()
+    ref = [p.grad.detach().clone() for p in net.parameters()]
+    net.zero_grad(set_to_none=True)
+    fg = ppo.FusedGrad(net, T * B, B, gpu)
+    out = fg(batch, cfg, torch.Generator(device=gpu).manual_seed(7))
+    torch.cuda.synchronize()
+    assert abs(float(out["loss"]) - float(loss)) <= 1e-5 * (1 + abs(float(loss)))
+    for k in m:
+        assert abs(float(out[k]) - float(m[k])) <= 1e-5 * (1 + abs(float(m[k]))), k
+    for (name, p), a in zip(net.named_parameters(), ref):
+        err = float((p.grad - a).abs().max()) / (1e-6 + float(a.abs().max()))
+        assert err < 1e-4, (name, err)
+
+
+def test_fused_mlp_gemm_shapes(gpu):
+    """duck_mlp_gemm modes 0 / 1 / 2 against torch at the learner's shapes (5120 x 101 -> 512 ..)."""
+    from open_duck_playground_amd.native import check, lib
+    L = lib()
+    st = torch.cuda.current_stream().cuda_stream
+    torch.manual_seed(1)
+    for (n, k, m) in [(5120, 101, 512), (5376, 512, 256), (5120, 128, 28), (130, 70, 1)]:
+        x, w, b = torch.randn(n, k, device=gpu), torch.randn(m, k, device=gpu) / k ** 0.5, torch.randn(m, device=gpu)
+        mean, std = torch.randn(k, device=gpu), torch.rand(k, device=gpu) + 0.5
+        z, h = torch.empty(n, m, device=gpu), torch.empty(n, m, device=gpu)
+        check(L.duck_mlp_gemm(1, n, k, m, x.data_ptr(), w.data_ptr(), b.data_ptr(), None, z.data_ptr(), h.data_ptr(),
+                              mean.data_ptr(), (1 / std).data_ptr(), st))
+        zr = torch.addmm(b, (x - mean) / std, w.t())
+        torch.cuda.synchronize()
+        assert float((z - zr).abs().max()) <= 1e-4 * float(zr.abs().max()), (n, k, m)
+        assert float((h - torch.nn.functional.silu(zr)).abs().max()) <= 1e-4 * float(zr.abs().max())
+        # the data gradient through this layer: (dY W) * silu'(zp)
+        dy, zp = torch.randn(n, m, device=gpu), torch.randn(n, k, device=gpu)
+        dx = torch.empty(n, k, device=gpu)
+        check(L.duck_mlp_gemm(2, n, m, k, dy.data_ptr(), w.data_ptr(), None, zp.data_ptr(), dx.data_ptr(), None, None,
+                              None, st))
+        s = torch.sigmoid(zp)
+        dxr = (dy @ w) * (s * (1 + zp * (1 - s)))
+        torch.cuda.synchronize()
+        assert float((dx - dxr).abs().max()) <= 1e-4 * float(dxr.abs().max()), (n, k, m)
