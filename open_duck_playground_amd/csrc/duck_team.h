@@ -144,11 +144,8 @@ DK float cfma(float x, float a) {
 constexpr float HF_WITNESS_BAND = 1e-3f;
 // depths within this (m) of the deepest prism contact count as equal (oracle HF_DEPTH_TIE)
 constexpr float HF_DEPTH_TIE = 1e-6f;
-// a prism's normal blends the second-smallest overlap's axis in with weight 1 - (ov2 - ov1) / band
-// (oracle HF_TIE_BAND), and its point moves towards the support midpoint while the total
-// penetration weight is below HF_POINT_BAND (oracle HF_POINT_BAND): both continuous where the exact
-// SAT / the weighted centroid are not
-constexpr float HF_TIE_BAND = 1e-4f;
+// a prism's contact point moves towards the support midpoint while the total penetration weight is
+// below this (m; oracle HF_POINT_BAND): continuous where the weighted centroid of ~1e-7 m weights is not
 constexpr float HF_POINT_BAND = 1e-4f;
 
 #ifndef DUCK_LS_DFLOOR
@@ -1492,30 +1489,24 @@ struct TPhys {
         em[a] = vsel(m0, Tm[1][a], vsel(m1, Tm[2][a], Tm[0][a])) - tm[a];
       }
     };
-    // the smallest overlap (mo, mp) and the second smallest (mo2, mp2), continued from the screen's:
-    // exact values and axis indices in priority order (among equal overlaps the first processed
-    // stays first; the normal's blend is symmetric in an exact tie). The axes themselves are formed
-    // once, after the search (axis()).
-    float mo2 = d4.w;
-    int mp2 = __float_as_int(d5.w);
-    auto take = [&](float ov, int pr) {
-      const bool b1 = ov < mo, b2 = ov < mo2;
-      mp2 = b1 ? mp : (b2 ? pr : mp2);
-      mo2 = fminf(mo2, fmaxf(mo, ov));
-      mp = b1 ? pr : mp;
-      mo = fminf(mo, ov);
+    float mu[3] = {0.0f, 0.0f, 0.0f};
+    auto take = [&](float ov, int pr, const float* u) {
+      const bool b = (ov < mo) | ((ov == mo) & (pr < mp));
+      mo = b ? ov : mo;
+      mp = b ? pr : mp;
+      for (int a = 0; a < 3; a++) mu[a] = b ? u[a] : mu[a];
     };
-    const lds_float* SL = L + ((foot >> 1) - tw) * TL::STRIDE + HF_CINQ + (foot & 1) * HF_SLSZ;
-    // vertical-edge pairs: the prism's support along w is its vertical edge at vertex kk (index: the
-    // foot's silhouette rank i, which is in hull-edge order)
+    // vertical-edge pairs: the prism's support along w is its vertical edge at vertex kk
     {
+      const lds_float* SL = L + ((foot >> 1) - tw) * TL::STRIDE + HF_CINQ + (foot & 1) * HF_SLSZ;
       const int n = ((const lds_int*)SL)[0];
       for (int i = 0; i < n; i++) {
+        const int e = ((const lds_int*)SL)[1 + i];
         const f4v w = ((const lds_f4*)(SL + HF_SLF))[i];
         const float wv[3] = {w.x, w.y, w.z};
         const float q0 = dot3(wv, Tm[0]), q1 = dot3(wv, Tm[1]), q2 = dot3(wv, Tm[2]);
         const int kk = q0 >= q1 ? (q0 >= q2 ? 0 : 2) : (q1 >= q2 ? 1 : 2);
-        take(fmaxf(q0, fmaxf(q1, q2)) - w.w, HF_PRIO_V + 3 * i + kk);
+        take(fmaxf(q0, fmaxf(q1, q2)) - w.w, HF_PRIO_V + 3 * e + kk, wv);
       }
     }
     STAGE_MARK(44);
@@ -1582,57 +1573,24 @@ struct TPhys {
       cross3(u, ev, em);
       const float u2 = dot3(u, u);
       const float sg = (dot3(u, ntm) + dot3(u, sk) < 0.0f ? -1.0f : 1.0f) * __builtin_amdgcn_rsqf(u2);
+      const float un[3] = {sg * u[0], sg * u[1], sg * u[2]};
       // (a degenerate pair, ev parallel to em, gives no axis; ev4.w = |ev|^2)
       const float ov = u2 >= 1e-12f * ev4.w * dot3(em, em) ? sg * (dot3(u, tm) - dot3(u, v0)) : 1e30f;
-      take(ov, HF_PRIO_T + p);
+      take(ov, HF_PRIO_T + p, un);
     }
     STAGE_MARK(47);
     if (!(mo > 0.0f)) {
       E4[0] = f4v{-1.0f, 0.0f, 0.0f, 0.0f};
       return;
     }
-    // axis pr of the priority order, from the same arithmetic that gave its overlap: the prism's top,
-    // sides, bottom, a hull face, a top-edge pair (hull edge e x prism top edge k) or a vertical-edge
-    // pair (silhouette entry i)
-    auto axis = [&](int pr, float* u) {
-      if (pr < HF_PRIO_T) {
-        const int f = pr - 5;
-        const f4v n4 = ht4(Md::B_HFACE + 4 * (f > 0 ? f : 0));
-        const float nf[3] = {-n4.x, -n4.y, -n4.z};
-        float sv[3];
-        side(pr - 1, sv);
-        for (int a = 0; a < 3; a++) u[a] = pr == 0 ? ntm[a] : (pr < 4 ? sv[a] : (pr == 4 ? -zc[a] : nf[a]));
-      } else if (pr < HF_PRIO_V) {
-        const int p = pr - HF_PRIO_T, e = p / 3, k = p - 3 * e;
-        const f4v ev4 = ht4(Md::B_HEDGE + 20 * e + 12);
-        const float ev[3] = {ev4.x, ev4.y, ev4.z};
-        float em[3], tm[3], sk[3], uu[3];
-        side(k, sk);
-        top_edge(k, tm, em);
-        cross3(uu, ev, em);
-        const float sg = (dot3(uu, ntm) + dot3(uu, sk) < 0.0f ? -1.0f : 1.0f) * __builtin_amdgcn_rsqf(dot3(uu, uu));
-        for (int a = 0; a < 3; a++) u[a] = sg * uu[a];
-      } else {
-        const f4v w = ((const lds_f4*)(SL + HF_SLF))[(pr - HF_PRIO_V) / 3];
-        u[0] = w.x;
-        u[1] = w.y;
-        u[2] = w.z;
-      }
-    };
-    // the normal: the smallest overlap's axis, plus the second smallest's weighted 1 - (mo2 - mo) /
-    // HF_TIE_BAND (oracle hf_prism_contact)
-    float mu[3];
-    axis(mp, mu);
-    const float wb = fmaxf(0.0f, 1.0f - (mo2 - mo) * (1.0f / HF_TIE_BAND));
-    if (wb > 0.0f) {
-      float u2v[3];
-      axis(mp2, u2v);
-      for (int a = 0; a < 3; a++) u2v[a] = mu[a] + wb * u2v[a];
-      const float n2 = dot3(u2v, u2v);
-      if (n2 > 1e-18f) {
-        const float r = __builtin_amdgcn_rsqf(n2);
-        for (int a = 0; a < 3; a++) mu[a] = u2v[a] * r;
-      }
+    // the screen's axes: the prism's top, sides, bottom or a hull face
+    if (mp < HF_PRIO_T) {
+      const int f = mp - 5;
+      const f4v n4 = ht4(Md::B_HFACE + 4 * (f > 0 ? f : 0));
+      const float nf[3] = {-n4.x, -n4.y, -n4.z};
+      float sv[3];
+      side(mp - 1, sv);
+      for (int a = 0; a < 3; a++) mu[a] = mp == 0 ? ntm[a] : (mp < 4 ? sv[a] : (mp == 4 ? -zc[a] : nf[a]));
     }
     // the contact point: hull vertices inside the prism and prism top vertices inside the hull,
     // weighted by their penetration
@@ -1829,16 +1787,14 @@ struct TPhys {
     // faces, the bottom and the hull's faces (the hull's support along its top normal from the
     // compile-time vertices). The running minimum and its axis priority are kept: the survivors'
     // SAT (hf_exec) continues from them with the edge pairs.
-    float smo[PPL], smo2[PPL], szt[PPL][3];
-    int smp[PPL], smp2[PPL];
+    float smo[PPL], szt[PPL][3];
+    int smp[PPL];
     unsigned surv = 0;
 #pragma unroll
     for (int j = 0; j < PPL; j++) {
       const int q = sub + 8 * j;
       smo[j] = 0.0f;
       smp[j] = 0;
-      smo2[j] = 1e30f;
-      smp2[j] = 0;
       for (int k = 0; k < 3; k++) szt[j][k] = 0.0f;
       // (a wave-uniform skip of the slots no foot of the wave has: most sub-grids hold <= 12 prisms)
       if (j > 0 && __ballot(q < np) == 0ull) continue;
@@ -1850,23 +1806,17 @@ struct TPhys {
       mulmtv3(ntm, R, nt);
       float hm = 1e30f;
       static_for<0, NH>([&](auto kI) { hm = fminf(hm, hv_dot<kI.value>(ntm)); });
-      // priority order (equal overlaps: the first): top 0, sides 1-3, bottom 4, hull faces 5 + f;
-      // the smallest overlap (mo, mp) and the second smallest (mo2, mp2), exact values
-      float mo = dot3(nt, T[0]) - hm, mo2 = 1e30f;
-      int mp = 0, mp2 = 0;
-      auto take2 = [&](float ov, int pr) {
-        const bool b1 = ov < mo, b2 = ov < mo2;
-        mp2 = b1 ? mp : (b2 ? pr : mp2);
-        mo2 = fminf(mo2, fmaxf(mo, ov));
-        mp = b1 ? pr : mp;
-        mo = fminf(mo, ov);
-      };
+      // priority order (equal overlaps: the first): top 0, sides 1-3, bottom 4, hull faces 5 + f
+      float mo = dot3(nt, T[0]) - hm;
+      int mp = 0;
       for (int k = 0; k < 3; k++) {  // (tri is 0 or 1: two-way selects, not an indexed register array)
         const float sxk = tri ? sx_[1][k] : sx_[0][k], syk = tri ? sy_[1][k] : sy_[0][k];
         const float ov = sxk * T[k][0] + syk * T[k][1] - (tri ? smin[1][k] : smin[0][k]);
-        take2(ov, 1 + k);
+        mp = ov < mo ? 1 + k : mp;
+        mo = fminf(mo, ov);
       }
-      take2(obot, 4);
+      mp = obot < mo ? 4 : mp;
+      mo = fminf(mo, obot);
       {
         // the hull's faces (compile-time normals): the prism's lowest point along n_f, a bottom
         // vertex where n_f leans up the field's z
@@ -1878,7 +1828,9 @@ struct TPhys {
           float pm = nf_dot<f>(Tm[0]) - hk[0] * nz;
           pm = fminf(pm, nf_dot<f>(Tm[1]) - hk[1] * nz);
           pm = fminf(pm, nf_dot<f>(Tm[2]) - hk[2] * nz);
-          take2(nf_off_minus<f>(pm), 5 + f);
+          const float ov = nf_off_minus<f>(pm);
+          mp = ov < mo ? 5 + f : mp;
+          mo = fminf(mo, ov);
         });
       }
       const bool high = !(T[0][2] < lo[2] && T[1][2] < lo[2] && T[2][2] < lo[2]);
@@ -1886,8 +1838,6 @@ struct TPhys {
       surv |= half_bits(__ballot(ok), lane) << (8 * j);
       smo[j] = mo;
       smp[j] = mp;
-      smo2[j] = mo2;
-      smp2[j] = mp2;
       for (int k = 0; k < 3; k++) szt[j][k] = T[k][2];
     }
     // this foot's silhouette edges (the hull's edges whose faces straddle the field's horizontal
@@ -1982,8 +1932,8 @@ struct TPhys {
           E4[1] = f4v{Tm[1][0], Tm[1][1], Tm[1][2], smo[j]};
           E4[2] = f4v{Tm[2][0], Tm[2][1], Tm[2][2], __int_as_float(smp[j])};
           E4[3] = f4v{ntm[0], ntm[1], ntm[2], __int_as_float(tri | (2 * tw + h) << 1)};
-          E4[4] = f4v{zc[0], zc[1], zc[2], smo2[j]};
-          E4[5] = f4v{R[0], R[1], R[2], __int_as_float(smp2[j])};
+          E4[4] = f4v{zc[0], zc[1], zc[2], 0.0f};
+          E4[5] = f4v{R[0], R[1], R[2], 0.0f};
           E4[6] = f4v{R[3], R[4], R[5], 0.0f};
         }
       }

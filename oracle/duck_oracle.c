@@ -690,26 +690,25 @@ static void collide_plane_convex(const oracle_model* m, oracle_data* d, int g1, 
  * prism contacts by MJX's _manifold_points starting at the deepest (within HF_DEPTH_TIE). Declared choices (DESIGN.md
  * §5 item 6): equal overlaps resolve to the first axis in the order prism top, sides, bottom, hull
  * faces, top-edge pairs, vertical-edge pairs, bottom-edge pairs; the contact point of a prism
- * is the penetration-weighted centroid of the vertices of each shape inside the other, or, when
- * none is (crossing edges), the midpoint of the two shapes' support features (the centroid of each
- * shape's vertices within HF_WITNESS_BAND of its support plane along the normal, weighted 1 at the
- * plane to 0 at the band edge; the prism's top vertices only). */
+ * is the penetration-weighted centroid of the vertices of each shape inside the other, moved towards
+ * the midpoint of the two shapes' support features (the centroid of each shape's vertices within
+ * HF_WITNESS_BAND of its support plane along the normal, weighted 1 at the plane to 0 at the band
+ * edge; the prism's top vertices only) while the total weight is below HF_POINT_BAND, and that
+ * midpoint alone when no vertex is inside (crossing edges). */
 #define HF_WITNESS_BAND 1e-3 /* m; = TPhys HF_WITNESS_BAND */
-#define HF_TIE_BAND 1e-4     /* m; = TPhys HF_TIE_BAND: the second-smallest overlap within this of the smallest blends its axis into the normal */
 #define HF_POINT_BAND 1e-4   /* m; = TPhys HF_POINT_BAND: a total penetration weight below this blends the point towards the support midpoint */
 #define HF_DEPTH_TIE 1e-6    /* m; = TPhys HF_DEPTH_TIE: prisms sharing a grid vertex or edge often tie exactly */
 #define HF_MAXPRISM 128      /* prisms under one hull (the sub-grid of a 0.11 m foot: <= 18) */
 
 /* test aid: how often each class of separating axis gave a prism's penetration (oracle_hfield_axis_wins) */
-static long long hf_axis_wins[17];
-void oracle_hfield_axis_wins(long long out[17], int reset) {
-  for (int i = 0; i < 17; i++) { out[i] = hf_axis_wins[i]; if (reset) hf_axis_wins[i] = 0; }
+static long long hf_axis_wins[14];
+void oracle_hfield_axis_wins(long long out[14], int reset) {
+  for (int i = 0; i < 14; i++) { out[i] = hf_axis_wins[i]; if (reset) hf_axis_wins[i] = 0; }
 }
 
 
-/* test aid (oracle_set_hf_band_scale): scales HF_TIE_BAND and HF_POINT_BAND (default 1; 0 = the exact
- * SAT's axis and the plain weighted centroid). Only the brute-force check of the prism SAT's depth and
- * axis (tools/hfield_deviation.py, blend=False) turns the blend off. */
+/* test aid (oracle_set_hf_band_scale): scales HF_POINT_BAND (default 1; 0 = the plain weighted
+ * centroid, round 3's point rule): tools/hfield_deviation.py compares the two. */
 static _Thread_local double g_hf_band_scale = 1.0;
 void oracle_set_hf_band_scale(double s) { g_hf_band_scale = s; }
 
@@ -838,54 +837,19 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
     }
     return 0;
   }
-  /* the smallest overlap (the first axis in priority order among equal ones) and the second smallest
-   * (likewise, over the other axes) */
   int w = 0;
   while (w < na - 1 && ov[w] > mn) w++;
-  int w2 = -1;
-  for (int i = 0; i < na; i++)
-    if (i != w && (w2 < 0 || ov[i] < ov[w2])) w2 = i;
   {
     /* which class of axis won (hf_axis_wins: prism top, sides, bottom, hull faces, top-edge,
-     * vertical-edge, bottom-edge pairs); 14-16: prisms with a second / third axis inside the tie band */
+     * vertical-edge, bottom-edge pairs) */
     int cls = w == 0 ? 0 : (w < 4 ? 1 : (w == 4 ? 2 : (w < 5 + H->nf ? 3 : 4)));
     if (cls == 4) cls = 4 + kind_of_axis[w];
-    int inband = 0;
-    for (int i = 0; i < na; i++) inband += ov[i] < mn + HF_TIE_BAND * g_hf_band_scale;
 #ifdef _OPENMP
 #pragma omp atomic
 #endif
     hf_axis_wins[cls]++;
-#ifdef _OPENMP
-#pragma omp atomic
-#endif
-    hf_axis_wins[14]++;
-    if (inband >= 2) {
-#ifdef _OPENMP
-#pragma omp atomic
-#endif
-      hf_axis_wins[15]++;
-    }
-    if (inband >= 3) {
-#ifdef _OPENMP
-#pragma omp atomic
-#endif
-      hf_axis_wins[16]++;
-    }
   }
-  /* the normal: the smallest overlap's axis, blended with the second smallest's by a weight that
-   * falls linearly from 1 at equal overlaps to 0 at HF_TIE_BAND apart (declared):
-   * the exact SAT's normal jumps between two axes whose overlaps cross, which fp32 and fp64 decide
-   * differently within ~1e-7 m; the blend is continuous there, and is the exact SAT's axis whenever
-   * no other axis comes within the band */
-  double u[3];
-  {
-    const double band = HF_TIE_BAND * g_hf_band_scale;
-    const double beta = w2 < 0 || band <= 0 ? 0.0 : fmax(0.0, 1.0 - (ov[w2] - ov[w]) / band);
-    for (int a = 0; a < 3; a++) u[a] = ax[w][a] + (beta > 0 ? beta * ax[w2][a] : 0.0);
-    const double un = norm3(u);
-    for (int a = 0; a < 3; a++) u[a] = un > 1e-9 ? u[a] / un : ax[w][a];
-  }
+  const double* u = ax[w];
   /* the contact point: the centroid of the vertices of each shape inside the other (hull vertices
    * inside the prism, prism top vertices inside the hull), each weighted by its penetration (distance
    * to the nearest face of the other shape), blended towards the midpoint of the two shapes' support

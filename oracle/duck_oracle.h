@@ -75,11 +75,11 @@ int oracle_hfield_prisms(const oracle_model* m, const oracle_data* d, int g_hf, 
 /* test aid: counts of the axis class that gave each prism contact (top, sides, bottom, hull faces,
  * top-edge pairs, vertical-edge pairs, bottom-edge pairs) since the last reset, then [7 + class]
  * the class that separated a prism whose own 5 faces do not */
-void oracle_hfield_axis_wins(long long out[17], int reset);
+void oracle_hfield_axis_wins(long long out[14], int reset);
 void oracle_set_trace(double* buf); /* test aid: record substep inputs of oracle_env_step */
 void oracle_set_ls_floor(double floor); /* test aid: the HIP line search's fp32 stop rule (0 = off) */
 void oracle_set_hdump(double* buf); /* test aid: dump the next solve's first Newton Hessian and row margins */
-void oracle_set_hf_band_scale(double s); /* test aid: scales HF_TIE_BAND / HF_POINT_BAND (0: exact SAT axis, plain centroid) */
+void oracle_set_hf_band_scale(double s); /* test aid: scales HF_POINT_BAND (0: the plain weighted centroid) */
 void oracle_set_con_override(const double* buf); /* test aid: replace the contact set after collision (7 doubles per slot) */
 void oracle_set_force_start(int mode);  /* test aid: Newton start 1 warm, 2 smooth, 0 the cheaper */
 void oracle_last_start_costs(double out[2]); /* test aid: costs at qacc_warmstart, qacc_smooth */

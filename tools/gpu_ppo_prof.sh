@@ -1,16 +1,18 @@
 #!/bin/bash
-# Kernel-level profile of the PPO outer loop (tools/ppo_throughput.py), for the learner's cost split.
+# rocprofv3 kernel trace of PPO training updates (tools/ppo_throughput.py): per-kernel time of the
+# rollout and the learner. usage: bash tools/gpu_ppo_prof.sh [tag]
 set -o pipefail
-OUT=gpurun_out/ppo_prof; rm -rf $OUT; mkdir -p $OUT; export TMPDIR=/tmp
-timeout -k 10 300 python tools/ppo_throughput.py --updates 3 > $OUT/plain.json 2>&1 || { tail $OUT/plain.json; exit 1; }
-cat $OUT/plain.json
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 tools/ppo_throughput.py --updates 2 > $OUT/prof.json 2>&1 || { tail $OUT/prof.json; exit 1; }
-python3 - <<'PY'
-import csv, glob
-f = glob.glob("gpurun_out/ppo_prof/trace/**/*kernel_stats.csv", recursive=True)[0]
-rows = list(csv.DictReader(open(f)))
+OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+T=${1:-ppo}
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof_$T -o prof -- python3 $GRAFT_REPO_ROOT/tools/ppo_throughput.py --updates 2 > $GRAFT_REPO_ROOT/$OUT/prof_$T.log 2>&1 || { tail -5 $GRAFT_REPO_ROOT/$OUT/prof_$T.log; exit 1; }
+cd $GRAFT_REPO_ROOT
+f=$(find $OUT/prof_$T -name "*kernel_stats.csv" | head -1)
+python3 - "$f" <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
-print("total kernel ms", tot / 1e6, "kernels", sum(int(r["Calls"]) for r in rows))
-for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
-    print("%8.2f ms %6d calls %7.1f us  %s" % (float(r["TotalDurationNs"]) / 1e6, int(r["Calls"]), float(r["AverageNs"]) / 1e3, r["Name"][:110]))
+print(f"total kernel time {tot/1e6:.1f} ms")
+for r in rows[:25]:
+    print(f'{float(r["TotalDurationNs"])/1e6:8.2f} ms {int(r["Calls"]):7d} calls {float(r["AverageNs"])/1e3:8.2f} us  {r["Name"][:90]}')
 PY

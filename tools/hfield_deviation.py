@@ -50,10 +50,10 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0, blend: bool = T
         pairs[g] = p
     rng = np.random.default_rng(seed)
     rows = []
-    wins = (C.c_longlong * 17)()
+    wins = (C.c_longlong * 14)()
     lib().oracle_hfield_axis_wins(wins, 1)
-    # blend=False: the exact SAT's axis and the plain centroid (oracle_set_hf_band_scale(0)), to check
-    # the Minkowski-filtered SAT against the unfiltered brute force axis for axis
+    # blend=False: round 3's plain penetration-weighted centroid (oracle_set_hf_band_scale(0)) in
+    # place of the point band
     lib().oracle_set_hf_band_scale(1.0 if blend else 0.0)
     try:
         rows = _rollout(m, base, cfg, pairs, floor, n_envs, n_steps, seed, rng)
@@ -103,8 +103,6 @@ def _summary(task, rows, wins, blend):
                                   [int(x) for x in wins[:7]])),
             "separated_past_prism_faces_by": dict(zip(("hull_face", "top_edge", "vertical_edge", "bottom_edge"),
                                                       [int(x) for x in wins[10:14]])),
-            "tie_band": {"prisms": int(wins[14]), "second_axis_in_band": int(wins[15]),
-                         "third_axis_in_band": int(wins[16])},
             "penetrating_prisms_per_foot": {"mean": float(nprism[flag_r > 0].mean()), "max": int(nprism.max())}}
 
 
