@@ -58,6 +58,13 @@ int duck_mlp_wgrad(int N, int M, int K, const float* dZ, const float* H, const f
                    int splits, float* partial, int P, int off_w, int off_b, void* stream);
 /* grad[i] = sum_{s < splits} partial[s][i] in order (deterministic), i < P */
 int duck_mlp_wgrad_reduce(int P, int splits, const float* partial, float* grad, void* stream);
+/* The rollout's policy sample (brax NormalTanhDistribution): for each of N rows of logits [N][2A]
+ * (loc | pre-softplus scale), eps ~ N(0, 1) from threefry2x32 keyed by seed at counter (row,
+ * 8 *ctr + pair) (Box-Muller), raw = loc + (softplus(pre) + 1e-3) eps -> raw [N][A], its NormalTanh
+ * log-probability -> logprob [N], tanh(raw) -> action [N][A]; then *ctr += 1 (device counter: a
+ * captured graph draws fresh noise on every replay). A <= 16. */
+int duck_policy_sample(int N, int A, const float* logits, unsigned long long seed, unsigned int* ctr, float* raw,
+                       float* logprob, float* action, void* stream);
 
 #ifdef __cplusplus
 }

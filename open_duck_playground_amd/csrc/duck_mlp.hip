@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include "duck_common.h"
+#include "duck_math.h"
 #include "../../include/duck_ppo.h"
 
 namespace {
@@ -254,6 +255,48 @@ __global__ __launch_bounds__(256) void mlp_reduce_kernel(int P, int S, const flo
   grad[i] = a;
 }
 
+
+// brax NormalTanhDistribution sampling for the rollout (ppo/networks.py; ppo.NormalTanh): one thread
+// per env row, raw = loc + scale eps with scale = softplus(pre) + 1e-3 and eps ~ N(0, 1) by
+// Box-Muller from threefry2x32 (key = seed, counter = (row, 8 draw + pair)), action = tanh(raw),
+// log_prob = sum_j -z^2/2 - log scale - log(2 pi)/2 - log|tanh'(raw)| with z = (raw - loc) / scale
+// (the same expression the loss recomputes). The draw counter lives in device memory and the
+// following one-thread launch advances it, so a captured rollout draws fresh noise on every replay.
+__global__ __launch_bounds__(256) void policy_sample_kernel(int N, int A, const float* __restrict__ logits,
+                                                            uint32_t k0, uint32_t k1, const uint32_t* __restrict__ ctr,
+                                                            float* __restrict__ raw, float* __restrict__ logprob,
+                                                            float* __restrict__ action) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const uint32_t c = *ctr;
+  const float* lg = logits + (size_t)n * 2 * A;
+  float lp = 0.f;
+  for (int j0 = 0; j0 < A; j0 += 2) {
+    uint32_t a, b;
+    threefry2x32(k0, k1, (uint32_t)n, c * 8u + (uint32_t)(j0 >> 1), a, b);
+    const float u1 = ((float)(a >> 9) + 1.f) * (1.f / 8388608.f);  // (0, 1]
+    const float u2 = (float)(b >> 9) * (1.f / 8388608.f);
+    const float r = sqrtf(-2.f * logf(u1));
+    float sn, cs;
+    sincosf(6.283185307179586f * u2, &sn, &cs);
+    const float e2[2] = {r * cs, r * sn};
+    for (int h = 0; h < 2 && j0 + h < A; h++) {
+      const int j = j0 + h;
+      const float loc = lg[j], pre = lg[A + j];
+      const float scale = (pre > 20.f ? pre : log1pf(__expf(pre))) + 1e-3f;
+      const float x = loc + scale * e2[h];
+      const float z = (x - loc) / scale;
+      const float sp = -2.f * x > 20.f ? -2.f * x : log1pf(__expf(-2.f * x));
+      lp += -0.5f * z * z - logf(scale) - 0.91893853320467274f - 2.f * (0.69314718055994531f - x - sp);
+      raw[(size_t)n * A + j] = x;
+      action[(size_t)n * A + j] = tanhf(x);
+    }
+  }
+  logprob[n] = lp;
+}
+
+__global__ void ctr_inc_kernel(uint32_t* ctr) { *ctr += 1u; }
+
 }  // namespace
 
 extern "C" int duck_mlp_gemm(int mode, int N, int R, int M, const float* A, const float* W, const float* bias,
@@ -298,6 +341,19 @@ extern "C" int duck_mlp_wgrad_reduce(int P, int splits, const float* partial, fl
   if (!partial || !grad) return duck_fail(DUCK_EINVAL, "duck_mlp_wgrad_reduce: null pointer");
   hipLaunchKernelGGL(mlp_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, P, splits, partial,
                      grad);
+  HIPCHECK(hipGetLastError());
+  return DUCK_OK;
+}
+
+extern "C" int duck_policy_sample(int N, int A, const float* logits, unsigned long long seed, unsigned int* ctr,
+                                  float* raw, float* logprob, float* action, void* stream) {
+  if (N < 0 || A <= 0 || A > 16) return duck_fail(DUCK_EINVAL, "duck_policy_sample: bad size");
+  if (N == 0) return DUCK_OK;
+  if (!logits || !ctr || !raw || !logprob || !action) return duck_fail(DUCK_EINVAL, "duck_policy_sample: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(policy_sample_kernel, dim3((N + 255) / 256), dim3(256), 0, st, N, A, logits, (uint32_t)seed,
+                     (uint32_t)(seed >> 32), ctr, raw, logprob, action);
+  hipLaunchKernelGGL(ctr_inc_kernel, dim3(1), dim3(1), 0, st, ctr);
   HIPCHECK(hipGetLastError());
   return DUCK_OK;
 }

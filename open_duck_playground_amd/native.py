@@ -22,7 +22,8 @@ BUILD = os.path.join(HERE, "build")  # libraries compiled for other models (mode
 EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get", "duck_aux_size", "duck_create", "duck_destroy",
            "duck_debug_stage_cycles", "duck_model_fingerprint", "duck_model_supported",
            "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae", "duck_ppo_loss",
-           "duck_ppo_loss_out_size", "duck_mlp_gemm", "duck_mlp_wgrad", "duck_mlp_wgrad_reduce"]
+           "duck_ppo_loss_out_size", "duck_mlp_gemm", "duck_mlp_wgrad", "duck_mlp_wgrad_reduce",
+           "duck_policy_sample"]
 
 
 class DuckError(RuntimeError):
@@ -248,6 +249,7 @@ def lib(path: str = None):
             L.duck_mlp_gemm.argtypes = [ci, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp]
             L.duck_mlp_wgrad.argtypes = [ci, ci, ci, vp, vp, vp, vp, ci, vp, ci, ci, ci, vp]
             L.duck_mlp_wgrad_reduce.argtypes = [ci, ci, vp, vp, vp]
+            L.duck_policy_sample.argtypes = [ci, ci, vp, C.c_uint64, vp, vp, vp, vp, vp]
         _libs[path] = L
     return _libs[path]
 

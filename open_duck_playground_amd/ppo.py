@@ -550,6 +550,102 @@ class _Learner:
         return self.out
 
 
+class _Rollout:
+    """The unroll of ``train``: ``unroll_length`` env-steps of all envs with the policy sampling, every
+    transition written in place into the time-major buffers. On the GPU the policy runs through the
+    duck_mlp_gemm kernels (normaliser fused) and duck_policy_sample (NormalTanh sample, log-prob and
+    tanh in one launch, counter-based threefry draws whose counter lives on the device), so the whole
+    unroll -- policy, env.step, buffer writes -- is captured once as a HIP graph and replayed per
+    update (~600 small launches per unroll otherwise). The first unroll runs eagerly (allocations)."""
+
+    def __init__(self, env, net: ActorCritic, cfg: PPOConfig, data: Dict[str, torch.Tensor], unrolls: int,
+                 device, use_graph: bool, seed: int):
+        from .native import lib
+        self.env, self.net, self.cfg, self.data = env, net, cfg, data
+        self.unrolls, self.n = unrolls, env.num_envs
+        self.lib = lib()
+        self.pol = [m for m in net.policy if isinstance(m, nn.Linear)]
+        n, dev = self.n, device
+        self.Z = [torch.empty(n, m.out_features, device=dev) for m in self.pol[:-1]]
+        self.H = [torch.empty(n, m.out_features, device=dev) for m in self.pol[:-1]]
+        self.logits = torch.empty(n, self.pol[-1].out_features, device=dev)
+        self.action = torch.empty(n, self.pol[-1].out_features // 2, device=dev)
+        self.ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x5EED) & 0xFFFFFFFFFFFFFFFF
+        self.use_graph, self.calls, self.graph = use_graph, 0, None
+
+    def _policy(self, obs: torch.Tensor, st) -> torch.Tensor:
+        from .native import check
+        norm = self.net.obs_norm if self.net.normalize else None
+        inp = obs
+        for i, m in enumerate(self.pol):
+            last = i == len(self.pol) - 1
+            check(self.lib.duck_mlp_gemm(0 if last else 1, self.n, m.in_features, m.out_features, inp.data_ptr(),
+                                         m.weight.data_ptr(), m.bias.data_ptr(), None,
+                                         (self.logits if last else self.Z[i]).data_ptr(),
+                                         None if last else self.H[i].data_ptr(),
+                                         norm.mean32.data_ptr() if (i == 0 and norm is not None) else None,
+                                         norm.istd32.data_ptr() if (i == 0 and norm is not None) else None, st))
+            if not last:
+                inp = self.H[i]
+        return self.logits
+
+    def _unroll(self, state):
+        from .native import check
+        cfg, data, n = self.cfg, self.data, self.n
+        st = torch.cuda.current_stream(self.logits.device).cuda_stream
+        A = self.action.shape[1]
+        for u in range(self.unrolls):
+            cols = slice(u * n, (u + 1) * n)
+            for t in range(cfg.unroll_length):
+                obs, priv = state.obs[cfg.policy_obs_key], state.obs[cfg.value_obs_key]
+                data["obs"][t, cols] = obs
+                data["priv"][t, cols] = priv
+                logits = self._policy(obs, st)
+                check(self.lib.duck_policy_sample(n, A, logits.data_ptr(), self.seed, self.ctr.data_ptr(),
+                                                  data["raw_action"][t, cols].data_ptr(),
+                                                  data["log_prob"][t, cols].data_ptr(), self.action.data_ptr(), st))
+                self.env.step(state, self.action, inplace=True)  # obs already copied out
+                data["reward"][t, cols] = state.reward
+                data["done"][t, cols] = state.done
+                data["truncation"][t, cols] = state.info["truncation"]
+                data["next_priv"][t, cols] = state.obs[cfg.value_obs_key]
+
+    @torch.no_grad()
+    def run(self, state) -> None:
+        self.calls += 1
+        if not self.use_graph or self.calls == 1:
+            self._unroll(state)
+            return
+        if self.graph is None:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._unroll(state)
+        self.graph.replay()
+
+
+@torch.no_grad()
+def _torch_unroll(env, net: ActorCritic, cfg: PPOConfig, data: Dict[str, torch.Tensor], state, unrolls: int,
+                  gen: torch.Generator) -> None:
+    """The unroll with the torch policy and torch's normal sampler (CPU runs, DUCK_PPO_FUSED_MLP=0)."""
+    n = env.num_envs
+    for u in range(unrolls):
+        cols = slice(u * n, (u + 1) * n)
+        for t in range(cfg.unroll_length):
+            obs, priv = state.obs[cfg.policy_obs_key], state.obs[cfg.value_obs_key]
+            data["obs"][t, cols] = obs
+            data["priv"][t, cols] = priv
+            d = NormalTanh(net.policy_logits(obs))
+            raw = d.sample_raw(gen)
+            data["raw_action"][t, cols] = raw
+            data["log_prob"][t, cols] = d.log_prob(raw)
+            env.step(state, torch.tanh(raw), inplace=True)  # obs already copied out
+            data["reward"][t, cols] = state.reward
+            data["done"][t, cols] = state.done
+            data["truncation"][t, cols] = state.info["truncation"]
+            data["next_priv"][t, cols] = state.obs[cfg.value_obs_key]
+
+
 @dataclass
 class TrainResult:
     net: ActorCritic
@@ -606,6 +702,10 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
               "done": (), "truncation": (), "next_priv": (priv_size,)}
     data = {k: torch.zeros((T, B) + sh, dtype=torch.float32, device=device) for k, sh in shapes.items()}
     learner = _Learner(net, opt, cfg, data, mb, device, use_graph)
+    # the GPU unroll through the duck_mlp / duck_policy_sample kernels, graph-captured (DUCK_PPO_FUSED_MLP=0:
+    # the torch policy and torch's normal sampler)
+    roller = _Rollout(env, net, cfg, data, unrolls_per_update, device, use_graph, cfg.seed * 7919 + rank) \
+        if fused_grad_available(device) else None
     state = env.reset(rng=cfg.seed)  # streams are keyed by global env id: ranks draw disjoint envs
     result = TrainResult(net=net)
     # brax: num_evals evaluations spread evenly over training, the first before any update
@@ -624,22 +724,10 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
         _sync()
         t_roll = time.time()
         # ---- rollouts: unroll_length env-steps of all envs, policy in inference mode ----
-        with torch.no_grad():
-            for u in range(unrolls_per_update):
-                cols = slice(u * n, (u + 1) * n)
-                for t in range(T):
-                    obs, priv = state.obs[cfg.policy_obs_key], state.obs[cfg.value_obs_key]
-                    data["obs"][t, cols] = obs
-                    data["priv"][t, cols] = priv
-                    d = NormalTanh(net.policy_logits(obs))
-                    raw = d.sample_raw(gen)
-                    data["raw_action"][t, cols] = raw
-                    data["log_prob"][t, cols] = d.log_prob(raw)
-                    env.step(state, torch.tanh(raw), inplace=True)  # obs already copied out
-                    data["reward"][t, cols] = state.reward
-                    data["done"][t, cols] = state.done
-                    data["truncation"][t, cols] = state.info["truncation"]
-                    data["next_priv"][t, cols] = state.obs[cfg.value_obs_key]
+        if roller is not None:
+            roller.run(state)
+        else:
+            _torch_unroll(env, net, cfg, data, state, unrolls_per_update, gen)
         _sync()
         t_learn = time.time()
         result.timing["rollout_s"] += t_learn - t_roll

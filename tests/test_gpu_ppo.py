@@ -194,3 +194,30 @@ def test_fused_mlp_gemm_shapes(gpu):
         dxr = (dy @ w) * (s * (1 + zp * (1 - s)))
         torch.cuda.synchronize()
         assert float((dx - dxr).abs().max()) <= 1e-4 * float(dxr.abs().max()), (n, k, m)
+
+
+def test_policy_sample_kernel(gpu):
+    """duck_policy_sample: action = tanh(raw), log_prob = NormalTanh(logits).log_prob(raw) (the torch
+    expression), the implied draws eps = (raw - loc) / scale standard normal, and the device counter
+    advancing (a second call draws other noise)."""
+    from open_duck_playground_amd.native import check, lib
+    n, A = 8192, 14
+    torch.manual_seed(2)
+    logits = torch.randn(n, 2 * A, device=gpu)
+    ctr = torch.zeros(1, dtype=torch.int32, device=gpu)
+    outs = []
+    for _ in range(2):
+        raw, lp, act = torch.empty(n, A, device=gpu), torch.empty(n, device=gpu), torch.empty(n, A, device=gpu)
+        check(lib().duck_policy_sample(n, A, logits.data_ptr(), 12345, ctr.data_ptr(), raw.data_ptr(), lp.data_ptr(),
+                                       act.data_ptr(), torch.cuda.current_stream().cuda_stream))
+        outs.append((raw, lp, act))
+    torch.cuda.synchronize()
+    assert int(ctr.item()) == 2
+    d = ppo.NormalTanh(logits)
+    for raw, lp, act in outs:
+        assert torch.allclose(act, torch.tanh(raw), atol=1e-6)
+        ref = d.log_prob(raw)
+        assert float((lp - ref).abs().max()) <= 1e-4 * (1 + float(ref.abs().max()))
+        eps = ((raw - d.loc) / d.scale).reshape(-1)
+        assert abs(float(eps.mean())) < 0.01 and abs(float(eps.std()) - 1) < 0.01
+    assert not torch.equal(outs[0][0], outs[1][0])
