@@ -707,6 +707,14 @@ void oracle_hfield_axis_wins(long long out[14], int reset) {
 }
 
 
+/* test aid (oracle_set_hf_tie_last): a prism's overlaps within this band of the minimum resolve to the
+ * LAST such axis of the priority order (0, default: the first, the declared rule). The band is the
+ * kernel's fp32 error bound on an overlap (hull coordinates ~0.3 m from the mesh origin, ~20
+ * operations: a few 1e-7 m): two axes that close are tied at the kernel's precision, and its fp32
+ * overlaps may order them the other way (teacher forcing's "sat_tie" rule). */
+static _Thread_local double g_hf_tie_last;
+void oracle_set_hf_tie_last(double band) { g_hf_tie_last = band; }
+
 /* test aid (oracle_set_hf_band_scale): scales HF_POINT_BAND (default 1; 0 = the plain weighted
  * centroid, round 3's point rule): tools/hfield_deviation.py compares the two. */
 static _Thread_local double g_hf_band_scale = 1.0;
@@ -839,6 +847,9 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
   }
   int w = 0;
   while (w < na - 1 && ov[w] > mn) w++;
+  if (g_hf_tie_last > 0) /* test aid: the last axis within the tie band instead of the first */
+    for (int i = 0; i < na; i++)
+      if (ov[i] <= mn + g_hf_tie_last) w = i;
   {
     /* which class of axis won (hf_axis_wins: prism top, sides, bottom, hull faces, top-edge,
      * vertical-edge, bottom-edge pairs) */
@@ -953,22 +964,52 @@ static int hf_prism_top(const oracle_model* m, const hf_frame* F, int r, int c, 
 }
 
 /* height field (g1) vs convex hull (g2): the DUCK_CON_PER_PAIR deepest prism contacts */
-static void collide_hfield_convex(const oracle_model* m, oracle_data* d, int g1, int g2, int slot0) {
-  for (int c = 0; c < DUCK_CON_PER_PAIR; c++) set_inactive(d, slot0 + c, g1, g2);
+/* every penetrating prism's contact (depth, normal, point; the hull frame F.t-relative field axes), in
+ * strip order; returns their number (0 when the hull misses the field) */
+static int hf_contacts(const oracle_model* m, const oracle_data* d, int g1, int g2, hf_frame* F,
+                       double dep[HF_MAXPRISM], double nrm[HF_MAXPRISM][3], double pt[HF_MAXPRISM][3]) {
   hf_hull H;
-  hf_frame F;
-  if (!hf_setup(m, d, g1, g2, &H, &F)) return;
-  double dep[HF_MAXPRISM], nrm[HF_MAXPRISM][3], pt[HF_MAXPRISM][3];
+  if (!hf_setup(m, d, g1, g2, &H, F)) return 0;
   int n = 0;
-  const double base = -m->hfield_size[3] - F.t[2];
-  for (int r = F.rmin; r < F.rmax; r++)
-    for (int c = F.cmin; c < F.cmax; c++)
+  const double base = -m->hfield_size[3] - F->t[2];
+  for (int r = F->rmin; r < F->rmax; r++)
+    for (int c = F->cmin; c < F->cmax; c++)
       for (int tri = 0; tri < 2; tri++) {
         double T[3][3];
-        if (!hf_prism_top(m, &F, r, c, tri, T)) continue;
+        if (!hf_prism_top(m, F, r, c, tri, T)) continue;
         if (n >= HF_MAXPRISM) abort(); /* the fixed-capacity list: never reached by a foot-sized hull */
         if (hf_prism_contact(m, &H, (const double(*)[3])T, base, &dep[n], nrm[n], pt[n])) n++;
       }
+  return n;
+}
+
+/* test aid: the prism contacts of height field g_hf vs hull g_cvx before the manifold selection (the
+ * candidates the 4 slots are chosen from), world frame: depth[i] > 0, unit normal (pushes the hull
+ * out), point. Returns their number (at most max). d must hold the kinematics (oracle_forward). */
+int oracle_hfield_contacts(const oracle_model* m, const oracle_data* d, int g_hf, int g_cvx, int max, double* depth,
+                           double* normal, double* point) {
+  if (!m->hfield_data) return 0;
+  hf_frame F;
+  double dep[HF_MAXPRISM], nrm[HF_MAXPRISM][3], pt[HF_MAXPRISM][3];
+  const int n = hf_contacts(m, d, g_hf, g_cvx, &F, dep, nrm, pt);
+  const double *hp = d->geom_xpos[g_hf], *HR = d->geom_xmat[g_hf];
+  int k = 0;
+  for (int i = 0; i < n && k < max; i++, k++) {
+    double pl[3];
+    for (int q = 0; q < 3; q++) pl[q] = pt[i][q] + F.t[q];
+    mulmv3(point + 3 * k, HR, pl);
+    for (int q = 0; q < 3; q++) point[3 * k + q] += hp[q];
+    mulmv3(normal + 3 * k, HR, nrm[i]);
+    depth[k] = dep[i];
+  }
+  return k;
+}
+
+static void collide_hfield_convex(const oracle_model* m, oracle_data* d, int g1, int g2, int slot0) {
+  for (int c = 0; c < DUCK_CON_PER_PAIR; c++) set_inactive(d, slot0 + c, g1, g2);
+  hf_frame F;
+  double dep[HF_MAXPRISM], nrm[HF_MAXPRISM][3], pt[HF_MAXPRISM][3];
+  const int n = hf_contacts(m, d, g1, g2, &F, dep, nrm, pt);
   if (n == 0) return;
   /* 4 of the prism contacts by mjx's _manifold_points over their points, from the deepest (the
    * first in strip order within HF_DEPTH_TIE of the deepest: prisms that share a grid vertex or

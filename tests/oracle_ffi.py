@@ -85,6 +85,8 @@ def lib():
         L.oracle_set_force_start.argtypes = [C.c_int]
         L.oracle_set_hdump.argtypes = [dp]
         L.oracle_set_hf_band_scale.argtypes = [C.c_double]
+        L.oracle_set_hf_tie_last.argtypes = [C.c_double]
+        L.oracle_hfield_contacts.argtypes = [vp, C.POINTER(OracleData), C.c_int, C.c_int, C.c_int, dp, dp, dp]
         L.oracle_set_con_override.argtypes = [dp]
         L.oracle_last_start_costs.argtypes = [C.POINTER(C.c_double)]
         L.oracle_hfield_axis_wins.argtypes = [C.POINTER(C.c_longlong), C.c_int]

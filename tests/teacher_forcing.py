@@ -434,9 +434,14 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     "onset": the two contact sets differ only in slots that are, on each side, inactive or active
     within `onset` (m) of zero depth -- which prisms of a height field touch at the onset is decided
     below fp32 resolution.
-    (Round 3's "sat_tie" and "onset_cascade" rules -- the oracle re-run with the other tied SAT axis,
-    or continued from the GPU's own contact set -- are gone: round 4's contact model is continuous at
-    SAT ties and onset prisms. Round 3's "conditioning" rule -- the oracle merely moving by the GPU's difference under 1e-6
+    "sat_tie": two separating axes of one height-field prism overlap within 1e-6 m (the kernel's fp32
+    error bound on an overlap), and the oracle resolving such ties to the other axis
+    (oracle_set_hf_tie_last) lands on the GPU's result;
+    "onset_selection": the manifold chose other prism contacts around an onset-depth prism -- every GPU
+    slot of the differing pairs is one of the oracle's own prism contacts (oracle_hfield_contacts) or
+    at the onset depth, and the oracle continued from the GPU's slots lands on the GPU's result
+    (round 3's "onset_cascade" checked only the landing: a collision bug in a shallow pair would have
+    passed). Round 3's "conditioning" rule -- the oracle merely moving by the GPU's difference under 1e-6
     perturbations, without landing on it -- is gone: a rule that does not require landing cannot tell
     a defect from a sensitive state, tests/test_gpu_teacher_forced.py::test_explain_has_teeth.)"""
     from tests.helpers import parse_aux
@@ -452,6 +457,16 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     # backward error: the oracle from an fp32-sized perturbation of the input lands on the GPU's result
     if backward_error_landing(om, x, g) is not None:
         return "backward_error"
+    # a height-field prism whose two best separating axes overlap within 1e-6 m (the kernel's fp32 error
+    # bound on an overlap: tied at its precision): the oracle resolving such ties to the other axis
+    # lands on the GPU
+    lib().oracle_set_hf_tie_last(1e-6)
+    try:
+        r = oracle_substep(om, x)
+    finally:
+        lib().oracle_set_hf_tie_last(0.0)
+    if _state_rel(m, g, r) <= sub_tol:
+        return "sat_tie"
     n = env.num_envs
     T = lambda y: torch.tensor(np.tile(y.astype(np.float32)[:, None], (1, n)), device=env.device).contiguous()  # noqa: E731
     tq, tv, tw, tc = (T(y) for y in _split(m, x))
@@ -469,7 +484,52 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     at_onset = ((gd >= 0) | (np.abs(gd) <= onset)) & ((od >= 0) | (np.abs(od) <= onset))
     if differ.any() and at_onset[differ].all():
         return "onset"
+    # the manifold's selection at an onset prism: the 4 slots of a height-field pair are chosen from
+    # its prism contacts, and a prism at the onset depth (in or out below fp32 resolution) changes the
+    # choice. Accepted only if (a) every active GPU slot of a differing pair IS one of the oracle's own
+    # prism contacts of that pair (oracle_hfield_contacts: point within 1e-4 m, depth within 2e-6 m,
+    # normal within 1e-3) or is itself at the onset depth, (b) the oracle's candidates or the GPU's
+    # slots of that pair hold an onset-depth contact, and (c) the oracle continued from the GPU's slots
+    # lands on the GPU's result (everything after collision agrees)
+    pair_differs = differ.reshape(m.npair, 4).any(axis=1)
+    if pair_differs.any() and _onset_selection(m, om, d, ga, pair_differs, onset) and \
+            _state_rel(m, g, oracle_substep_with_contacts(om, x, ga)) <= sub_tol:
+        return "onset_selection"
     return None
+
+
+def _onset_selection(m, om, d, ga, pair_differs, onset) -> bool:
+    import ctypes as C
+    from tests.oracle_ffi import lib
+    floor = m.id("geom", "floor")
+    gd = np.asarray(ga["con_dist"][0], dtype=np.float64)
+    gp = np.asarray(ga["con_pos"][0], dtype=np.float64).reshape(-1, 3)
+    gn = np.asarray(ga["con_normal"][0], dtype=np.float64).reshape(-1, 3)
+    for p in np.nonzero(pair_differs)[0]:
+        g1, g2 = int(m.pair_geom1[p]), int(m.pair_geom2[p])
+        if floor not in (g1, g2):
+            return False                       # only height-field pairs choose among prism contacts
+        foot = g2 if g1 == floor else g1
+        dep, nrm, pt = np.zeros(128), np.zeros(3 * 128), np.zeros(3 * 128)
+        k = lib().oracle_hfield_contacts(om.ptr, C.byref(d), floor, foot, 128, dep.ctypes.data_as(C.POINTER(C.c_double)),
+                                         nrm.ctypes.data_as(C.POINTER(C.c_double)), pt.ctypes.data_as(C.POINTER(C.c_double)))
+        dep, nrm, pt = dep[:k], nrm[:3 * k].reshape(k, 3), pt[:3 * k].reshape(k, 3)
+        cand_onset = bool((dep <= onset).any())
+        slot_onset = False
+        for sl in range(4 * p, 4 * p + 4):
+            if gd[sl] >= 0:
+                continue
+            if -gd[sl] <= onset:
+                slot_onset = True
+                continue
+            nn = gn[sl] / max(np.linalg.norm(gn[sl]), 1e-12)
+            match = (np.abs(pt - gp[sl]).max(axis=1) <= 1e-4) & (np.abs(dep + gd[sl]) <= 2e-6) & \
+                (np.abs(nrm @ nn - 1.0) <= 1e-3)
+            if not match.any():
+                return False                   # a GPU slot the oracle's candidates do not hold
+        if not (cand_onset or slot_onset):
+            return False
+    return True
 
 
 def rule_of(x: dict) -> List[str]:
