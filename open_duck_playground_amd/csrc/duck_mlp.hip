@@ -1,19 +1,23 @@
 // The PPO networks' MLP layers on fp32 MFMA (include/duck_ppo.h: duck_mlp_gemm, duck_mlp_wgrad,
-// duck_mlp_wgrad_reduce). brax's MLP (ppo/networks.py: Dense layers with swish between them, the
-// reference reaches it through common/runner.py:104-118) forward and backward for a minibatch of
-// N rows as a handful of GEMM launches with the elementwise work fused into their loads and stores:
+// duck_mlp_wgrad_reduce, duck_policy_sample). brax's MLP (ppo/networks.py: Dense layers with swish
+// between them, the reference reaches it through common/runner.py:104-118) forward and backward for a
+// minibatch of N rows as a handful of GEMM launches with the elementwise work fused into their loads
+// and stores:
 //
 //   forward   Z = op(X) W^T + b, H = silu(Z)       (op: the observation normaliser on the first layer)
 //   backward  dZ_prev = (dZ W) * silu'(Z_prev)      (the activation's derivative in the epilogue)
-//   weights   dW = dZ^T H_prev, db = sum_n dZ        (split over the batch rows; the partial products
+//   weights   [dW | db] = dZ^T [H | 1]             (the bias gradient as one more column of ones; split
+//                                                    over row blocks of the batch, the partial products
 //                                                    summed in fixed order by duck_mlp_wgrad_reduce:
 //                                                    deterministic, no atomics)
 //
 // v_mfma_f32_16x16x4_f32 (exact f32 products, fp32 accumulation: a k-ordered fmaf chain). A
-// 256-thread workgroup computes a 64 x 64 output tile, each wave 32 x 32 as 2 x 2 MFMA tiles (four
-// independent accumulators cover the instruction's 40-cycle dependent latency); operands pass
-// through LDS in 32-deep reduction chunks, the next chunk's global loads issued before the current
-// chunk's MFMAs (software pipelined), LDS rows padded to 33 floats (conflict-free fragment reads).
+// 256-thread workgroup computes a 64 x 32 output tile, each wave 32 x 16 as 2 x 1 MFMA tiles; operands
+// pass through one LDS buffer per operand in 32-deep reduction chunks, the next chunk's global loads
+// in flight during the current chunk's MFMAs; 12.7 KB of LDS and small tiles keep several
+// workgroups per CU resident, so one workgroup's load latency hides behind another's MFMAs (the
+// learner's GEMMs are 5120 rows deep and at most 512 wide: a 64 x 64 tile left ~1 workgroup per CU
+// and ran 3-4x slower). LDS rows padded to 33 floats.
 #include <hip/hip_runtime.h>
 
 #include "duck_common.h"
@@ -22,134 +26,173 @@
 
 namespace {
 
-constexpr int MT = 64;    // output tile rows (the batch dimension for the forward / dX GEMMs)
-constexpr int NT = 64;    // output tile columns
+constexpr int BM = 64;    // output tile rows (the batch rows for the forward / data-gradient GEMMs)
+constexpr int BN = 32;    // output tile columns
 constexpr int KC = 32;    // reduction chunk
 constexpr int LDP = KC + 1;
 using f4 = __attribute__((ext_vector_type(4))) float;
 
 __device__ __forceinline__ float sigm(float z) { return 1.f / (1.f + __expf(-z)); }
 
-// A tile [64 rows][KC] from a matrix whose REDUCTION index is contiguous (row stride ld): X for
-// the forward (rows n, reduction k), dZ for dX (rows n, reduction m). 256 threads x 2 float4.
-// norm: (x - mean[k]) * istd[k] on the way in (the first layer's observation normaliser).
-struct LoadRowMajor {
-  float v[8];
-  __device__ void load(const float* __restrict__ A, int ld, int rows, int red, int r0, int k0,
-                       const float* __restrict__ mean, const float* __restrict__ istd) {
+// ROWS x KC tile of a matrix whose REDUCTION index is contiguous (row stride ld): X for the forward
+// (rows n, reduction k), dZ for the data gradient (rows n, reduction m). Thread t holds rows
+// t / 8 (+ 32 p) and the 4 reduction indices 4 (t % 8) .. + 3 of every chunk; row pointers are
+// formed once. norm: (x - mean[k]) * istd[k] on the way in (the first layer's normaliser).
+template <int ROWS>
+struct RowTile {
+  static constexpr int P = ROWS / 32;
+  const float* rp[P];
+  bool ok[P];
+  float v[4 * P];
+  __device__ void init(const float* __restrict__ A, int ld, int rows, int r0) {
 #pragma unroll
-    for (int p = 0; p < 2; p++) {
-      const int t = threadIdx.x + 256 * p, r = t >> 3, c = 4 * (t & 7);
-      const int gr = r0 + r;
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int gk = k0 + c + q;
-        float x = (gr < rows && gk < red) ? A[(size_t)gr * ld + gk] : 0.f;
-        if (mean && gk < red) x = (x - mean[gk]) * istd[gk];
-        v[4 * p + q] = x;
-      }
+    for (int p = 0; p < P; p++) {
+      const int r = r0 + ((int)threadIdx.x >> 3) + 32 * p;
+      ok[p] = r < rows;
+      rp[p] = A + (size_t)(ok[p] ? r : 0) * ld;
     }
   }
-  __device__ void store(float* S) const {  // S[row][k]
+  __device__ void load(int red, int k0, const float* __restrict__ mean, const float* __restrict__ istd) {
+    const int c = k0 + 4 * ((int)threadIdx.x & 7);
 #pragma unroll
-    for (int p = 0; p < 2; p++) {
-      const int t = threadIdx.x + 256 * p, r = t >> 3, c = 4 * (t & 7);
+    for (int p = 0; p < P; p++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int k = c + q;
+        float x = (ok[p] && k < red) ? rp[p][k] : 0.f;
+        if (mean) x = k < red ? (x - mean[k]) * istd[k] : 0.f;
+        v[4 * p + q] = x;
+      }
+  }
+  __device__ void store(float* S) const {  // S[row][k]
+    const int c = 4 * ((int)threadIdx.x & 7);
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+      const int r = ((int)threadIdx.x >> 3) + 32 * p;
 #pragma unroll
       for (int q = 0; q < 4; q++) S[r * LDP + c + q] = v[4 * p + q];
     }
   }
 };
 
-// A tile [64 columns][KC] from a matrix whose OUTPUT index is contiguous and whose reduction index
-// runs over its rows (W for dX: W[m][k'], reduction m; dZ and H for the weight gradient: rows n):
-// global rows k0..k0+31, columns c0..c0+63, stored transposed as S[column][k].
-struct LoadColMajor {
-  float v[8];
-  __device__ void load(const float* __restrict__ B, int ld, int red, int cols, int k0, int c0) {
+// KC x COLS tile of a matrix whose OUTPUT index is contiguous and whose reduction index runs over its
+// rows (W for the data gradient; dZ and H for the weight gradient), stored transposed as S[col][k].
+// Thread t holds columns 4 (t % (COLS / 4)) .. + 3 of reduction rows t / (COLS / 4) (+ step).
+// ones: column `cols` reads 1 (the bias gradient as one more weight-gradient column).
+template <int COLS>
+struct ColTile {
+  static constexpr int TPR = COLS / 4, RSTEP = 256 / TPR, P = KC / RSTEP;
+  float v[4 * P];
+  __device__ void load(const float* __restrict__ B, int ld, int red, int cols, int k0, int c0, bool ones,
+                       const float* __restrict__ mean, const float* __restrict__ istd) {
+    const int c = c0 + 4 * ((int)threadIdx.x % TPR);
+    const bool vec = ((ld & 3) == 0) && (((size_t)B & 15) == 0) && c + 3 < cols;
 #pragma unroll
-    for (int p = 0; p < 2; p++) {
-      const int t = threadIdx.x + 256 * p, r = t >> 4, c = 4 * (t & 15);
-      const int gk = k0 + r;
+    for (int p = 0; p < P; p++) {
+      const int k = k0 + (int)threadIdx.x / TPR + RSTEP * p;
+      const bool kr = k < red;
+      const float* row = B + (size_t)(kr ? k : 0) * ld;
+      if (vec) {
+        const f4 x = kr ? *(const f4*)(row + c) : f4{0.f, 0.f, 0.f, 0.f};
+        v[4 * p] = x[0]; v[4 * p + 1] = x[1]; v[4 * p + 2] = x[2]; v[4 * p + 3] = x[3];
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int gc = c0 + c + q;
-        v[4 * p + q] = (gk < red && gc < cols) ? B[(size_t)gk * ld + gc] : 0.f;
+        for (int q = 0; q < 4; q++) {
+          const int cc = c + q;
+          v[4 * p + q] = (kr && cc < cols) ? row[cc] : ((kr && ones && cc == cols) ? 1.f : 0.f);
+        }
+      }
+      if (mean) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int cc = c + q;
+          if (kr && cc < cols) v[4 * p + q] = (v[4 * p + q] - mean[cc]) * istd[cc];
+        }
       }
     }
   }
   __device__ void store(float* S) const {
+    const int c = 4 * ((int)threadIdx.x % TPR);
 #pragma unroll
-    for (int p = 0; p < 2; p++) {
-      const int t = threadIdx.x + 256 * p, r = t >> 4, c = 4 * (t & 15);
+    for (int p = 0; p < P; p++) {
+      const int r = (int)threadIdx.x / TPR + RSTEP * p;
 #pragma unroll
       for (int q = 0; q < 4; q++) S[(c + q) * LDP + r] = v[4 * p + q];
     }
   }
 };
 
-// the 2 x 2 MFMA tiles of this wave over one LDS chunk: As[row][k], Bs[col][k]
-__device__ __forceinline__ void mma_chunk(const float* As, const float* Bs, int wr, int wc, f4 (&acc)[2][2]) {
+// this wave's TI x TJ MFMA tiles over one LDS chunk: As[row][k], Bs[col][k]
+template <int TI, int TJ>
+__device__ __forceinline__ void mma_chunk(const float* As, const float* Bs, int wr, int wc, f4 (&acc)[TI][TJ]) {
   const int l = threadIdx.x & 63, li = l & 15, lk = l >> 4;
 #pragma unroll
   for (int s = 0; s < KC / 4; s++) {
     const int k = 4 * s + lk;
-    const float a0 = As[(wr + li) * LDP + k], a1 = As[(wr + 16 + li) * LDP + k];
-    const float b0 = Bs[(wc + li) * LDP + k], b1 = Bs[(wc + 16 + li) * LDP + k];
-    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+    float a[TI], b[TJ];
+#pragma unroll
+    for (int i = 0; i < TI; i++) a[i] = As[(wr + 16 * i + li) * LDP + k];
+#pragma unroll
+    for (int j = 0; j < TJ; j++) b[j] = Bs[(wc + 16 * j + li) * LDP + k];
+#pragma unroll
+    for (int i = 0; i < TI; i++)
+#pragma unroll
+      for (int j = 0; j < TJ; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
   }
 }
 
-// Forward (MODE 0: Y = op(X) W^T + b; MODE 1: the same, Y = Z and Y2 = silu(Z)) and the backward
-// data GEMM (MODE 2: Y = (dZ W) * silu'(Zp), Zp = aux). Output [N][Mo], tile (blockIdx.x: rows,
-// blockIdx.y: columns).
+// Forward (MODE 0: Y = op(A) W^T + b; MODE 1: the same, Y = Z and Y2 = silu(Z)) and the data gradient
+// (MODE 2: Y = (A W) * silu'(aux), A = dZ [N][R], W [R][Mo], aux = Z_prev). Output [N][Mo].
 template <int MODE>
 __global__ __launch_bounds__(256) void mlp_gemm_kernel(int N, int R, int Mo, const float* __restrict__ A,
                                                        const float* __restrict__ W, const float* __restrict__ bias,
                                                        const float* __restrict__ aux, float* __restrict__ Y,
                                                        float* __restrict__ Y2, const float* __restrict__ mean,
                                                        const float* __restrict__ istd) {
-  __shared__ float As[2][MT * LDP], Bs[2][NT * LDP];
-  const int r0 = blockIdx.x * MT, c0 = blockIdx.y * NT;
-  const int w = threadIdx.x >> 6, wr = 32 * (w >> 1), wc = 32 * (w & 1);
-  f4 acc[2][2];
+  constexpr int TI = BM / 32, TJ = BN / 32;
+  __shared__ float As[BM * LDP], Bs[BN * LDP];
+  const int r0 = blockIdx.x * BM, c0 = blockIdx.y * BN;
+  const int w = threadIdx.x >> 6, wr = (BM / 2) * (w >> 1), wc = (BN / 2) * (w & 1);
+  f4 acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 2; i++)
+  for (int i = 0; i < TI; i++)
 #pragma unroll
-    for (int j = 0; j < 2; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  LoadRowMajor la;
-  LoadRowMajor lbr;  // MODE 0/1: W[m][k], reduction k contiguous (as X)
-  LoadColMajor lbc;  // MODE 2: W[m][k'], reduction m over rows
-  const int ldA = R;
+    for (int j = 0; j < TJ; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  RowTile<BM> la;
+  RowTile<BN> lbr;  // MODE 0/1: the rows of W (output columns), reduction contiguous
+  ColTile<BN> lbc;  // MODE 2: W [R][Mo], reduction over its rows
+  la.init(A, R, N, r0);
+  if (MODE != 2) lbr.init(W, R, Mo, c0);
+  const float* mn = MODE == 2 ? nullptr : mean;
   auto load = [&](int k0) {
-    la.load(A, ldA, N, R, r0, k0, MODE == 2 ? nullptr : mean, istd);
-    if (MODE == 2) lbc.load(W, Mo, R, Mo, k0, c0);
-    else lbr.load(W, R, Mo, R, c0, k0, nullptr, nullptr);
+    la.load(R, k0, mn, istd);
+    if (MODE == 2) lbc.load(W, Mo, R, Mo, k0, c0, false, nullptr, nullptr);
+    else lbr.load(R, k0, nullptr, nullptr);
   };
-  auto store = [&](int b) {
-    la.store(As[b]);
-    if (MODE == 2) lbc.store(Bs[b]);
-    else lbr.store(Bs[b]);
+  auto store = [&]() {
+    la.store(As);
+    if (MODE == 2) lbc.store(Bs);
+    else lbr.store(Bs);
   };
   const int nch = (R + KC - 1) / KC;
   load(0);
-  store(0);
+  store();
   __syncthreads();
   for (int c = 0; c < nch; c++) {
-    const int b = c & 1;
     if (c + 1 < nch) load(KC * (c + 1));  // in flight while this chunk's MFMAs run
-    mma_chunk(As[b], Bs[b], wr, wc, acc);
-    if (c + 1 < nch) store(b ^ 1);
+    mma_chunk<TI, TJ>(As, Bs, wr, wc, acc);
     __syncthreads();
+    if (c + 1 < nch) {
+      store();
+      __syncthreads();
+    }
   }
   // epilogue: acc[i][j][q] is C[wr + 16 i + 4 (l >> 4) + q][wc + 16 j + (l & 15)]
   const int l = threadIdx.x & 63;
 #pragma unroll
-  for (int i = 0; i < 2; i++)
+  for (int i = 0; i < TI; i++)
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
+    for (int j = 0; j < TJ; j++) {
       const int col = c0 + wc + 16 * j + (l & 15);
       if (col >= Mo) continue;
       const float bj = (MODE != 2 && bias) ? bias[col] : 0.f;
@@ -172,77 +215,62 @@ __global__ __launch_bounds__(256) void mlp_gemm_kernel(int N, int R, int Mo, con
     }
 }
 
-// dW[m][k] = sum over this block's rows n of dZ[n][m] H[n][k] (+ the bias partial sum_n dZ[n][m]
-// on the k-tile-0 blocks): partial s = blockIdx.z of S, written to part + s * P at the layer's
-// offsets (weights at offw, bias at offb, P = the parameter count of the whole network).
+// [dW | db][m][k] = sum over this workgroup's rows n of dZ[n][m] [op(H) | 1][n][k]: partial s =
+// blockIdx.z, written to part + s * P at the layer's offsets (weights at offw, bias at offb; P = the
+// parameter count of the networks sharing the partial array).
 __global__ __launch_bounds__(256) void mlp_wgrad_kernel(int N, int Mo, int Ki, const float* __restrict__ dZ,
                                                         const float* __restrict__ H, const float* __restrict__ mean,
                                                         const float* __restrict__ istd, int rows_per_split,
                                                         float* __restrict__ part, int P, int offw, int offb) {
-  __shared__ float As[2][MT * LDP], Bs[2][NT * LDP];
-  const int m0 = blockIdx.x * MT, k0c = blockIdx.y * NT, s = blockIdx.z;
-  const int n_lo = s * rows_per_split, n_hi = min(N, n_lo + rows_per_split);
-  const int w = threadIdx.x >> 6, wr = 32 * (w >> 1), wc = 32 * (w & 1);
-  f4 acc[2][2];
+  constexpr int TI = BM / 32, TJ = BN / 32;
+  __shared__ float As[BM * LDP], Bs[BN * LDP];
+  const int m0 = blockIdx.x * BM, k0c = blockIdx.y * BN, s = blockIdx.z;
+  const int n_lo = s * rows_per_split, R = min(N, n_lo + rows_per_split) - n_lo;
+  const int w = threadIdx.x >> 6, wr = (BM / 2) * (w >> 1), wc = (BN / 2) * (w & 1);
+  f4 acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 2; i++)
+  for (int i = 0; i < TI; i++)
 #pragma unroll
-    for (int j = 0; j < 2; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  LoadColMajor la, lb;  // A = dZ^T (columns m, reduction n over rows), B = H (columns k, rows n)
-  float bsum = 0.f;     // bias partial of column m0 + (tid & 63) (k-tile 0 only)
-  const bool dob = blockIdx.y == 0;
+    for (int j = 0; j < TJ; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  ColTile<BM> la;  // A = dZ^T: columns m, reduction n over the rows
+  ColTile<BN> lb;  // B = [op(H) | 1]: columns k, rows n
+  const float* dz = dZ + (size_t)(R > 0 ? n_lo : 0) * Mo;
+  const float* h = H + (size_t)(R > 0 ? n_lo : 0) * Ki;
   auto load = [&](int n0) {
-    la.load(dZ + (size_t)n_lo * Mo, Mo, n_hi - n_lo, Mo, n0, m0);
-    lb.load(H + (size_t)n_lo * Ki, Ki, n_hi - n_lo, Ki, n0, k0c);
-    if (mean) {  // the first layer's input is the normalised observation
-#pragma unroll
-      for (int p = 0; p < 2; p++) {
-        const int t = threadIdx.x + 256 * p, r = t >> 4, c = 4 * (t & 15);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int gk = k0c + c + q;
-          if (n0 + r < n_hi - n_lo && gk < Ki) lb.v[4 * p + q] = (lb.v[4 * p + q] - mean[gk]) * istd[gk];
-        }
-      }
-    }
+    la.load(dz, Mo, R, Mo, n0, m0, false, nullptr, nullptr);
+    lb.load(h, Ki, R, Ki, n0, k0c, true, mean, istd);
   };
-  auto store = [&](int b) {
-    la.store(As[b]);
-    lb.store(Bs[b]);
-  };
-  const int R = n_hi - n_lo;
   const int nch = (R + KC - 1) / KC;
   if (nch > 0) {
     load(0);
-    store(0);
+    la.store(As);
+    lb.store(Bs);
   }
   __syncthreads();
   for (int c = 0; c < nch; c++) {
-    const int b = c & 1;
     if (c + 1 < nch) load(KC * (c + 1));
-    mma_chunk(As[b], Bs[b], wr, wc, acc);
-    if (dob && threadIdx.x < 64) {
-#pragma unroll 8
-      for (int k = 0; k < KC; k++) bsum += As[b][threadIdx.x * LDP + k];
-    }
-    if (c + 1 < nch) store(b ^ 1);
+    mma_chunk<TI, TJ>(As, Bs, wr, wc, acc);
     __syncthreads();
+    if (c + 1 < nch) {
+      la.store(As);
+      lb.store(Bs);
+      __syncthreads();
+    }
   }
   float* out = part + (size_t)s * P;
   const int l = threadIdx.x & 63;
 #pragma unroll
-  for (int i = 0; i < 2; i++)
+  for (int i = 0; i < TI; i++)
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
+    for (int j = 0; j < TJ; j++) {
       const int col = k0c + wc + 16 * j + (l & 15);
-      if (col >= Ki) continue;
+      if (col > Ki) continue;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int row = m0 + wr + 16 * i + 4 * (l >> 4) + q;
-        if (row < Mo) out[offw + (size_t)row * Ki + col] = acc[i][j][q];
+        if (row < Mo) out[col < Ki ? offw + (size_t)row * Ki + col : offb + row] = acc[i][j][q];
       }
     }
-  if (dob && threadIdx.x < 64 && m0 + (int)threadIdx.x < Mo) out[offb + m0 + threadIdx.x] = bsum;
 }
 
 // grad[i] = sum_s part[s * P + i], s in order (deterministic)
@@ -254,7 +282,6 @@ __global__ __launch_bounds__(256) void mlp_reduce_kernel(int P, int S, const flo
   for (int s = 0; s < S; s++) a += part[(size_t)s * P + i];
   grad[i] = a;
 }
-
 
 // brax NormalTanhDistribution sampling for the rollout (ppo/networks.py; ppo.NormalTanh): one thread
 // per env row, raw = loc + scale eps with scale = softplus(pre) + 1e-3 and eps ~ N(0, 1) by
@@ -306,7 +333,7 @@ extern "C" int duck_mlp_gemm(int mode, int N, int R, int M, const float* A, cons
   if (N == 0) return DUCK_OK;
   if (!A || !W || !Y || (mode == 1 && !Y2) || (mode == 2 && !aux) || (!mean) != (!istd))
     return duck_fail(DUCK_EINVAL, "duck_mlp_gemm: null pointer");
-  const dim3 grid((N + MT - 1) / MT, (M + NT - 1) / NT);
+  const dim3 grid((N + BM - 1) / BM, (M + BN - 1) / BN);
   hipStream_t st = (hipStream_t)stream;
   switch (mode) {
     case 0: hipLaunchKernelGGL(mlp_gemm_kernel<0>, grid, dim3(256), 0, st, N, R, M, A, W, bias, aux, Y, Y2, mean, istd); break;
@@ -329,7 +356,7 @@ extern "C" int duck_mlp_wgrad(int N, int M, int K, const float* dZ, const float*
   if (off_w < 0 || off_b < 0 || (long long)off_w + (long long)M * K > P || off_b + M > P)
     return duck_fail(DUCK_EINVAL, "duck_mlp_wgrad: offsets outside the parameter vector");
   const int rps = (N + splits - 1) / splits;
-  const dim3 grid((M + MT - 1) / MT, (K + NT - 1) / NT, splits);
+  const dim3 grid((M + BM - 1) / BM, (K + 1 + BN - 1) / BN, splits);  // K + 1: the bias column
   hipLaunchKernelGGL(mlp_wgrad_kernel, grid, dim3(256), 0, (hipStream_t)stream, N, M, K, dZ, H, mean, istd, rps,
                      partial, P, off_w, off_b);
   HIPCHECK(hipGetLastError());

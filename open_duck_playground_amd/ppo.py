@@ -350,7 +350,7 @@ class FusedGrad:
     The parameters' ``.grad`` are views of one flat buffer that the final reduction overwrites (never
     set to None), so the all-reduce over ranks is a single collective on that buffer."""
 
-    SPLITS = 8
+    SPLITS = 16      # partial products per weight gradient at most (duck_mlp_wgrad's row blocks)
 
     def __init__(self, net: ActorCritic, rows: int, boot_rows: int, device):
         from .native import lib
@@ -364,7 +364,8 @@ class FusedGrad:
             self.off[id(p)] = o
             p.grad = self.flat[o:o + p.numel()].view_as(p)
             o += p.numel()
-        self.part = torch.empty(self.SPLITS * self.P, device=device)
+        # zeroed once: a layer that uses fewer row blocks than SPLITS leaves its other partials at 0
+        self.part = torch.zeros(self.SPLITS * self.P, device=device)
         self.pol = [m for m in net.policy if isinstance(m, nn.Linear)]
         self.val = [m for m in net.value if isinstance(m, nn.Linear)]
         self.N, self.Nv = rows, rows + boot_rows
@@ -402,8 +403,11 @@ class FusedGrad:
             m = layers[i]
             h = x if i == 0 else b["H"][i - 1]
             mean, istd = (norm.mean32.data_ptr(), norm.istd32.data_ptr()) if (i == 0 and norm is not None) else (None, None)
+            # row blocks: enough workgroups to fill the chip (64 x 32 tiles over [W | b])
+            tiles = -(-m.out_features // 64) * -(-(m.in_features + 1) // 32)
+            splits = max(1, min(self.SPLITS, -(-768 // tiles), n // 64))
             check(self.lib.duck_mlp_wgrad(n, m.out_features, m.in_features, d.data_ptr(), h.data_ptr(), mean, istd,
-                                          self.SPLITS, self.part.data_ptr(), self.P, self.off[id(m.weight)],
+                                          splits, self.part.data_ptr(), self.P, self.off[id(m.weight)],
                                           self.off[id(m.bias)], stream))
             if i > 0:
                 dz = b["dZ"][i - 1]
