@@ -415,7 +415,23 @@ class FusedGrad:
                                              None, b["Z"][i - 1].data_ptr(), dz.data_ptr(), None, None, None, stream))
                 d = dz
 
+    def gather(self, data: Dict[str, torch.Tensor], idx: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """The minibatch's trajectories (columns idx of the [T, B, ...] buffers) into persistent buffers:
+        the value network's input [priv rows | the bootstrap rows] assembled in place (no cat), and of
+        next_priv only the last step (the bootstrap observation; the rest is never read)."""
+        T, mb = data["reward"].shape[0], idx.numel()
+        if not hasattr(self, "_mb"):
+            self._mb = {k: torch.empty((T, mb) + v.shape[2:], device=v.device, dtype=v.dtype)
+                        for k, v in data.items() if k not in ("priv", "next_priv")}
+            self._xv = torch.empty(self.Nv, data["priv"].shape[-1], device=idx.device)
+        for k, buf in self._mb.items():
+            torch.index_select(data[k], 1, idx, out=buf)
+        torch.index_select(data["priv"], 1, idx, out=self._xv[:self.N].view(T, mb, -1))
+        torch.index_select(data["next_priv"][-1], 0, idx, out=self._xv[self.N:])
+        return {**self._mb, "xv": self._xv}
+
     def __call__(self, mb: Dict[str, torch.Tensor], cfg: PPOConfig, gen: Optional[torch.Generator]):
+        """mb: the minibatch [T, B, ...] (gather's output, or any dict with obs, priv, next_priv, ...)"""
         from .native import check
         net = self.net
         T, B = mb["reward"].shape
@@ -425,7 +441,7 @@ class FusedGrad:
         st = torch.cuda.current_stream(self.flat.device).cuda_stream
         on, pn = (net.obs_norm, net.priv_norm) if net.normalize else (None, None)
         obs = mb["obs"].reshape(N, -1)
-        xv = torch.cat([mb["priv"].reshape(N, -1), mb["next_priv"][-1]], 0)
+        xv = mb["xv"] if "xv" in mb else torch.cat([mb["priv"].reshape(N, -1), mb["next_priv"][-1]], 0)
         logits = self._forward(self.pol, self.bp, obs, on, N, st)
         v_all = self._forward(self.val, self.bv, xv, pn, self.Nv, st).view(-1)
         baseline, bootstrap = v_all[:N].view(T, B), v_all[N:]
@@ -511,9 +527,9 @@ class _Learner:
         self.out = None
 
     def _fwd_bwd(self):
+        if self.fused is not None:   # writes every .grad (views of one flat buffer)
+            return self.fused(self.fused.gather(self.data, self.idx), self.cfg, None)
         mbatch = {k: v[:, self.idx] for k, v in self.data.items()}
-        if self.fused is not None:
-            return self.fused(mbatch, self.cfg, None)   # writes every .grad (views of one flat buffer)
         loss, m = ppo_loss(self.net, mbatch, self.cfg, None)
         # gradients set to None before the backward that is captured: it then writes them instead of
         # zero-filling and accumulating (one fill + one add kernel per parameter tensor saved)

@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
 T=${1:-ppo}
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof_$T -o prof -- python3 $GRAFT_REPO_ROOT/tools/ppo_throughput.py --updates 2 > $GRAFT_REPO_ROOT/$OUT/prof_$T.log 2>&1 || { tail -5 $GRAFT_REPO_ROOT/$OUT/prof_$T.log; exit 1; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/prof_$T -o prof -- python3 $GRAFT_REPO_ROOT/tools/ppo_throughput.py --updates 2 > $GRAFT_REPO_ROOT/$OUT/prof_$T.log 2>&1 || { tail -5 $GRAFT_REPO_ROOT/$OUT/prof_$T.log; exit 1; }
 cd $GRAFT_REPO_ROOT
 f=$(find $OUT/prof_$T -name "*kernel_stats.csv" | head -1)
 python3 - "$f" <<'PY'
