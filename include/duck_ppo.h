@@ -65,6 +65,14 @@ int duck_mlp_wgrad_reduce(int P, int splits, const float* partial, float* grad, 
  * captured graph draws fresh noise on every replay). A <= 16. */
 int duck_policy_sample(int N, int A, const float* logits, unsigned long long seed, unsigned int* ctr, float* raw,
                        float* logprob, float* action, void* stream);
+/* The learner's parameter update on flat buffers of P floats (both networks): clip_grad_norm_(max_norm)
+ * then Adam (torch.optim.Adam / optax.adam): g' = g min(1, max_norm / (|g| + 1e-6)),
+ * m = b1 m + (1 - b1) g', v = b2 v + (1 - b2) g'^2, t = ++*step,
+ * param -= lr / (1 - b1^t) m / (sqrt(v) / sqrt(1 - b2^t) + eps). Two launches; `step` a device int,
+ * `scratch` duck_clip_adam_scratch_size(P) floats. */
+int duck_clip_adam(int P, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float* scratch,
+                   int* step, float lr, float beta1, float beta2, float eps, float max_norm, void* stream);
+int duck_clip_adam_scratch_size(int P);
 
 #ifdef __cplusplus
 }

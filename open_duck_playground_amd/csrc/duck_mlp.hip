@@ -324,6 +324,70 @@ __global__ __launch_bounds__(256) void policy_sample_kernel(int N, int A, const 
 
 __global__ void ctr_inc_kernel(uint32_t* ctr) { *ctr += 1u; }
 
+
+// The learner's update after the gradient all-reduce, on the flat parameter / gradient / moment
+// buffers of both networks (ppo.FusedGrad): torch.nn.utils.clip_grad_norm_ then torch.optim.Adam
+// (optax.adam in brax: the same moments and bias corrections), in two launches instead of ~10.
+// Launch 1: per-workgroup partial sums of g^2 (fixed order), and the step counter advanced (a
+// captured graph replays with the device counter). Launch 2: every workgroup sums the partials in
+// the same order (the same norm everywhere), scales by min(1, max_norm / (norm + 1e-6)) and applies
+// m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2, p -= lr / (1 - b1^t) m / (sqrt(v) / sqrt(1 - b2^t) + eps).
+constexpr int ADAM_TPB = 256, ADAM_PER = 8;  // a workgroup covers 2048 entries
+
+__global__ __launch_bounds__(ADAM_TPB) void adam_norm_kernel(int P, const float* __restrict__ g,
+                                                             float* __restrict__ partial, int* __restrict__ step) {
+  __shared__ float red[ADAM_TPB / 64];
+  const int base = blockIdx.x * ADAM_TPB * ADAM_PER;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < ADAM_PER; j++) {
+    const int i = base + j * ADAM_TPB + threadIdx.x;
+    const float x = i < P ? g[i] : 0.f;
+    s += x * x;
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < ADAM_TPB / 64; w++) t += red[w];
+    partial[blockIdx.x] = t;
+    if (blockIdx.x == 0) *step += 1;
+  }
+}
+
+__global__ __launch_bounds__(ADAM_TPB) void adam_update_kernel(int P, int nblk, float* __restrict__ p,
+                                                               const float* __restrict__ g, float* __restrict__ m,
+                                                               float* __restrict__ v, const float* __restrict__ partial,
+                                                               const int* __restrict__ step, float lr, float b1,
+                                                               float b2, float eps, float max_norm) {
+  __shared__ float coef;
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int b = 0; b < nblk; b++) t += partial[b];
+    const float norm = sqrtf((float)t);
+    const float c = max_norm > 0.f ? max_norm / (norm + 1e-6f) : 1.f;
+    coef = c < 1.f ? c : 1.f;
+  }
+  __syncthreads();
+  const float k = coef;
+  const float ts = (float)*step;
+  const float bc1 = 1.f - powf(b1, ts), bc2s = sqrtf(1.f - powf(b2, ts));
+  const float step_size = lr / bc1;
+  const int base = blockIdx.x * ADAM_TPB * ADAM_PER;
+#pragma unroll
+  for (int j = 0; j < ADAM_PER; j++) {
+    const int i = base + j * ADAM_TPB + threadIdx.x;
+    if (i >= P) continue;
+    const float gi = g[i] * k;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] -= step_size * mi / (sqrtf(vi) / bc2s + eps);
+  }
+}
+
 }  // namespace
 
 extern "C" int duck_mlp_gemm(int mode, int N, int R, int M, const float* A, const float* W, const float* bias,
@@ -384,3 +448,20 @@ extern "C" int duck_policy_sample(int N, int A, const float* logits, unsigned lo
   HIPCHECK(hipGetLastError());
   return DUCK_OK;
 }
+
+extern "C" int duck_clip_adam(int P, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                              float* scratch, int* step, float lr, float beta1, float beta2, float eps,
+                              float max_norm, void* stream) {
+  if (P <= 0) return duck_fail(DUCK_EINVAL, "duck_clip_adam: empty parameter vector");
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !scratch || !step)
+    return duck_fail(DUCK_EINVAL, "duck_clip_adam: null pointer");
+  const int nblk = (P + ADAM_TPB * ADAM_PER - 1) / (ADAM_TPB * ADAM_PER);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adam_norm_kernel, dim3(nblk), dim3(ADAM_TPB), 0, st, P, grad, scratch, step);
+  hipLaunchKernelGGL(adam_update_kernel, dim3(nblk), dim3(ADAM_TPB), 0, st, P, nblk, param, grad, exp_avg, exp_avg_sq,
+                     scratch, step, lr, beta1, beta2, eps, max_norm);
+  HIPCHECK(hipGetLastError());
+  return DUCK_OK;
+}
+
+extern "C" int duck_clip_adam_scratch_size(int P) { return (P + ADAM_TPB * ADAM_PER - 1) / (ADAM_TPB * ADAM_PER); }

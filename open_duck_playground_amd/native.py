@@ -23,7 +23,7 @@ EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get"
            "duck_debug_stage_cycles", "duck_model_fingerprint", "duck_model_supported",
            "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae", "duck_ppo_loss",
            "duck_ppo_loss_out_size", "duck_mlp_gemm", "duck_mlp_wgrad", "duck_mlp_wgrad_reduce",
-           "duck_policy_sample"]
+           "duck_policy_sample", "duck_clip_adam", "duck_clip_adam_scratch_size"]
 
 
 class DuckError(RuntimeError):
@@ -250,6 +250,9 @@ def lib(path: str = None):
             L.duck_mlp_wgrad.argtypes = [ci, ci, ci, vp, vp, vp, vp, ci, vp, ci, ci, ci, vp]
             L.duck_mlp_wgrad_reduce.argtypes = [ci, ci, vp, vp, vp]
             L.duck_policy_sample.argtypes = [ci, ci, vp, C.c_uint64, vp, vp, vp, vp, vp]
+            cf = C.c_float
+            L.duck_clip_adam.argtypes = [ci, vp, vp, vp, vp, vp, vp, cf, cf, cf, cf, cf, vp]
+            L.duck_clip_adam_scratch_size.argtypes = [ci]
         _libs[path] = L
     return _libs[path]
 

@@ -359,11 +359,19 @@ class FusedGrad:
         self.params = list(net.parameters())
         self.P = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(self.P, device=device)
+        # the parameters become views of one flat buffer too (same values, same module / state dict), so
+        # clip + Adam is one pass over flat arrays (duck_clip_adam)
+        self.pflat = torch.cat([p.detach().reshape(-1) for p in self.params]).contiguous()
         self.off, o = {}, 0
         for p in self.params:
             self.off[id(p)] = o
+            p.data = self.pflat[o:o + p.numel()].view_as(p)
             p.grad = self.flat[o:o + p.numel()].view_as(p)
             o += p.numel()
+        self.exp_avg = torch.zeros(self.P, device=device)
+        self.exp_avg_sq = torch.zeros(self.P, device=device)
+        self.adam_step = torch.zeros(1, dtype=torch.int32, device=device)
+        self.adam_scratch = torch.zeros(self.lib.duck_clip_adam_scratch_size(self.P), device=device)
         # zeroed once: a layer that uses fewer row blocks than SPLITS leaves its other partials at 0
         self.part = torch.zeros(self.SPLITS * self.P, device=device)
         self.pol = [m for m in net.policy if isinstance(m, nn.Linear)]
@@ -463,6 +471,15 @@ class FusedGrad:
         return {"loss": o[0], "policy_loss": o[1], "v_loss": o[2], "entropy": o[3]}
 
 
+def _fused_update(fg: "FusedGrad", cfg: PPOConfig) -> None:
+    """clip_grad_norm_(max_grad_norm) + Adam(learning_rate) on FusedGrad's flat buffers (duck_clip_adam)"""
+    from .native import check
+    st = torch.cuda.current_stream(fg.flat.device).cuda_stream
+    check(fg.lib.duck_clip_adam(fg.P, fg.pflat.data_ptr(), fg.flat.data_ptr(), fg.exp_avg.data_ptr(),
+                                fg.exp_avg_sq.data_ptr(), fg.adam_scratch.data_ptr(), fg.adam_step.data_ptr(),
+                                float(cfg.learning_rate), 0.9, 0.999, 1e-8, float(cfg.max_grad_norm or 0.0), st))
+
+
 def fused_grad_available(device) -> bool:
     """the fused learner runs on the GPU when libduck.so exports the duck_mlp_* kernels
     (DUCK_PPO_FUSED_MLP=0 keeps the autograd learner)"""
@@ -538,6 +555,9 @@ class _Learner:
         return {"loss": loss.detach(), **m}
 
     def _apply(self):
+        if self.fused is not None:
+            _fused_update(self.fused, self.cfg)   # clip + Adam in two launches on the flat buffers
+            return
         torch.nn.utils.clip_grad_norm_(self.params, self.cfg.max_grad_norm)
         self.opt.step()
 

@@ -221,3 +221,32 @@ def test_policy_sample_kernel(gpu):
         eps = ((raw - d.loc) / d.scale).reshape(-1)
         assert abs(float(eps.mean())) < 0.01 and abs(float(eps.std()) - 1) < 0.01
     assert not torch.equal(outs[0][0], outs[1][0])
+
+
+def test_clip_adam_matches_torch(gpu):
+    """duck_clip_adam (flat clip_grad_norm_ + Adam, two launches) against torch's clip_grad_norm_ and
+    Adam over 5 steps of random gradients, with clipping active (large gradients) and inactive."""
+    from open_duck_playground_amd.native import check, lib
+    L = lib()
+    torch.manual_seed(4)
+    P = 300_001
+    p0 = torch.randn(P, device=gpu)
+    for scale, max_norm in ((10.0, 1.0), (1e-4, 1.0)):
+        ref = torch.nn.Parameter(p0.clone())
+        opt = torch.optim.Adam([ref], lr=3e-4)
+        p = p0.clone()
+        m, v = torch.zeros(P, device=gpu), torch.zeros(P, device=gpu)
+        step = torch.zeros(1, dtype=torch.int32, device=gpu)
+        scratch = torch.zeros(L.duck_clip_adam_scratch_size(P), device=gpu)
+        for _ in range(5):
+            g = scale * torch.randn(P, device=gpu)
+            ref.grad = g.clone()
+            torch.nn.utils.clip_grad_norm_([ref], max_norm)
+            opt.step()
+            check(L.duck_clip_adam(P, p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), scratch.data_ptr(),
+                                   step.data_ptr(), 3e-4, 0.9, 0.999, 1e-8, max_norm,
+                                   torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        assert int(step.item()) == 5
+        err = float((p - ref.detach()).abs().max())
+        assert err <= 1e-6, (scale, err)
