@@ -162,6 +162,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline sampling (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this job may use")
     ap.add_argument("--strong", action="store_true", help="4096 envs in total over the ranks (strong scaling)")
+    ap.add_argument("--step-mode", default="auto", choices=["auto", "throughput", "latency"],
+                    help="duck_set_step_mode: auto = the latency kernel at <= 4 envs per CU (strong scaling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -188,6 +190,7 @@ def main():
     shard = shard_from_env(n)
     env = Joystick(cfg["task"], num_envs=n, device=dev, use_imitation=cfg["imitation"], env_offset=shard.env_offset)
     env = wrap_for_brax_training(env, episode_length=1000, randomization_fn=domain_randomize if cfg["dr"] else None)
+    env.set_step_mode(args.step_mode)
     state = env.reset(rng=0)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -274,10 +277,11 @@ def main():
                                    f"{', domain randomization' if cfg['dr'] else ''}, {n} envs per GPU, "
                                    "episode_length 1000 + auto-reset",
                        "envs_per_gpu": n, "total_envs": world * n, "substeps": env.n_substeps,
-                       "parallelism": f"env-shard x{world}"},
+                       "parallelism": f"env-shard x{world}", "step_kernel": env.step_kernel},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "step_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": B},
+                         "kernel": "step_kernel" if env.step_kernel == "throughput" else "step_kernel_lat",
+                         "kernel_ms": kern_ms, "bytes_per_env_step": B},
             "issue_roofline": issue_rf,
             "cpu_baseline": cpu,
             "finite": ok,

@@ -73,6 +73,18 @@ void duck_destroy(duck_sim* sim);
 int duck_reset(duck_sim* sim, int n_envs, float* fstate, int32_t* istate, const uint8_t* mask, uint64_t seed,
                int64_t env_offset, const float* dr, float* obs, float* priv, void* stream);
 
+/* Step kernel selection for duck_step (the same results bit for bit, a different work split):
+ * THROUGHPUT runs 16 envs per workgroup, each env's substeps on one 16-lane team (the batch
+ * rate at >= 4 envs per SIMD); LATENCY runs 4 envs per workgroup with each substep's stages
+ * split over its waves (a shorter env-step for small batches: strong scaling over GPUs);
+ * AUTO (the default) picks LATENCY while n_envs <= 4 x the device's CU count. */
+enum { DUCK_STEP_AUTO = 0, DUCK_STEP_THROUGHPUT = 1, DUCK_STEP_LATENCY = 2 };
+int duck_set_step_mode(duck_sim* sim, int mode);
+/* the kernel duck_step would launch for n_envs envs: DUCK_STEP_THROUGHPUT or DUCK_STEP_LATENCY */
+int duck_step_kernel_for(const duck_sim* sim, int n_envs);
+/* debug: latency-mode event waits that gave up (a broken cross-wave schedule; must stay 0) */
+int duck_debug_lat_timeouts(const duck_sim* sim, unsigned* out, int reset);
+
 /* Joystick.step (+ wrappers if cfg->auto_reset). `dr` (nullable) = per-env randomised
  * model values (duck_dr_layout, SoA [k][n_envs]) written by duck_randomize. `reward`,
  * `done` are [n_envs]. `scratch` (nullable unless feet can collide) = n_envs*nv*nv floats

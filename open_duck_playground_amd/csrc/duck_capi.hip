@@ -129,7 +129,8 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
   if (cfg->use_imitation && !ref) return duck_fail(DUCK_EINVAL, "use_imitation requires a reference-motion table");
   if (cfg->n_substeps < 1 || cfg->action_max_delay < 1 || cfg->action_max_delay > 3)
     return duck_fail(DUCK_EINVAL, "bad config (n_substeps >= 1, 1 <= action_max_delay <= 3)");
-  if (kVariants[v]->lds_bytes() > 160 * 1024) return duck_fail(DUCK_EUNSUPPORTED, "per-workgroup LDS over 160 KiB");
+  if (kVariants[v]->lds_bytes() > 160 * 1024 || kVariants[v]->lds_bytes_lat() > 160 * 1024)
+    return duck_fail(DUCK_EUNSUPPORTED, "per-workgroup LDS over 160 KiB");
   // the elevation is uploaded here, not baked (the fingerprint covers nrow / ncol / size only)
   if (kVariants[v]->floor_type == 1 && (!model->hfield_data || model->hfield_nrow < 2 || model->hfield_ncol < 2))
     return duck_fail(DUCK_EINVAL, "height-field model without hfield_data [nrow >= 2][ncol >= 2]");
@@ -138,6 +139,14 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
   memset(s, 0, sizeof(*s));
   s->device = device;
   s->variant = v;
+  s->step_mode = DUCK_STEP_AUTO;
+  {
+    hipError_t e = hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) {
+      delete s;
+      return duck_fail(DUCK_EHIP, std::string("hipDeviceGetAttribute: ") + hipGetErrorString(e));
+    }
+  }
   s->cfg = *cfg;
   s->nq = model->nq; s->nv = model->nv; s->nu = model->nu;
   s->lay = duck_layout_make(model->nq, model->nv, model->nu, cfg->use_imitation, cfg->task);
@@ -215,6 +224,25 @@ int duck_physics_step(duck_sim* s, int n, float* qpos, float* qvel, float* warm,
   if (n == 0) return DUCK_OK;
   HIPCHECK(hipSetDevice(s->device));
   return kVariants[s->variant]->physics(s, n, qpos, qvel, warm, ctrl, dr, nsub, aux, scratch, (hipStream_t)stream);
+}
+
+int duck_set_step_mode(duck_sim* s, int mode) {
+  g_err.clear();
+  if (!s || mode < DUCK_STEP_AUTO || mode > DUCK_STEP_LATENCY) return duck_fail(DUCK_EINVAL, "bad argument");
+  s->step_mode = mode;
+  return DUCK_OK;
+}
+
+int duck_step_kernel_for(const duck_sim* s, int n) {
+  if (!s || n < 0) return duck_fail(DUCK_EINVAL, "bad argument");
+  const bool lat = s->step_mode == DUCK_STEP_LATENCY || (s->step_mode == DUCK_STEP_AUTO && n <= LAT_WG_HOST * s->n_cu);
+  return lat ? DUCK_STEP_LATENCY : DUCK_STEP_THROUGHPUT;
+}
+
+int duck_debug_lat_timeouts(const duck_sim* s, unsigned* out, int reset) {
+  if (!s || !out) return duck_fail(DUCK_EINVAL, "bad argument");
+  HIPCHECK(hipSetDevice(s->device));
+  return kVariants[s->variant]->lat_timeouts(out, reset);
 }
 
 // debug: per-stage cycle counters of a -DDUCK_STAGE_PROF build (DUCK_EUNSUPPORTED otherwise)

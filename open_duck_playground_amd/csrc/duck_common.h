@@ -25,6 +25,9 @@ struct RefMeta {
   float dx_range[2], dy_range[2], dtheta_range[2];
 };
 
+// envs per latency-mode workgroup (duck_team.h LAT_WG; the host side of DUCK_STEP_AUTO)
+constexpr int LAT_WG_HOST = 4;
+
 // per-handle state (device pointers owned by the handle)
 struct duck_sim {
   int device;
@@ -36,6 +39,8 @@ struct duck_sim {
   float* frames_d;
   float* hfield_d;
   int nq, nv, nu;
+  int step_mode;  // DUCK_STEP_*
+  int n_cu;       // compute units of the device (DUCK_STEP_AUTO)
 };
 
 // per-variant entry points, one table per compiled model variant (variant_*.hip)
@@ -53,4 +58,6 @@ struct VariantOps {
   int (*physics)(duck_sim*, int n, float* qpos, float* qvel, float* warm, const float* ctrl, const float* dr,
                  int nsub, float* aux, float* scratch, hipStream_t st);
   int (*stage_cycles)(unsigned long long* out, int reset);
+  int (*lat_timeouts)(unsigned* out, int reset);
+  size_t (*lds_bytes_lat)();
 };

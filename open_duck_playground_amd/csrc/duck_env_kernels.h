@@ -59,9 +59,9 @@ DK int local_env(int& lane) {
   return threadIdx.x / TEAM;
 }
 
-template <class Md>
+template <class Md, bool LAT = false>
 DK Slice<SW> env_slice(float* lds, int t) {
-  return Slice<SW>{(lds_float*)(lds + t * TLay<Md>::STRIDE)};
+  return Slice<SW>{(lds_float*)(lds + t * TLay<Md, LAT>::STRIDE)};
 }
 
 template <class Md>
@@ -164,10 +164,10 @@ DK void load_dyn(const KArgs& A, int e, Slice<WG> L) {
 }
 
 // load_dyn with the team's lanes: nominal block from the LDS model blob, then the env's DR record
-template <class Md>
+template <class Md, bool LAT = false>
 DK void load_dyn_team(const KArgs& A, int e, Slice<SW> L, int lane) {
   using Ly = Lay<Md>;
-  using TP = TPhys<Md>;
+  using TP = TPhys<Md, LAT>;
   constexpr int NDYN = Md::NB + 3 + 2 * Md::NV + Md::NQ + Md::NU;
   static_assert(Ly::DKP + Md::NU - Ly::DMASS == NDYN, "contiguous per-env model block");
   for (int k = lane; k < NDYN; k += TEAM) L[Ly::DMASS + k] = TP::tf(Md::B_NOM + k);
@@ -473,7 +473,7 @@ DK StepPre step_prefetch(const KArgs& A, int e, int lane) {
 
 // Joystick.step body for env e (joystick.py:323-481 + wrappers); F = the env's hot state
 // (LDS-staged or the global row), G = the global row (auto-reset snapshot)
-template <class Md, class FA, bool STAGE_OBS, class RT>
+template <class Md, class FA, bool STAGE_OBS, class RT, bool LAT = false>
 DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, const Col<0>& G, const RT& r,
                  const StepPre& P) {
   using Ly = Lay<Md>;
@@ -535,7 +535,7 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
       L[Ly::QVEL + i] = F[Lo.qvel + i] + (i == 0 ? push[0] * mag : (i == 1 ? push[1] * mag : 0.0f));
       L[Ly::WARM + i] = F[Lo.qacc_warmstart + i];
     }
-    load_dyn_team<Md>(A, e, L, lane);
+    load_dyn_team<Md, LAT>(A, e, L, lane);
     TSYNC();
   } else {
     for (int i = 0; i < NQ; i++) L[Ly::QPOS + i] = F[Lo.qpos + i];
@@ -547,8 +547,17 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   // physics (joystick.py:420)
   float* scr = A.scratch ? A.scratch + e : nullptr;
   STAGE_MARK(29);
-  for (int s = 0; s < c.n_substeps; s++)
-    phys_step<Md>(L, lane, true, s == c.n_substeps - 1, nullptr, 0, scr, n, A.hfield);
+  if constexpr (LAT) {
+    // wave 0's share of each substep; waves 1 and 2 run theirs in step_kernel_lat. The env code
+    // below reads the last substep's state and sensors: wait for wave 1's Euler
+    using TPL = TPhys<Md, true>;
+    (void)scr;
+    for (int s = 0; s < c.n_substeps; s++) TPL::lat_r0(L.p, lane, s);
+    TPL::ev_wait(TPL::EV_EULER, c.n_substeps);
+  } else {
+    for (int s = 0; s < c.n_substeps; s++)
+      phys_step<Md>(L, lane, true, s == c.n_substeps - 1, nullptr, 0, scr, n, A.hfield);
+  }
   STAGE_RESET();
   for (int a = STAGE_OBS ? lane : 0; a < NU; a += STAGE_OBS ? TEAM : 1) {
     F[Lo.motor_targets + a] = L[Ly::CTRL + a];
@@ -865,6 +874,83 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
 #endif
 }
 
+// Latency mode (duck_set_step_mode / DUCK_STEP_LATENCY, or AUTO at <= 4 envs per CU): 4 envs per
+// workgroup and the stages of each substep split over its waves (TPhys::lat_r0 / lat_r1 / lat_r2,
+// duck_team.h): wave 0 runs the env code and kinematics / com_pos / rne / actuation, wave 1 crb, the
+// factorizations, the Newton solve, sensors and Euler, wave 2 collision and the constraint rows;
+// wave 3 only helps stage the hot state. Same stage code and arithmetic as step_kernel, so the
+// results are the same bit for bit (test_gpu_env.py::test_latency_mode_matches_throughput_mode);
+// one env-step of a small batch takes the critical path through the waves instead of the sum.
+template <class Md>
+__global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
+  using TL = TLay<Md, true>;
+  using TPL = TPhys<Md, true>;
+  constexpr int WGL = LAT_WG;
+  static_assert(TL::TAB_LDS && TL::ES_LDS, "latency mode: the model blob and the hot state in LDS");
+  static_assert(TPB == 4 * 64 && WGL * TEAM == 64, "latency mode: 4 waves, one set of 4 teams per wave");
+  extern __shared__ float lds[];
+  TPL::ev_init((int)threadIdx.x);
+  load_model_tables<Md, true>(lds);  // (ends with a workgroup barrier: the event counters are 0 before any wait)
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int t = ((int)threadIdx.x & 63) / TEAM, lane = (int)threadIdx.x % TEAM;
+  const int e = blockIdx.x * WGL + t;
+  const int n = A.n;
+  const int j = threadIdx.x % WGL, ej = blockIdx.x * WGL + j;
+  lds_float* esj = (lds_float*)(lds + TL::ES + j * TL::ESTRIDE);
+  const StepPre P = step_prefetch<Md>(A, e, lane);
+  constexpr int NK = (TL::HOT + TPB / WGL - 1) / (TPB / WGL);
+  {
+    const int ejc = ej < n ? ej : 0;
+    float hv[NK];
+#pragma unroll
+    for (int kk = 0; kk < NK; kk++) {
+      const int k = (int)threadIdx.x / WGL + (TPB / WGL) * kk;
+      hv[kk] = A.fs[(size_t)(k < TL::HOT ? k : TL::HOT - 1) * n + ejc];
+    }
+#pragma unroll
+    for (int kk = 0; kk < NK; kk++) {
+      const int k = (int)threadIdx.x / WGL + (TPB / WGL) * kk;
+      if (ej < n && k < TL::HOT) esj[k] = hv[kk];
+    }
+  }
+  __syncthreads();
+  if (e < n) {
+    const Slice<SW> L = env_slice<Md, true>(lds, t);
+    const int ns = A.cfg.n_substeps;
+    if (wave == 0) {
+      const Col<0> G{A.fs + e, n};
+      lds_float* esp = (lds_float*)(lds + TL::ES + t * TL::ESTRIDE);
+      RngTab rt;
+      rt.k0 = P.k0;
+      rt.k1 = P.k1;
+      rt.ctr = P.ctr;
+      rt.tab = esp + TL::HOT;
+      rt.fill(esp + TL::HOT, lane);
+      TSYNC();
+      step_env<Md, LCol, true, RngTab, true>(A, e, lane, L, LCol{esp}, G, rt, P);
+    } else if (wave == 1) {
+      float* scr = A.scratch ? A.scratch + e : nullptr;
+      for (int s = 0; s < ns; s++) TPL::lat_r1(L.p, lane, s, true, s == ns - 1, scr, n);
+    } else if (wave == 2) {
+      for (int s = 0; s < ns; s++) TPL::lat_r2(L.p, lane, s, A.hfield);
+    }
+  }
+  __syncthreads();
+  {
+    float hv[NK];
+#pragma unroll
+    for (int kk = 0; kk < NK; kk++) {
+      const int k = (int)threadIdx.x / WGL + (TPB / WGL) * kk;
+      hv[kk] = esj[k < TL::HOT ? k : TL::HOT - 1];
+    }
+#pragma unroll
+    for (int kk = 0; kk < NK; kk++) {
+      const int k = (int)threadIdx.x / WGL + (TPB / WGL) * kk;
+      if (ej < n && k < TL::HOT) A.fs[(size_t)k * n + ej] = hv[kk];
+    }
+  }
+}
+
 template <class Md, int WG>
 __global__ void __launch_bounds__(TPB) physics_kernel(KArgs A, float* qpos_g, float* qvel_g, float* warm_g,
                                                      const float* ctrl_g, int nsub, float* aux) {
@@ -938,6 +1024,10 @@ static size_t lds_bytes() {
   static_assert(WG == TEAM_WG, "team workgroup size");
   return (size_t)TLay<Md>::LDS_FLOATS * sizeof(float);
 }
+template <class Md>
+static size_t lds_bytes_lat() {
+  return (size_t)TLay<Md, true>::LDS_FLOATS * sizeof(float);
+}
 
 template <class Md>
 static int aux_size_of() {
@@ -976,6 +1066,16 @@ static int launch_step(duck_sim* s, int n, float* fs, int32_t* is, const float* 
   A.fs = fs; A.is = is; A.dr = dr; A.action = action; A.obs = obs; A.priv = priv;
   A.reward = reward; A.done = done; A.scratch = scratch;
   if (s->lay.first_qpos != TLay<Md>::HOT) return duck_fail(DUCK_EINVAL, "state layout does not match the kernel's hot-state size");
+  // latency mode while the batch leaves at least a CU per 4 envs (each latency workgroup takes a
+  // whole CU: one wave of 512 registers per SIMD), or when asked for
+  static_assert(LAT_WG == LAT_WG_HOST, "latency workgroup size");
+  const bool lat = s->step_mode == DUCK_STEP_LATENCY || (s->step_mode == DUCK_STEP_AUTO && n <= LAT_WG * s->n_cu);
+  if (lat) {
+    const dim3 grid((A.n + LAT_WG - 1) / LAT_WG), block(TPB);
+    hipLaunchKernelGGL((step_kernel_lat<Md>), grid, block, lds_bytes_lat<Md>(), st, A);
+    HIPCHECK(hipGetLastError());
+    return DUCK_OK;
+  }
   const dim3 grid((A.n + WG - 1) / WG), block(TPB);
   hipLaunchKernelGGL((step_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A);
   HIPCHECK(hipGetLastError());
@@ -1000,6 +1100,15 @@ static int launch_physics(duck_sim* s, int n, float* qpos, float* qvel, float* w
   hipLaunchKernelGGL((physics_kernel<Md, WG>), grid, block, lds_bytes<Md>(), st, A, qpos, qvel, warm, ctrl, nsub, aux);
   HIPCHECK(hipGetLastError());
   return DUCK_OK;
+}
+
+static int lat_timeouts_of(unsigned* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lat_timeouts), sizeof(unsigned));
+  if (e == hipSuccess && reset) {
+    const unsigned z = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_lat_timeouts), &z, sizeof(unsigned));
+  }
+  return e == hipSuccess ? DUCK_OK : duck_fail(DUCK_EHIP, hipGetErrorString(e));
 }
 
 static int stage_cycles_of(unsigned long long* out, int reset) {
@@ -1028,6 +1137,6 @@ static int stage_cycles_of(unsigned long long* out, int reset) {
     static const VariantOps ops = {#NAME,               matches<MODEL>,         aux_size_of<MODEL>, \
                                    lds_bytes<MODEL>,    MODEL::FLOOR_TYPE,      launch_reset<MODEL>, \
                                    launch_step<MODEL>,  launch_randomize<MODEL>, launch_physics<MODEL>, \
-                                   stage_cycles_of};                                            \
+                                   stage_cycles_of,     lat_timeouts_of,        lds_bytes_lat<MODEL>}; \
     return &ops;                                                                                \
   }

@@ -152,19 +152,42 @@ constexpr float HF_POINT_BAND = 1e-4f;
 #define DUCK_LS_DFLOOR 1e-6f
 #endif
 
-template <class Md>
+// Latency mode (LAT, step_kernel_lat): the stages of one substep are split over the four waves of a
+// workgroup that all work the same 4 envs (wave 0: kinematics, com_pos, rne, actuation and the env
+// code; wave 1: composite inertias, crb, M's factorization, the smooth solve, the Newton solve,
+// sensors, Euler; wave 2: collision and the constraint rows). Waves that run concurrently must not
+// share scratch, so a latency slice gives rne's scratch, the composite inertias and the height
+// field's silhouette lists regions of their own after the throughput slice's words.
+constexpr int LAT_WG = 4;  // envs (teams) per latency-mode workgroup: 4 waves x 4 teams, one team set per wave
+// latency-mode event waits that gave up (TPhys::ev_wait; read by duck_debug_lat_timeouts, must stay 0)
+static __device__ unsigned int g_lat_timeouts;
+
+template <class Md, bool LAT = false>
 struct TLay {
   using Ly = Lay<Md>;
   // per-lane dump slots (SINK, 2 x TEAM words; debug line-search dumps use 136 words from here)
   static constexpr int KC = Ly::TOTAL;
 #ifdef DUCK_LS_DUMP
-  static constexpr int USED = KC + 136;
+  static constexpr int USED0 = KC + 136;
 #else
-  static constexpr int USED = KC + 2 * TEAM;
+  static constexpr int USED0 = KC + 2 * TEAM;
 #endif
+  // the height field's per-foot silhouette lists (collide_hfield -> hf_exec)
+  static constexpr int HF_SLF = (1 + Md::HF_SILCAP + 3) & ~3;
+  static constexpr int HF_SLSZ = HF_SLF + 4 * Md::HF_SILCAP;
+  // rne's scratch: body accelerations (6 NB), subtree forces (6 NB), body forces (6 NB)
+  static constexpr int XRNE = LAT ? ((USED0 + 3) & ~3) : Ly::H;
+  static constexpr int RCA = XRNE, CFRC = XRNE + 6 * Md::NB, RFB = XRNE + 12 * Md::NB;
+  // composite inertias (summed by rne's subtree pass, read by crb); throughput mode overwrites the
+  // body inertias in CIN (phase B of rne has read them)
+  static constexpr int XCIN = LAT ? XRNE + 18 * Md::NB : Ly::CIN;
+  // the subtree pass's lanes that a latency-mode wave does not own write here (forces / inertias)
+  static constexpr int XDUM0 = LAT ? XCIN + 10 * Md::NB : 0, XDUM1 = LAT ? XDUM0 + 10 * Md::NB : 0;
+  static constexpr int XSIL = LAT ? ((XDUM1 + 6 * Md::NB + 3) & ~3) : ((Ly::CIN + 3) & ~3);
+  static constexpr int USED = LAT ? XSIL + (Md::FLOOR_TYPE == 1 ? 2 * HF_SLSZ : 0) : USED0;
   static constexpr int STRIDE = ((USED + 15) / 32) * 32 + 16;  // = 16 (mod 32), >= USED
+  static constexpr int NWG = LAT ? LAT_WG : TEAM_WG;          // envs per workgroup
   static_assert(STRIDE >= USED && STRIDE % 32 == 16, "stride");
-  static constexpr int FTMP = Ly::JA;                  // crb: F_i = I_b cdof_i (dead row storage)
   // per-lane dump slots for branchless conditional stores (L[ok ? addr : SINK + lane] = v): a
   // lane-divergent `if` leaves a join block whose exec restore the register allocator may put
   // live-range split copies in front of (tools/isa_exec_check.py), so the hot
@@ -174,18 +197,19 @@ struct TLay {
   // constraint stage (kinematics / rne / crb run before it)
   static constexpr int TMP = Ly::H;
   static constexpr int KLOC = TMP;                               // local body transforms (7 per body)
-  static constexpr int RCS = TMP, RCF = TMP + 6 * Md::NB, RCDD = TMP + 12 * Md::NB;  // rne
-  static constexpr int CRB = TMP, FT = TMP + 10 * Md::NB;        // crb
-  static_assert(12 * Md::NB + 6 * Md::NV <= Ly::HSZ + 4 * Ly::NROW, "tree scratch must fit in H + rows");
+  static_assert(7 * Md::NB <= Ly::HSZ + 4 * Ly::NROW, "tree scratch must fit in H + rows");
   // the model blob (lane-indexed tables, constraint-row records) follows the env slices in
   // LDS when it fits, else it is read from global memory
-  static constexpr int TAB = STRIDE * TEAM_WG;
+  static constexpr int TAB = STRIDE * NWG;
   // step_kernel stages each env's hot state (the duck_layout fields before first_qpos) in LDS:
   // one batch of independent global loads in, one batch of stores out
   static constexpr int HOT = Md::NQ + 2 * Md::NV + 8 * Md::NU + 77;
   static constexpr int ESTRIDE = (HOT + 64) | 1;  // + the step's 64 random draws; odd: distinct banks
-  static constexpr int ES_FLOATS = ESTRIDE * TEAM_WG;
-  static constexpr size_t LDS_MAX = 160 * 1024 / 4;
+  static constexpr int ES_FLOATS = ESTRIDE * NWG;
+  // latency mode: the cross-wave event counters, one 16-B word group each, in front of the slices'
+  // end of LDS (LDS_FLOATS counts them)
+  static constexpr int NEV = LAT ? 8 : 0;
+  static constexpr size_t LDS_MAX = 160 * 1024 / 4 - 4 * NEV;
   // LDS priority: model blob (read every substep), then the hot state (read once per env-step)
   static constexpr bool TAB_LDS = (size_t)(TAB + Md::NBLOB) <= LDS_MAX;
   // the height field's hull SAT tables (hull faces + edges, contiguous in the blob) in LDS on their
@@ -194,18 +218,23 @@ struct TLay {
   static constexpr bool HT_LDS = !TAB_LDS && NHT > 0 && (size_t)(TAB + NHT) <= LDS_MAX;
   static constexpr int ES = TAB + (TAB_LDS ? Md::NBLOB : (HT_LDS ? NHT : 0));
   static constexpr bool ES_LDS = (size_t)(ES + ES_FLOATS) <= LDS_MAX;
-  static constexpr int LDS_FLOATS = ES + (ES_LDS ? ES_FLOATS : 0);
+  static constexpr int EV = ES + (ES_LDS ? ES_FLOATS : 0);
+  static constexpr int LDS_FLOATS = EV + 4 * NEV;
   static_assert((size_t)LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
   static_assert(6 * Md::NV <= 4 * Ly::NROW, "crb scratch must fit in the row storage");
+  static_assert(LAT || 18 * Md::NB <= Ly::HSZ + 4 * Ly::NROW, "rne scratch must fit in H + rows");
+  static_assert(LAT || Md::FLOOR_TYPE != 1 || XSIL + 2 * HF_SLSZ <= Ly::CIN + 10 * Md::NB,
+                "the silhouette lists must fit in the composite inertias' storage");
 };
 
 // copy the model blob into the workgroup's LDS (before any thread of the block exits)
-template <class Md>
+template <class Md, bool LAT = false>
 DK void load_model_tables(float* lds) {
-  if constexpr (TLay<Md>::TAB_LDS) {
+  using TLy = TLay<Md, LAT>;
+  if constexpr (TLy::TAB_LDS) {
     // a compile-time trip count: every load of the thread is issued before the first store waits
     // (a runtime-bounded loop waits for each group of loads: one memory round trip per group)
-    int* dst = (int*)(lds + TLay<Md>::TAB);
+    int* dst = (int*)(lds + TLy::TAB);
     constexpr int NK = (Md::NBLOB + TPB_TEAM - 1) / TPB_TEAM;
     int w[NK];
 #pragma unroll
@@ -219,9 +248,9 @@ DK void load_model_tables(float* lds) {
       if (i < Md::NBLOB) dst[i] = w[kk];
     }
     __syncthreads();
-  } else if constexpr (TLay<Md>::HT_LDS) {
-    int* dst = (int*)(lds + TLay<Md>::TAB);
-    constexpr int N = TLay<Md>::NHT, NK = (N + TPB_TEAM - 1) / TPB_TEAM;
+  } else if constexpr (TLy::HT_LDS) {
+    int* dst = (int*)(lds + TLy::TAB);
+    constexpr int N = TLy::NHT, NK = (N + TPB_TEAM - 1) / TPB_TEAM;
     int w[NK];
 #pragma unroll
     for (int kk = 0; kk < NK; kk++) {
@@ -261,10 +290,10 @@ struct HullFaceOrder {
   }
 };
 
-template <class Md>
+template <class Md, bool LAT = false>
 struct TPhys {
   using Ly = Lay<Md>;
-  using TL = TLay<Md>;
+  using TL = TLay<Md, LAT>;
   using P1 = Phys<Md, 1>;
   using S1 = Slice<1>;
   typedef lds_float* LP;
@@ -534,7 +563,7 @@ struct TPhys {
   // limb's cdof/qvel loaded into registers before the chain; (B) body forces
   // cinert cacc + cvel x* (cinert cvel), a body per lane; (C) subtree sums of the forces — limb
   // suffix sums per lane, a team sum at the trunk, the root path on every lane.
-  static constexpr int RCA = TL::RCS, RFB = TL::RCDD;  // body accelerations / body forces (scratch)
+  static constexpr int RCA = TL::RCA, RFB = TL::RFB;  // body accelerations / body forces (scratch)
 
   // cvel/cacc of the free-joint root body (every lane); its cdof_dot rows go to CDD1 (sensors)
   static DK void root_motion(LP L, int lane, int b, float* cv, float* ca) {
@@ -564,12 +593,19 @@ struct TPhys {
     }
   }
 
+  // PART 0: the whole pass (throughput mode). Latency mode: wave 0 runs rne_vel, then rne_rest<1>
+  // (the composite-inertia lanes of phase C write a dump region), wave 1 runs subtree_sums<2> (the
+  // composite inertias only: they need com_pos, not the velocities), so crb starts before rne ends
   static DK void rne(LP L, int lane) {
+    rne_vel(L, lane);
+    rne_rest<0>(L, lane);
+  }
+  // (A) velocities and accelerations
+  static DK void rne_vel(LP L, int lane) {
 #pragma clang fp reassociate(on)
     STAGE_T0();
     constexpr int NR = Md::T_NROOT, BL = Md::T_BRLEN, MD = Md::T_BRMD;  // dofs per limb body (2: backlash)
     static_assert(Md::T_NBR <= TEAM, "a limb per lane");
-    // (A) velocities and accelerations
     float cv[6], ca[6];
     for (int k = 0; k < 6; k++) { cv[k] = 0.0f; ca[k] = (k >= 3) ? -Md::gravity[k - 3] : 0.0f; }
 #pragma unroll
@@ -614,6 +650,11 @@ struct TPhys {
     }
     TSYNC();
     STAGE_MARK(21);
+  }
+  template <int PART>
+  static DK void rne_rest(LP L, int lane) {
+#pragma clang fp reassociate(on)
+    STAGE_T0();
     // (B) body forces, a body per lane
     for (int b = 1 + lane; b < NB; b += TEAM) {
       if (!moving(b)) continue;
@@ -632,13 +673,31 @@ struct TPhys {
     // lane k < 6 sums force component k, lane 6 + j inertia component j, down every limb from its
     // tip (the limb bodies are compile-time, Md::T_BRB), then the limb totals, then the root path.
     // Each component's additions run in the same order as a limb-per-lane pass.
+    subtree_sums<PART>(L, lane);
+    for (int i = lane; i < NV; i += TEAM) {
+      const int b = dof_body(i);
+      float s = 0.0f;
+      for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * i + k] * L[TL::CFRC + 6 * b + k];
+      L[Ly::FSM + i] = -s;
+    }
+    TSYNC();
+  }
+  // phase C of rne: PART 0 both sums, PART 1 the forces (inertia lanes into XDUM0), PART 2 the
+  // composite inertias (force lanes read CIN and write XDUM1: no read of rne's forces in flight)
+  template <int PART>
+  static DK void subtree_sums(LP L, int lane) {
+#pragma clang fp reassociate(on)
+    STAGE_T0();
+    constexpr int NR = Md::T_NROOT, BL = Md::T_BRLEN;
     static_assert(TEAM == 6 + 10, "a force or inertia component per lane");
     {
       int lk = lane;
       asm volatile("" : "+v"(lk));  // else the per-lane address selects are hoisted out of the substep
                                     // loop into registers (+19 AGPRs, -6 % measured)
       const bool fk = lk < 6;
-      const int src = fk ? RFB + lk : Ly::CIN + (lk - 6), dst = fk ? Ly::CFRC + lk : Ly::CIN + (lk - 6);
+      const int fsrc = PART == 2 ? Ly::CIN + lk : RFB + lk, fdst = PART == 2 ? TL::XDUM1 + lk : TL::CFRC + lk;
+      const int idst = PART == 1 ? TL::XDUM0 + (lk - 6) : TL::XCIN + (lk - 6);
+      const int src = fk ? fsrc : Ly::CIN + (lk - 6), dst = fk ? fdst : idst;
       const int st = fk ? 6 : 10;
       float tot = 0.0f;
 #pragma unroll
@@ -663,13 +722,6 @@ struct TPhys {
     }
     TSYNC();
     STAGE_MARK(36);
-    for (int i = lane; i < NV; i += TEAM) {
-      const int b = dof_body(i);
-      float s = 0.0f;
-      for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * i + k] * L[Ly::CFRC + 6 * b + k];
-      L[Ly::FSM + i] = -s;
-    }
-    TSYNC();
   }
 
   // ---------------- mj_crb: the sparse M from the composite inertias (summed in rne) ----
@@ -697,7 +749,7 @@ struct TPhys {
       float cd[6], F[6], I[10];
       for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * ic + k];
       const int bi = dof_body(ic);
-      for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * bi + k];
+      for (int k = 0; k < 10; k++) I[k] = L[TL::XCIN + 10 * bi + k];
       int jj[MC];
       float cj[MC][6];
       // with B_DCHAFF the chain is the B_DCHN free-joint dofs, then the run of limb dofs from the
@@ -742,7 +794,7 @@ struct TPhys {
       float cd[6], F[6], I[10];
       for (int k = 0; k < 6; k++) cd[k] = L[Ly::CDOF + 6 * ic + k];
       const int bi = dof_body(ic);
-      for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * bi + k];
+      for (int k = 0; k < 10; k++) I[k] = L[TL::XCIN + 10 * bi + k];
       const float arm = L[Ly::DARM + ic];
       const int rs = ti(Md::B_MROW + ic);
       mul_inert_vec(F, I, cd);
@@ -889,6 +941,10 @@ struct TPhys {
   // the diagonal may hold anything) in place and
   // solve for x (lane l holds x[l], x[l+16])
   static DK void factor_solve(Fac& F, float* x, int lane) {
+    factor(F, lane);
+    solve_factored(F, x, lane);
+  }
+  static DK void factor(Fac& F, int lane) {
 #pragma unroll
     for (int s = 0; s < NC; s++) F.dg[s] = 1.0f;
     fac_all(F, lane, std::make_integer_sequence<int, NV>{});
@@ -898,6 +954,8 @@ struct TPhys {
     for (int s = 0; s < NC; s++)
 #pragma unroll
       for (int r = TEAM * s + 1; r < NV; r++) F.col[s][r] = lane < r - TEAM * s ? F.col[s][r] : 0.0f;
+  }
+  static DK void solve_factored(const Fac& F, float* x, int lane) {
     back_all(F, x, std::make_integer_sequence<int, NV>{});
 #pragma unroll
     for (int s = 0; s < NC; s++) x[s] = x[s] * __builtin_amdgcn_rcpf(F.dg[s]);
@@ -1020,6 +1078,30 @@ struct TPhys {
       x[s] = c < NV ? v : 0.0f;
     }
     factor_solve(F, x, lane);
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane;
+      if (c < NV) L[Ly::QSM + c] = x[s];
+    }
+    TSYNC();
+  }
+  // (latency mode: the factorization runs before qfrc_smooth is known, the solve after)
+  static DK void smooth_factor(Fac& F, int lane, const float (*Mc)[NV]) {
+#pragma unroll
+    for (int s = 0; s < NC; s++)
+#pragma unroll
+      for (int r = 0; r < NV; r++) F.col[s][r] = Mc[s][r];
+    factor(F, lane);
+  }
+  static DK void smooth_solve(LP L, int lane, const Fac& F) {
+    float x[NC];
+#pragma unroll
+    for (int s = 0; s < NC; s++) {
+      const int c = TEAM * s + lane;
+      const float v = L[Ly::FSM + (c < NV ? c : 0)];
+      x[s] = c < NV ? v : 0.0f;
+    }
+    solve_factored(F, x, lane);
 #pragma unroll
     for (int s = 0; s < NC; s++) {
       const int c = TEAM * s + lane;
@@ -1433,10 +1515,8 @@ struct TPhys {
   static constexpr int HF_PRIO_T = 5 + Md::NHF, HF_PRIO_V = HF_PRIO_T + 3 * Md::NHE;
   static constexpr int HF_ENT = 28, HF_QH0 = (Ly::H + 3) & ~3;
   static constexpr int HF_QE = (Ly::CR - HF_QH0) / HF_ENT, HF_QR = 4 * HF_QE < 64 ? 4 * HF_QE : 64;
-  static constexpr int HF_CINQ = (Ly::CIN + 3) & ~3, HF_SLF = (1 + Md::HF_SILCAP + 3) & ~3;
-  static constexpr int HF_SLSZ = HF_SLF + 4 * Md::HF_SILCAP;
-  static_assert(Md::FLOOR_TYPE != 1 || (HF_QE >= 16 && HF_CINQ + 2 * HF_SLSZ <= Ly::CIN + 10 * Md::NB),
-                "height-field SAT queue / silhouette lists must fit their LDS storage");
+  static constexpr int HF_CINQ = TL::XSIL, HF_SLF = TL::HF_SLF, HF_SLSZ = TL::HF_SLSZ;
+  static_assert(Md::FLOOR_TYPE != 1 || HF_QE >= 16, "height-field SAT queue must fit its LDS storage");
 
   // One prism's separating-axis test against the hull for the lane that runs queue entry E
   // (collide_hfield), in the hull's mesh frame with the hull's compile-time vertices, faces and
@@ -3043,5 +3123,81 @@ struct TPhys {
       TSYNC();
     }
     STAGE_MARK(8);
+  }
+
+  // ---------------- latency mode: one substep over three waves (step_kernel_lat) ----------------
+  // Cross-wave events are counters in LDS (one 16-B group each, after the slices): the producer
+  // wave stores the number of the substep it finished (a workgroup-scope release: its LDS writes
+  // complete first), a consumer spins on an acquire load until the count is reached. Counts only
+  // grow within a launch, so no event is reset between substeps. A spin is bounded (~40 ms, far
+  // beyond a substep) so that a broken schedule ends the launch instead of hanging the device;
+  // g_lat_timeouts counts such exits (tests read it: it must stay 0).
+  enum { EV_KIN = 0, EV_VEL = 1, EV_FSM = 2, EV_ROWS = 3, EV_EULER = 4 };
+  static DK lds_int* ev_ptr(int k) {
+    extern __shared__ float lds_dyn[];
+    return (lds_int*)(lds_dyn + TL::EV) + 4 * k;
+  }
+  static DK void ev_init(int tid) {
+    if (tid < TL::NEV) ev_ptr(tid)[0] = 0;
+  }
+  static DK void ev_signal(int k, int v) {
+    __hip_atomic_store(ev_ptr(k), v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  static DK void ev_wait(int k, int v) {
+    for (int it = 0; __hip_atomic_load(ev_ptr(k), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v; it++) {
+      if (it > (1 << 20)) {
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_lat_timeouts, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  // wave 0, substep s: kinematics and com_pos (everything else waits for them), rne's velocities
+  // (the contact rows need the feet's), then the rest of rne and the actuation (qfrc_smooth)
+  static DK void lat_r0(LP L, int lane, int s) {
+    ev_wait(EV_EULER, s);
+    kinematics(L, lane);
+    com_pos(L, lane);
+    ev_signal(EV_KIN, s + 1);
+    rne_vel(L, lane);
+    ev_signal(EV_VEL, s + 1);
+    rne_rest<1>(L, lane);
+    smooth(L, lane);
+    ev_signal(EV_FSM, s + 1);
+  }
+  // wave 1: composite inertias, M, its register columns and factorization while wave 0 finishes rne;
+  // the smooth solve once qfrc_smooth is there, the Newton solve once the rows are, sensors, Euler
+  static DK void lat_r1(LP L, int lane, int s, bool integrate, bool want_out, float* scratch, int sstride) {
+    ev_wait(EV_KIN, s + 1);
+    subtree_sums<2>(L, lane);
+    crb(L, lane);
+    {
+      float Mc[NC][NV];
+      load_cols(L, lane, Mc, false);
+      {
+        Fac F;
+        smooth_factor(F, lane, Mc);
+        ev_wait(EV_FSM, s + 1);
+        smooth_solve(L, lane, F);
+      }
+      ev_wait(EV_ROWS, s + 1);
+      solve(L, lane, scratch, sstride, Mc);
+    }
+    if (want_out) sensors(L, lane);
+    if (integrate) {
+      euler(L, lane);
+    } else {
+      for (int i = lane; i < NV; i += TEAM) L[Ly::WARM + i] = L[Ly::QACC + i];
+      TSYNC();
+    }
+    ev_signal(EV_EULER, s + 1);
+  }
+  // wave 2: collision (kinematics only), then the constraint rows (the feet's velocities)
+  static DK void lat_r2(LP L, int lane, int s, const float* hf) {
+    ev_wait(EV_KIN, s + 1);
+    collision(L, lane, hf);
+    ev_wait(EV_VEL, s + 1);
+    make_rows(L, lane);
+    ev_signal(EV_ROWS, s + 1);
   }
 };

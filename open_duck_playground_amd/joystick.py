@@ -41,6 +41,8 @@ from .refmotion import PolyReferenceMotion
 
 USE_IMITATION_REWARD = cfgmod.USE_IMITATION_REWARD
 USE_MOTOR_SPEED_LIMITS = cfgmod.USE_MOTOR_SPEED_LIMITS
+# duck_set_step_mode (include/duck.h DUCK_STEP_*)
+STEP_MODES = {"auto": 0, "throughput": 1, "latency": 2}
 
 
 @dataclass
@@ -170,6 +172,7 @@ class Joystick(OpenDuckMiniV2Env):
         self.auto_reset = False
         self.episode_length = int(self._config.episode_length)
         self.dr: Optional[torch.Tensor] = None
+        self._step_mode = "auto"
         self._post_init()
 
     def _post_init(self) -> None:
@@ -211,6 +214,35 @@ class Joystick(OpenDuckMiniV2Env):
                                     dev, C.byref(handle)), self._lib)
         self._sim = handle
         self._scratch = None
+        if hasattr(self._lib, "duck_set_step_mode"):  # (A/B baselines built before the latency kernel)
+            check(self._lib.duck_set_step_mode(self._sim, STEP_MODES[self._step_mode]), self._lib)
+
+    def set_step_mode(self, mode: str) -> None:
+        """duck_set_step_mode: "auto" (default), "throughput" or "latency". The same env-steps bit for
+        bit; "latency" splits each substep's stages over four waves per 4 envs (a shorter env-step
+        for small batches, e.g. a 4096-env job strong-scaled over 8 GPUs), "throughput" runs 16 envs
+        per workgroup on one team each; "auto" takes latency at <= 4 envs per CU."""
+        if mode not in STEP_MODES:
+            raise DuckError(f"step mode {mode!r} not in {sorted(STEP_MODES)}")
+        if not hasattr(self._lib, "duck_set_step_mode") and mode in ("auto", "throughput"):
+            return  # an A/B baseline library without the latency kernel
+        self._step_mode = mode
+        check(self._lib.duck_set_step_mode(self._sim, STEP_MODES[mode]), self._lib)
+
+    @property
+    def step_kernel(self) -> str:
+        """The kernel step() launches for this batch: "throughput" or "latency"."""
+        if not hasattr(self._lib, "duck_step_kernel_for"):
+            return "throughput"
+        k = self._lib.duck_step_kernel_for(self._sim, self.num_envs)
+        check(min(k, 0), self._lib)
+        return {1: "throughput", 2: "latency"}[k]
+
+    def lat_timeouts(self, reset: bool = False) -> int:
+        """Latency-mode event waits that gave up since the last reset (a broken schedule; must be 0)."""
+        out = C.c_uint(0)
+        check(self._lib.duck_debug_lat_timeouts(self._sim, C.byref(out), int(reset)), self._lib)
+        return int(out.value)
 
     def __del__(self):
         try:

@@ -23,7 +23,8 @@ EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get"
            "duck_debug_stage_cycles", "duck_model_fingerprint", "duck_model_supported",
            "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae", "duck_ppo_loss",
            "duck_ppo_loss_out_size", "duck_mlp_gemm", "duck_mlp_wgrad", "duck_mlp_wgrad_reduce",
-           "duck_policy_sample", "duck_clip_adam", "duck_clip_adam_scratch_size"]
+           "duck_policy_sample", "duck_clip_adam", "duck_clip_adam_scratch_size", "duck_set_step_mode",
+           "duck_step_kernel_for", "duck_debug_lat_timeouts"]
 
 
 class DuckError(RuntimeError):
@@ -238,6 +239,10 @@ def lib(path: str = None):
         L.duck_model_fingerprint.restype = C.c_uint64
         L.duck_model_fingerprint.argtypes = [C.POINTER(DuckModelDesc)]
         L.duck_model_supported.argtypes = [C.POINTER(DuckModelDesc)]
+        if hasattr(L, "duck_set_step_mode"):  # (libraries built before the latency kernel: A/B baselines)
+            L.duck_set_step_mode.argtypes = [vp, C.c_int]
+            L.duck_step_kernel_for.argtypes = [vp, C.c_int]
+            L.duck_debug_lat_timeouts.argtypes = [vp, C.POINTER(C.c_uint), C.c_int]
         if hasattr(L, "duck_gae"):
             L.duck_gae.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp]
         if hasattr(L, "duck_ppo_loss"):

@@ -98,9 +98,11 @@ def _fs_err(L, fa, fb, n):
 def run(task: str, imitation: bool, n: int, steps: int, device, seed: int = 7, dr: bool = False,
         auto_reset: bool = False, episode_length: int = 1000, overrides: Optional[dict] = None,
         force_push: bool = False, force_resample: bool = False, env_cls=Joystick, action_seed: int = 0,
-        keep_states: bool = False, oracle_edit: Optional[Callable[[Model], Model]] = None) -> Report:
+        keep_states: bool = False, oracle_edit: Optional[Callable[[Model], Model]] = None,
+        step_mode: str = "auto") -> Report:
     """``oracle_edit`` hands the oracle a deliberately wrong model (a copy of the GPU's, edited; the
-    GPU keeps the nominal one): the injected-defect test of ``explain`` (DEFECTS)."""
+    GPU keeps the nominal one): the injected-defect test of ``explain`` (DEFECTS). ``step_mode``:
+    Joystick.set_step_mode ("auto" runs the latency kernel at these batch sizes, <= 4 envs per CU)."""
     kw = {} if env_cls is not Joystick else {"use_imitation": imitation}
     env = env_cls(task, num_envs=n, device=device, config_overrides=overrides, **kw)
     if auto_reset:
@@ -108,6 +110,7 @@ def run(task: str, imitation: bool, n: int, steps: int, device, seed: int = 7, d
                                      randomization_fn=domain_randomize if dr else None, rng=seed + 1)
     elif dr:
         domain_randomize(env, rng=seed + 1)
+    env.set_step_mode(step_mode)
     st = env.reset(rng=seed)
     om_model = oracle_edit(copy_model(env.mj_model)) if oracle_edit is not None else env.mj_model
     base = OracleModel(om_model)
@@ -246,6 +249,12 @@ CASES = {
                                            "flat_terrain_edited.npz"), imitation=False, force_push=True,
                          force_resample=True),
     "standing": dict(task="flat_terrain", imitation=False, force_push=True, force_resample=True, standing=True),
+    # the throughput kernel (16 envs per workgroup) at the same size; the cases above run the latency
+    # kernel ("auto" at <= 4 envs per CU)
+    "flat_throughput_kernel": dict(task="flat_terrain", imitation=True, force_push=True, force_resample=True,
+                                   step_mode="throughput"),
+    "rough_backlash_dr_throughput_kernel": dict(task="rough_terrain_backlash", imitation=False, dr=True,
+                                                force_push=True, step_mode="throughput"),
 }
 
 

@@ -184,6 +184,61 @@ def test_full_size_runs_are_deterministic(cfg, gpu):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("cfg,n", [("C2", 512), ("C3", 1021), ("C4", 1024), ("C5", 510)])
+def test_latency_mode_matches_throughput_mode(cfg, n, gpu):
+    """The latency kernel (each substep's stages split over four waves per 4 envs, DUCK_STEP_LATENCY)
+    runs the same stage code on the same data as the throughput kernel (one team per env). Every
+    env-step is taken by both kernels from the same state (the throughput kernel's), over auto-resets
+    (5-step episodes), DR, and a batch with a partial workgroup (n % 4 != 0). Height-field scenes: bit
+    for bit. Flat scenes: the compiler contracts a few fp32 expressions of the inlined plane collision
+    differently in the two kernels, so they agree to fp32 rounding (measured on MI355X, 512 envs x 6
+    env-steps: qpos 1.3e-7, qvel 1.1e-5, obs 1.6e-4 relative at most); integers and dones exactly.
+    No cross-wave wait gave up."""
+    from bench import CONFIGS
+    c = CONFIGS[cfg]
+    exact = cfg in ("C4", "C5")
+    g = torch.Generator(device=gpu)
+    g.manual_seed(11)
+    envs = {}
+    for mode in ("throughput", "latency"):
+        env = wrap_for_brax_training(Joystick(c["task"], num_envs=n, device=gpu, use_imitation=c["imitation"]),
+                                     episode_length=5, randomization_fn=domain_randomize if c["dr"] else None)
+        env.set_step_mode(mode)
+        assert env.step_kernel == mode
+        env.lat_timeouts(reset=True)
+        envs[mode] = env
+    st = envs["throughput"].reset(rng=4)
+    L = envs["throughput"]._layout
+    nq = envs["throughput"].mj_model.nq
+    rel = lambda x, y: ((x - y).abs() / (1 + y.abs())).max().item()  # noqa: E731
+    for t in range(8):
+        a = torch.rand(n, 14, device=gpu, generator=g) * 2 - 1
+        s_t = envs["throughput"].step(st, a)
+        s_l = envs["latency"].step(st, a)
+        torch.cuda.synchronize()
+        assert torch.equal(s_t.istate, s_l.istate) and torch.equal(s_t.done, s_l.done), t
+        if exact:
+            for x, y in ((s_t.fstate, s_l.fstate), (s_t.obs["state"], s_l.obs["state"]),
+                         (s_t.obs["privileged_state"], s_l.obs["privileged_state"]), (s_t.reward, s_l.reward)):
+                assert torch.equal(x, y), (t, (x != y).sum().item())
+        else:
+            ft, fl = s_t.fstate.view(L.nfloat, n), s_l.fstate.view(L.nfloat, n)
+            q0 = L.off["qpos"]
+            assert rel(fl[q0:q0 + nq], ft[q0:q0 + nq]) < 1e-6, t
+            assert rel(s_l.obs["privileged_state"], s_t.obs["privileged_state"]) < 2e-3, t
+            assert rel(s_l.reward, s_t.reward) < 1e-4, t
+        st = s_t
+    assert envs["latency"].lat_timeouts() == 0
+
+
+def test_step_mode_auto_selects_by_batch(gpu):
+    """AUTO: the latency kernel while the batch leaves a CU per 4 envs, the throughput kernel above."""
+    ncu = torch.cuda.get_device_properties(gpu).multi_processor_count
+    for n, want in ((4 * ncu, "latency"), (4 * ncu + 1, "throughput")):
+        env = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
+        assert env.step_kernel == want, (n, ncu)
+
+
 def test_full_size_long_rollout_with_auto_reset(gpu):
     """4096 envs x 300 env-steps of U(-1,1) actions with a 100-step episode limit: every row stays
     finite and the EpisodeWrapper/AutoReset bookkeeping holds for every env: an env is done at the
