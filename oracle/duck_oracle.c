@@ -714,6 +714,11 @@ void oracle_hfield_axis_wins(long long out[14], int reset) {
  * overlaps may order them the other way (teacher forcing's "sat_tie" rule). */
 static _Thread_local double g_hf_tie_last;
 void oracle_set_hf_tie_last(double band) { g_hf_tie_last = band; }
+/* test aid (oracle_set_hf_tie_first): the FIRST axis of the priority order whose overlap is within this
+ * band of the minimum (0, default: the minimum itself). The mirror case of tie_last: the fp64 minimum is
+ * a later axis by less than the band, the kernel's fp32 overlaps put an earlier one at or below it. */
+static _Thread_local double g_hf_tie_first;
+void oracle_set_hf_tie_first(double band) { g_hf_tie_first = band; }
 
 /* test aid (oracle_set_hf_band_scale): scales HF_POINT_BAND (default 1; 0 = the plain weighted
  * centroid, round 3's point rule): tools/hfield_deviation.py compares the two. */
@@ -846,7 +851,7 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
     return 0;
   }
   int w = 0;
-  while (w < na - 1 && ov[w] > mn) w++;
+  while (w < na - 1 && ov[w] > mn + g_hf_tie_first) w++; /* (g_hf_tie_first: test aid, 0 by default) */
   if (g_hf_tie_last > 0) /* test aid: the last axis within the tie band instead of the first */
     for (int i = 0; i < na; i++)
       if (ov[i] <= mn + g_hf_tie_last) w = i;

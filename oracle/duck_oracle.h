@@ -81,6 +81,7 @@ void oracle_set_ls_floor(double floor); /* test aid: the HIP line search's fp32 
 void oracle_set_hdump(double* buf); /* test aid: dump the next solve's first Newton Hessian and row margins */
 void oracle_set_hf_band_scale(double s); /* test aid: scales HF_POINT_BAND (0: the plain weighted centroid) */
 void oracle_set_hf_tie_last(double band); /* test aid: height-field SAT near-ties resolve to the last axis in the band */
+void oracle_set_hf_tie_first(double band); /* test aid: height-field SAT near-ties resolve to the first axis in the band */
 int oracle_hfield_contacts(const oracle_model* m, const oracle_data* d, int g_hf, int g_cvx, int max, double* depth,
                            double* normal, double* point); /* test aid: the prism contacts before the manifold selection */
 void oracle_set_con_override(const double* buf); /* test aid: replace the contact set after collision (7 doubles per slot) */

@@ -86,6 +86,7 @@ def lib():
         L.oracle_set_hdump.argtypes = [dp]
         L.oracle_set_hf_band_scale.argtypes = [C.c_double]
         L.oracle_set_hf_tie_last.argtypes = [C.c_double]
+        L.oracle_set_hf_tie_first.argtypes = [C.c_double]
         L.oracle_hfield_contacts.argtypes = [vp, C.POINTER(OracleData), C.c_int, C.c_int, C.c_int, dp, dp, dp]
         L.oracle_set_con_override.argtypes = [dp]
         L.oracle_last_start_costs.argtypes = [C.POINTER(C.c_double)]

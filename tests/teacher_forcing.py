@@ -444,8 +444,8 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     within `onset` (m) of zero depth -- which prisms of a height field touch at the onset is decided
     below fp32 resolution.
     "sat_tie": two separating axes of one height-field prism overlap within 1e-6 m (the kernel's fp32
-    error bound on an overlap), and the oracle resolving such ties to the other axis
-    (oracle_set_hf_tie_last) lands on the GPU's result;
+    error bound on an overlap), and the oracle resolving such ties to the other axis -- the last one in
+    the band (oracle_set_hf_tie_last) or the first (oracle_set_hf_tie_first) -- lands on the GPU's result;
     "onset_selection": the manifold chose other prism contacts around an onset-depth prism -- every GPU
     slot of the differing pairs is one of the oracle's own prism contacts (oracle_hfield_contacts) or
     at the onset depth, and the oracle continued from the GPU's slots lands on the GPU's result
@@ -469,13 +469,14 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     # a height-field prism whose two best separating axes overlap within 1e-6 m (the kernel's fp32 error
     # bound on an overlap: tied at its precision): the oracle resolving such ties to the other axis
     # lands on the GPU
-    lib().oracle_set_hf_tie_last(1e-6)
-    try:
-        r = oracle_substep(om, x)
-    finally:
-        lib().oracle_set_hf_tie_last(0.0)
-    if _state_rel(m, g, r) <= sub_tol:
-        return "sat_tie"
+    for tie in (lib().oracle_set_hf_tie_last, lib().oracle_set_hf_tie_first):
+        tie(1e-6)
+        try:
+            r = oracle_substep(om, x)
+        finally:
+            tie(0.0)
+        if _state_rel(m, g, r) <= sub_tol:
+            return "sat_tie"
     n = env.num_envs
     T = lambda y: torch.tensor(np.tile(y.astype(np.float32)[:, None], (1, n)), device=env.device).contiguous()  # noqa: E731
     tq, tv, tw, tc = (T(y) for y in _split(m, x))
