@@ -875,10 +875,10 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
 }
 
 // Latency mode (duck_set_step_mode / DUCK_STEP_LATENCY, or AUTO at <= 4 envs per CU): 4 envs per
-// workgroup and the stages of each substep split over its waves (TPhys::lat_r0 / lat_r1 / lat_r2,
+// workgroup and the stages of each substep split over its waves (TPhys::lat_r0 .. lat_r3,
 // duck_team.h): wave 0 runs the env code and kinematics / com_pos / rne / actuation, wave 1 crb, the
-// factorizations, the Newton solve, sensors and Euler, wave 2 collision and the constraint rows;
-// wave 3 only helps stage the hot state. Same stage code and arithmetic as step_kernel, so the
+// warm start, the Newton solve, sensors and Euler, wave 2 collision and the constraint rows, wave 3
+// the smooth acceleration (M's factorization and solve). Same stage code and arithmetic as step_kernel, so the
 // results are the same bit for bit (test_gpu_env.py::test_latency_mode_matches_throughput_mode);
 // one env-step of a small batch takes the critical path through the waves instead of the sum.
 template <class Md>
@@ -933,6 +933,8 @@ __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
       for (int s = 0; s < ns; s++) TPL::lat_r1(L.p, lane, s, true, s == ns - 1, scr, n);
     } else if (wave == 2) {
       for (int s = 0; s < ns; s++) TPL::lat_r2(L.p, lane, s, A.hfield);
+    } else {
+      for (int s = 0; s < ns; s++) TPL::lat_r3(L.p, lane, s);
     }
   }
   __syncthreads();

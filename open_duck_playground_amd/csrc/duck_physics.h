@@ -24,7 +24,7 @@ typedef __attribute__((address_space(3))) float lds_float;
 
 // optional per-stage cycle counters (build with -DDUCK_STAGE_PROF; read by duck_debug_stage_cycles);
 // -DDUCK_WAVE_PROF records only the per-wave launch cycles (no stage marks perturbing wave 0)
-#if defined(DUCK_STAGE_PROF) || defined(DUCK_WAVE_PROF)
+#if defined(DUCK_STAGE_PROF) || defined(DUCK_WAVE_PROF) || defined(DUCK_LAT_PROF)
 #define DUCK_ANY_PROF 1
 #endif
 #ifdef DUCK_ANY_PROF

@@ -154,13 +154,25 @@ constexpr float HF_POINT_BAND = 1e-4f;
 
 // Latency mode (LAT, step_kernel_lat): the stages of one substep are split over the four waves of a
 // workgroup that all work the same 4 envs (wave 0: kinematics, com_pos, rne, actuation and the env
-// code; wave 1: composite inertias, crb, M's factorization, the smooth solve, the Newton solve,
-// sensors, Euler; wave 2: collision and the constraint rows). Waves that run concurrently must not
+// code; wave 1: composite inertias, crb, the warm start, the Newton solve, sensors, Euler; wave 2:
+// collision and the constraint rows; wave 3: M's factorization and the smooth solve). Waves that run concurrently must not
 // share scratch, so a latency slice gives rne's scratch, the composite inertias and the height
 // field's silhouette lists regions of their own after the throughput slice's words.
 constexpr int LAT_WG = 4;  // envs (teams) per latency-mode workgroup: 4 waves x 4 teams, one team set per wave
 // latency-mode event waits that gave up (TPhys::ev_wait; read by duck_debug_lat_timeouts, must stay 0)
 static __device__ unsigned int g_lat_timeouts;
+// -DDUCK_LAT_PROF (tools/lat_prof.py): clock64 of each cross-wave event of substep 5 in workgroup 0, into
+// the per-wave cycle slots of g_stage_cycles (which only the throughput kernel writes)
+#ifdef DUCK_LAT_PROF
+#define LAT_T(k, s)                                                                                         \
+  do {                                                                                                      \
+    if (blockIdx.x == 0 && ((int)threadIdx.x & 63) == 0 && (s) == 5) g_stage_cycles[DUCK_NSTAGE + (k)] = clock64(); \
+  } while (0)
+#else
+#define LAT_T(k, s) \
+  do {              \
+  } while (0)
+#endif
 
 template <class Md, bool LAT = false>
 struct TLay {
@@ -2720,6 +2732,103 @@ struct TPhys {
   // Mc: M as full symmetric columns in registers for every M.x of the solver
   static DK void solve(LP L, int lane, float* scratch, int stride, const float (*Mc)[NV]) {
     STAGE_T0();
+    const float g0 = warm_start(L, lane, Mc);
+    newton(L, lane, scratch, stride, Mc, g0);
+  }
+  // latency mode: the warm start's products that need only qacc_warmstart (its feet motions, M and J
+  // products, constraint costs) run while wave 3 solves for qacc_smooth; then those of qacc_smooth
+  // and the choice. The same operations in the same order as warm_start's fused pass: same values.
+  static DK void warm_start_a(LP L, int lane, const float (*Mc)[NV], float& cwp) {
+    float sw, ss;
+    spatial2(L, lane, Ly::WARM, -1, sw, ss);
+    {
+      float xw[NC];
+      lane_vec(L, lane, Ly::WARM, xw);
+      mul_cols(L, lane, Mc, xw, Ly::MA);
+    }
+    TSYNC();
+    float SL[6], SR[6];
+    sp_bcast(sw, SL, SR);
+    cwp = 0.0f;
+    {
+      const bool fr = lane < NFRIC;
+      const int r = fr ? lane : 0, i = fric_dof(r);
+      const float D = L[Ly::RD + r], f = L[Ly::DFRIC + i], ar = L[Ly::AREF + r];
+      const float jw = L[Ly::WARM + i] - ar;
+      cwp += fr ? fric_cost(D, jw, f) : 0.0f;
+      L[fr ? Ly::JA + r : TL::SINK + lane] = jw;
+    }
+    for (int r = lane; r < NLIM; r += TEAM) {
+      const int i = lim_dof(r), row = R_LIM + r;
+      const float D = L[Ly::RD + row], sg = L[Ly::LSGN + r], ar = L[Ly::AREF + row];
+      const float jw = sg * L[Ly::WARM + i] - ar;
+      cwp += jw < 0.0f ? 0.5f * D * jw * jw : 0.0f;
+      L[Ly::JA + row] = jw;
+    }
+    if (lane < NCON) {
+      float vw[4];
+      contact_jx(L, lane >> 2, lane, SL, SR, vw);
+      for (int e = 0; e < 4; e++) {
+        const int row = R_CON + 4 * lane + e;
+        const float D = L[Ly::RD + row], ar = L[Ly::AREF + row];
+        const float jw = vw[e] - ar;
+        cwp += jw < 0.0f ? 0.5f * D * jw * jw : 0.0f;
+        L[Ly::JA + row] = jw;
+      }
+    }
+  }
+  static DK float warm_start_b(LP L, int lane, float cwp) {
+    float ss, s2;
+    spatial2(L, lane, Ly::QSM, -1, ss, s2);
+    TSYNC();
+    float SL2[6], SR2[6];
+    sp_bcast(ss, SL2, SR2);
+    float csp = 0.0f, gwp = 0.0f;
+    {
+      const bool fr = lane < NFRIC;
+      const int r = fr ? lane : 0, i = fric_dof(r);
+      const float D = L[Ly::RD + r], f = L[Ly::DFRIC + i], ar = L[Ly::AREF + r];
+      const float js = L[Ly::QSM + i] - ar;
+      csp += fr ? fric_cost(D, js, f) : 0.0f;
+      L[fr ? Ly::JV + r : TL::SINK + TEAM + lane] = js;
+    }
+    for (int r = lane; r < NLIM; r += TEAM) {
+      const int i = lim_dof(r), row = R_LIM + r;
+      const float D = L[Ly::RD + row], sg = L[Ly::LSGN + r], ar = L[Ly::AREF + row];
+      const float js = sg * L[Ly::QSM + i] - ar;
+      csp += js < 0.0f ? 0.5f * D * js * js : 0.0f;
+      L[Ly::JV + row] = js;
+    }
+    if (lane < NCON) {
+      float vs[4];
+      contact_jx(L, lane >> 2, lane, SL2, SR2, vs);
+      for (int e = 0; e < 4; e++) {
+        const int row = R_CON + 4 * lane + e;
+        const float D = L[Ly::RD + row], ar = L[Ly::AREF + row];
+        const float js = vs[e] - ar;
+        csp += js < 0.0f ? 0.5f * D * js * js : 0.0f;
+        L[Ly::JV + row] = js;
+      }
+    }
+    for (int i = lane; i < NV; i += TEAM)
+      gwp += 0.5f * (L[Ly::MA + i] - L[Ly::FSM + i]) * (L[Ly::WARM + i] - L[Ly::QSM + i]);
+    const float gw = tsum(gwp);
+    const float cw = gw + tsum(cwp), cs = tsum(csp);
+    float g0;
+    if (cw < cs) {
+      for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] = L[Ly::WARM + i];
+      g0 = gw;
+    } else {
+      for (int i = lane; i < NV; i += TEAM) { L[Ly::QACC + i] = L[Ly::QSM + i]; L[Ly::MA + i] = L[Ly::FSM + i]; }
+      for (int r = lane; r < NROW; r += TEAM) L[Ly::JA + r] = L[Ly::JV + r];
+      g0 = 0.0f;
+    }
+    TSYNC();
+    return g0;
+  }
+  // warm start vs smooth acceleration (mjx solver.solve's start): returns the Gauss cost at the start
+  static DK float warm_start(LP L, int lane, const float (*Mc)[NV]) {
+    STAGE_T0();
     // warm start vs smooth acceleration: J and M products of both in one pass
     // (M qacc_smooth = qfrc_smooth by definition: no product needed for the smooth start)
     float sw, ss;
@@ -2785,6 +2894,13 @@ struct TPhys {
     }
     TSYNC();
     STAGE_MARK(9);
+    return g0;
+  }
+  // Md::iterations Newton steps from the start in QACC / MA / JA (Gauss cost g0 there)
+  static DK void newton(LP L, int lane, float* scratch, int stride, const float (*Mc)[NV], float g0) {
+    STAGE_T0();
+    (void)scratch;
+    (void)stride;
     for (int newton_it = 0;;) {
     const bool sparse_ok = newton_fused<false>(L, lane, Mc);
     STAGE_MARK(10);
@@ -3132,7 +3248,7 @@ struct TPhys {
   // grow within a launch, so no event is reset between substeps. A spin is bounded (~40 ms, far
   // beyond a substep) so that a broken schedule ends the launch instead of hanging the device;
   // g_lat_timeouts counts such exits (tests read it: it must stay 0).
-  enum { EV_KIN = 0, EV_VEL = 1, EV_FSM = 2, EV_ROWS = 3, EV_EULER = 4 };
+  enum { EV_KIN = 0, EV_VEL = 1, EV_FSM = 2, EV_ROWS = 3, EV_EULER = 4, EV_M = 5, EV_QSM = 6 };
   static DK lds_int* ev_ptr(int k) {
     extern __shared__ float lds_dyn[];
     return (lds_int*)(lds_dyn + TL::EV) + 4 * k;
@@ -3156,32 +3272,44 @@ struct TPhys {
   // (the contact rows need the feet's), then the rest of rne and the actuation (qfrc_smooth)
   static DK void lat_r0(LP L, int lane, int s) {
     ev_wait(EV_EULER, s);
+    LAT_T(0, s);
     kinematics(L, lane);
     com_pos(L, lane);
     ev_signal(EV_KIN, s + 1);
+    LAT_T(1, s);
     rne_vel(L, lane);
     ev_signal(EV_VEL, s + 1);
+    LAT_T(2, s);
     rne_rest<1>(L, lane);
     smooth(L, lane);
     ev_signal(EV_FSM, s + 1);
+    LAT_T(3, s);
   }
-  // wave 1: composite inertias, M, its register columns and factorization while wave 0 finishes rne;
-  // the smooth solve once qfrc_smooth is there, the Newton solve once the rows are, sensors, Euler
+  // wave 1: composite inertias and M (crb) while wave 0 finishes rne; M's register columns and the warm
+  // start's products of qacc_warmstart while wave 3 factors M and solves for qacc_smooth; then the rest
+  // of the warm start, the Newton solve, sensors, Euler
   static DK void lat_r1(LP L, int lane, int s, bool integrate, bool want_out, float* scratch, int sstride) {
     ev_wait(EV_KIN, s + 1);
+    LAT_T(10, s);
     subtree_sums<2>(L, lane);
     crb(L, lane);
+    ev_signal(EV_M, s + 1);
+    LAT_T(11, s);
     {
       float Mc[NC][NV];
       load_cols(L, lane, Mc, false);
-      {
-        Fac F;
-        smooth_factor(F, lane, Mc);
-        ev_wait(EV_FSM, s + 1);
-        smooth_solve(L, lane, F);
-      }
+      LAT_T(12, s);
       ev_wait(EV_ROWS, s + 1);
-      solve(L, lane, scratch, sstride, Mc);
+      LAT_T(13, s);
+      float cwp;
+      warm_start_a(L, lane, Mc, cwp);
+      LAT_T(14, s);
+      ev_wait(EV_QSM, s + 1);
+      LAT_T(15, s);
+      const float g0 = warm_start_b(L, lane, cwp);
+      LAT_T(16, s);
+      newton(L, lane, scratch, sstride, Mc, g0);
+      LAT_T(17, s);
     }
     if (want_out) sensors(L, lane);
     if (integrate) {
@@ -3191,13 +3319,33 @@ struct TPhys {
       TSYNC();
     }
     ev_signal(EV_EULER, s + 1);
+    LAT_T(18, s);
   }
   // wave 2: collision (kinematics only), then the constraint rows (the feet's velocities)
   static DK void lat_r2(LP L, int lane, int s, const float* hf) {
     ev_wait(EV_KIN, s + 1);
+    LAT_T(20, s);
     collision(L, lane, hf);
+    LAT_T(21, s);
     ev_wait(EV_VEL, s + 1);
+    LAT_T(22, s);
     make_rows(L, lane);
     ev_signal(EV_ROWS, s + 1);
+    LAT_T(23, s);
+  }
+  // wave 3: qacc_smooth = M^-1 qfrc_smooth from its own register columns of M
+  static DK void lat_r3(LP L, int lane, int s) {
+    ev_wait(EV_M, s + 1);
+    LAT_T(30, s);
+    float Mc[NC][NV];
+    load_cols(L, lane, Mc, false);
+    Fac F;
+    smooth_factor(F, lane, Mc);
+    LAT_T(31, s);
+    ev_wait(EV_FSM, s + 1);
+    LAT_T(32, s);
+    smooth_solve(L, lane, F);
+    ev_signal(EV_QSM, s + 1);
+    LAT_T(33, s);
   }
 };

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Timeline of one substep of the latency kernel (step_kernel_lat): clock64 at every cross-wave event of
+substep 5 in workgroup 0, from a -DDUCK_LAT_PROF build (DUCK_LIB=...libduck_latprof.so), in cycles after
+wave 0 starts the substep, averaged over the last launches.
+usage: DUCK_LIB=open_duck_playground_amd/libduck_latprof.so python tools/lat_prof.py [--config C2] [--envs 512]"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from bench import CONFIGS  # noqa: E402
+from open_duck_playground_amd.joystick import Joystick, domain_randomize, wrap_for_brax_training  # noqa: E402
+
+NAMES = {0: "w0 start (Euler of s-1 seen)", 1: "w0 kinematics+com_pos done", 2: "w0 rne velocities done",
+         3: "w0 rne + actuation done (qfrc_smooth)",
+         10: "w1 com_pos seen", 11: "w1 composite inertias + crb done", 12: "w1 M columns loaded",
+         13: "w1 rows seen", 14: "w1 warm start (qacc_warmstart) done", 15: "w1 qacc_smooth seen",
+         16: "w1 warm start done", 17: "w1 Newton + line search done", 18: "w1 Euler done",
+         20: "w2 com_pos seen", 21: "w2 collision done", 22: "w2 rne velocities seen", 23: "w2 rows done",
+         30: "w3 crb seen", 31: "w3 M factored", 32: "w3 qfrc_smooth seen", 33: "w3 qacc_smooth done"}
+NSTAGE = 56
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--envs", type=int, default=512)
+    ap.add_argument("--steps", type=int, default=30)
+    a = ap.parse_args()
+    c = CONFIGS[a.config]
+    dev = torch.device("cuda:0")
+    env = wrap_for_brax_training(Joystick(c["task"], num_envs=a.envs, device=dev, use_imitation=c["imitation"]),
+                                 episode_length=1000, randomization_fn=domain_randomize if c["dr"] else None)
+    env.set_step_mode("latency")
+    st = env.reset(rng=0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    buf = (C.c_ulonglong * (NSTAGE + 3 * 1024))()
+    rows = []
+    for t in range(a.steps):
+        st = env.step(st, torch.rand(a.envs, 14, device=dev, generator=g) * 2 - 1, inplace=True)
+        torch.cuda.synchronize()
+        if env._lib.duck_debug_stage_cycles(env._sim, buf, 1) != 0:
+            raise SystemExit("not a DUCK_LAT_PROF build")
+        if t >= 10:
+            v = np.array([buf[NSTAGE + k] for k in range(40)], dtype=np.float64)
+            rows.append(v - v[0])
+    r = np.mean(rows, axis=0)
+    for k in sorted(NAMES, key=lambda k: r[k]):
+        print(f"{r[k]:9.0f}  {NAMES[k]}")
+    print(f"substep (w0 start -> w1 Euler): {r[18]:.0f} cycles")
+
+
+if __name__ == "__main__":
+    main()
