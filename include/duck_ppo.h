@@ -5,6 +5,7 @@
  *   duck_ppo_loss  brax losses.compute_ppo_loss after GAE: clipped surrogate + value loss + entropy
  *                  bonus of one minibatch and its gradient w.r.t. the policy logits and the value
  *                  baseline (open_duck_playground_amd/ppo.py:ppo_loss is the same computation in torch)
+ *   duck_gather_columns  a minibatch's trajectories out of the rollout buffers (all fields, one launch)
  *
  * Same conventions as duck.h: DEVICE pointers, float32, time-major [T][B] arrays (B = number of
  * trajectories, contiguous), `stream` a hipStream_t, negative return codes on error.
@@ -38,8 +39,20 @@ int duck_ppo_loss(int N, int A, const float* logits, const float* raw_action, co
                   const float* advantage, const float* value_target, const float* baseline, const float* eps,
                   float clip_eps, float entropy_cost, int normalize_advantage, float* out, float* grad_logits,
                   float* grad_baseline, void* stream);
-/* 4 + 2 + 3 ceil(N / 128): the length of duck_ppo_loss's out array (A <= 31) */
+/* 4 + 2 + 3 ceil(N / 16): the length of duck_ppo_loss's out array (A <= 31) */
 int duck_ppo_loss_out_size(int N);
+
+/* One minibatch's trajectories out of the rollout buffers (brax ppo/train.py: the shuffled
+ * jnp.take(data, permutation, axis=1) of each minibatch), every field in one launch: field f copies
+ * dst[t][j][c] = src[t][idx[j]][c] for t < T_f, j < m, c < w_f (src [T_f][B_f][w_f], dst [T_f][m][w_f],
+ * float32, row-major; idx int64 [m], each < B_f). At most DUCK_GATHER_MAX fields. */
+#define DUCK_GATHER_MAX 8
+typedef struct {
+  const float* src;
+  float* dst;
+  int T, B, w;
+} duck_gather_field;
+int duck_gather_columns(int nfields, const duck_gather_field* fields, const long long* idx, int m, void* stream);
 
 /* The policy / value MLP layers (brax ppo/networks.py: Dense + swish; nn.Linear weight layout
  * W [M][R] row-major, bias [M]) on fp32 MFMA, row-major activations [N][.]:

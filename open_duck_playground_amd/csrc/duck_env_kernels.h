@@ -552,8 +552,10 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
     // below reads the last substep's state and sensors: wait for wave 1's Euler
     using TPL = TPhys<Md, true>;
     (void)scr;
+    LAT_T(43, 5);
     for (int s = 0; s < c.n_substeps; s++) TPL::lat_r0(L.p, lane, s);
     TPL::ev_wait(TPL::EV_EULER, c.n_substeps);
+    LAT_T(44, 5);
   } else {
     for (int s = 0; s < c.n_substeps; s++)
       phys_step<Md>(L, lane, true, s == c.n_substeps - 1, nullptr, 0, scr, n, A.hfield);
@@ -889,8 +891,10 @@ __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
   static_assert(TL::TAB_LDS && TL::ES_LDS, "latency mode: the model blob and the hot state in LDS");
   static_assert(TPB == 4 * 64 && WGL * TEAM == 64, "latency mode: 4 waves, one set of 4 teams per wave");
   extern __shared__ float lds[];
+  LAT_T(40, 5);
   TPL::ev_init((int)threadIdx.x);
   load_model_tables<Md, true>(lds);  // (ends with a workgroup barrier: the event counters are 0 before any wait)
+  LAT_T(41, 5);
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int t = ((int)threadIdx.x & 63) / TEAM, lane = (int)threadIdx.x % TEAM;
   const int e = blockIdx.x * WGL + t;
@@ -914,6 +918,7 @@ __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
     }
   }
   __syncthreads();
+  LAT_T(42, 5);
   if (e < n) {
     const Slice<SW> L = env_slice<Md, true>(lds, t);
     const int ns = A.cfg.n_substeps;
@@ -928,6 +933,7 @@ __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
       rt.fill(esp + TL::HOT, lane);
       TSYNC();
       step_env<Md, LCol, true, RngTab, true>(A, e, lane, L, LCol{esp}, G, rt, P);
+      LAT_T(45, 5);
     } else if (wave == 1) {
       float* scr = A.scratch ? A.scratch + e : nullptr;
       for (int s = 0; s < ns; s++) TPL::lat_r1(L.p, lane, s, true, s == ns - 1, scr, n);
@@ -938,6 +944,7 @@ __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
     }
   }
   __syncthreads();
+  LAT_T(46, 5);
   {
     float hv[NK];
 #pragma unroll

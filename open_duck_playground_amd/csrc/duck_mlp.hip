@@ -20,6 +20,8 @@
 // and ran 3-4x slower). LDS rows padded to 33 floats.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "duck_common.h"
 #include "duck_math.h"
 #include "../../include/duck_ppo.h"
@@ -186,34 +188,47 @@ __global__ __launch_bounds__(256) void mlp_gemm_kernel(int N, int R, int Mo, con
   for (int i = 0; i < TI; i++)
 #pragma unroll
     for (int j = 0; j < TJ; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  RowTile<BM> la;
-  RowTile<BN> lbr;  // MODE 0/1: the rows of W (output columns), reduction contiguous
-  ColTile<BN> lbc;  // MODE 2: W [R][Mo], reduction over its rows
-  la.init(A, R, N, r0);
-  if (MODE != 2) lbr.init(W, R, Mo, c0);
+  // two register sets of staged chunks (set k & 1 holds chunk k): chunk c + 2's loads are issued while
+  // chunk c's MFMAs run and stored a whole chunk later, so each load has two chunks of MFMAs to land
+  RowTile<BM> la[2];
+  RowTile<BN> lbr[2];  // MODE 0/1: the rows of W (output columns), reduction contiguous
+  ColTile<BN> lbc[2];  // MODE 2: W [R][Mo], reduction over its rows
+  for (int q = 0; q < 2; q++) {
+    la[q].init(A, R, N, r0);
+    if (MODE != 2) lbr[q].init(W, R, Mo, c0);
+  }
   const float* mn = MODE == 2 ? nullptr : mean;
-  auto load = [&](int k0) {
-    la.load(R, k0, mn, istd);
-    if (MODE == 2) lbc.load(W, Mo, R, Mo, k0, c0, false, nullptr, nullptr);
-    else lbr.load(R, k0, nullptr, nullptr);
+  auto load = [&](auto S, int k0) {
+    constexpr int q = decltype(S)::value;
+    la[q].load(R, k0, mn, istd);
+    if (MODE == 2) lbc[q].load(W, Mo, R, Mo, k0, c0, false, nullptr, nullptr);
+    else lbr[q].load(R, k0, nullptr, nullptr);
   };
-  auto store = [&]() {
-    la.store(As);
-    if (MODE == 2) lbc.store(Bs);
-    else lbr.store(Bs);
+  auto store = [&](auto S) {
+    constexpr int q = decltype(S)::value;
+    la[q].store(As);
+    if (MODE == 2) lbc[q].store(Bs);
+    else lbr[q].store(Bs);
   };
   const int nch = (R + KC - 1) / KC;
-  load(0);
-  store();
+  const std::integral_constant<int, 0> S0;
+  const std::integral_constant<int, 1> S1;
+  load(S0, 0);
+  if (nch > 1) load(S1, KC);
+  store(S0);
   __syncthreads();
-  for (int c = 0; c < nch; c++) {
-    if (c + 1 < nch) load(KC * (c + 1));  // in flight while this chunk's MFMAs run
+  auto body = [&](int c, auto S, auto SN) {
+    if (c + 2 < nch) load(S, KC * (c + 2));  // set S held chunk c (already in LDS)
     mma_chunk<TI, TJ>(As, Bs, wr, wc, acc);
     __syncthreads();
     if (c + 1 < nch) {
-      store();
+      store(SN);
       __syncthreads();
     }
+  };
+  for (int c = 0; c < nch; c += 2) {
+    body(c, S0, S1);
+    if (c + 1 < nch) body(c + 1, S1, S0);
   }
   // epilogue: acc[i][j][q] is C[wr + 16 i + 4 (l >> 4) + q][wc + 16 j + (l & 15)]
   const int l = threadIdx.x & 63;
@@ -260,30 +275,41 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(int N, int Mo, int Ki, c
   for (int i = 0; i < TI; i++)
 #pragma unroll
     for (int j = 0; j < TJ; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  ColTile<BM> la;  // A = dZ^T: columns m, reduction n over the rows
-  ColTile<BN> lb;  // B = [op(H) | 1]: columns k, rows n
+  ColTile<BM> la[2];  // A = dZ^T: columns m, reduction n over the rows (two staged chunks, as above)
+  ColTile<BN> lb[2];  // B = [op(H) | 1]: columns k, rows n
   const float* dz = dZ + (size_t)(R > 0 ? n_lo : 0) * Mo;
   const float* h = H + (size_t)(R > 0 ? n_lo : 0) * Ki;
-  auto load = [&](int n0) {
-    la.load(dz, Mo, R, Mo, n0, m0, false, nullptr, nullptr);
-    lb.load(h, Ki, R, Ki, n0, k0c, true, mean, istd);
+  auto load = [&](auto S, int n0) {
+    constexpr int q = decltype(S)::value;
+    la[q].load(dz, Mo, R, Mo, n0, m0, false, nullptr, nullptr);
+    lb[q].load(h, Ki, R, Ki, n0, k0c, true, mean, istd);
+  };
+  auto store = [&](auto S) {
+    constexpr int q = decltype(S)::value;
+    la[q].store(As);
+    lb[q].store(Bs);
   };
   const int nch = (R + KC - 1) / KC;
+  const std::integral_constant<int, 0> S0;
+  const std::integral_constant<int, 1> S1;
   if (nch > 0) {
-    load(0);
-    la.store(As);
-    lb.store(Bs);
+    load(S0, 0);
+    if (nch > 1) load(S1, KC);
+    store(S0);
   }
   __syncthreads();
-  for (int c = 0; c < nch; c++) {
-    if (c + 1 < nch) load(KC * (c + 1));
+  auto body = [&](int c, auto S, auto SN) {
+    if (c + 2 < nch) load(S, KC * (c + 2));
     mma_chunk<TI, TJ>(As, Bs, wr, wc, acc);
     __syncthreads();
     if (c + 1 < nch) {
-      la.store(As);
-      lb.store(Bs);
+      store(SN);
       __syncthreads();
     }
+  };
+  for (int c = 0; c < nch; c += 2) {
+    body(c, S0, S1);
+    if (c + 1 < nch) body(c + 1, S1, S0);
   }
   float* out = part + (size_t)s * P;
   const int l = threadIdx.x & 63;

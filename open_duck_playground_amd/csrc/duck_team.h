@@ -2738,7 +2738,8 @@ struct TPhys {
   // latency mode: the warm start's products that need only qacc_warmstart (its feet motions, M and J
   // products, constraint costs) run while wave 3 solves for qacc_smooth; then those of qacc_smooth
   // and the choice. The same operations in the same order as warm_start's fused pass: same values.
-  static DK void warm_start_a(LP L, int lane, const float (*Mc)[NV], float& cwp) {
+  // (a0 needs only qacc_warmstart and M: it runs before the rows are there; a1 the rows' costs)
+  static DK void warm_start_a0(LP L, int lane, const float (*Mc)[NV], float* SL, float* SR) {
     float sw, ss;
     spatial2(L, lane, Ly::WARM, -1, sw, ss);
     {
@@ -2747,8 +2748,9 @@ struct TPhys {
       mul_cols(L, lane, Mc, xw, Ly::MA);
     }
     TSYNC();
-    float SL[6], SR[6];
     sp_bcast(sw, SL, SR);
+  }
+  static DK void warm_start_a1(LP L, int lane, const float* SL, const float* SR, float& cwp) {
     cwp = 0.0f;
     {
       const bool fr = lane < NFRIC;
@@ -3299,10 +3301,11 @@ struct TPhys {
       float Mc[NC][NV];
       load_cols(L, lane, Mc, false);
       LAT_T(12, s);
+      float SL[6], SR[6], cwp;
+      warm_start_a0(L, lane, Mc, SL, SR);
       ev_wait(EV_ROWS, s + 1);
       LAT_T(13, s);
-      float cwp;
-      warm_start_a(L, lane, Mc, cwp);
+      warm_start_a1(L, lane, SL, SR, cwp);
       LAT_T(14, s);
       ev_wait(EV_QSM, s + 1);
       LAT_T(15, s);

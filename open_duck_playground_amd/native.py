@@ -24,7 +24,12 @@ EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get"
            "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae", "duck_ppo_loss",
            "duck_ppo_loss_out_size", "duck_mlp_gemm", "duck_mlp_wgrad", "duck_mlp_wgrad_reduce",
            "duck_policy_sample", "duck_clip_adam", "duck_clip_adam_scratch_size", "duck_set_step_mode",
-           "duck_step_kernel_for", "duck_debug_lat_timeouts"]
+           "duck_step_kernel_for", "duck_debug_lat_timeouts", "duck_gather_columns"]
+
+
+class DuckGatherField(C.Structure):
+    """include/duck_ppo.h duck_gather_field"""
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("T", C.c_int), ("B", C.c_int), ("w", C.c_int)]
 
 
 class DuckError(RuntimeError):
@@ -249,6 +254,8 @@ def lib(path: str = None):
             L.duck_ppo_loss.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_int,
                                         vp, vp, vp, vp]
             L.duck_ppo_loss_out_size.argtypes = [C.c_int]
+        if hasattr(L, "duck_gather_columns"):
+            L.duck_gather_columns.argtypes = [C.c_int, C.POINTER(DuckGatherField), vp, C.c_int, vp]
         if hasattr(L, "duck_mlp_gemm"):
             ci = C.c_int
             L.duck_mlp_gemm.argtypes = [ci, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp]

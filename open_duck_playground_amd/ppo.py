@@ -427,15 +427,39 @@ class FusedGrad:
         """The minibatch's trajectories (columns idx of the [T, B, ...] buffers) into persistent buffers:
         the value network's input [priv rows | the bootstrap rows] assembled in place (no cat), and of
         next_priv only the last step (the bootstrap observation; the rest is never read)."""
+        from .native import DuckGatherField, check
         T, mb = data["reward"].shape[0], idx.numel()
         if not hasattr(self, "_mb"):
             self._mb = {k: torch.empty((T, mb) + v.shape[2:], device=v.device, dtype=v.dtype)
                         for k, v in data.items() if k not in ("priv", "next_priv")}
             self._xv = torch.empty(self.Nv, data["priv"].shape[-1], device=idx.device)
-        for k, buf in self._mb.items():
-            torch.index_select(data[k], 1, idx, out=buf)
-        torch.index_select(data["priv"], 1, idx, out=self._xv[:self.N].view(T, mb, -1))
-        torch.index_select(data["next_priv"][-1], 0, idx, out=self._xv[self.N:])
+        if not hasattr(self.lib, "duck_gather_columns"):  # (A/B baselines built before the gather kernel)
+            for k, buf in self._mb.items():
+                torch.index_select(data[k], 1, idx, out=buf)
+            torch.index_select(data["priv"], 1, idx, out=self._xv[:self.N].view(T, mb, -1))
+            torch.index_select(data["next_priv"][-1], 0, idx, out=self._xv[self.N:])
+            return {**self._mb, "xv": self._xv}
+        # every field in one duck_gather_columns launch (the rollout buffers and these are persistent,
+        # so the field table is built once; a captured learner graph replays the same pointers)
+        key = (tuple(v.data_ptr() for v in data.values()), idx.data_ptr())
+        if getattr(self, "_gkey", None) != key:
+            fl = []
+            for k, buf in self._mb.items():
+                v = data[k]
+                fl.append((v, buf, v.shape[0], v.shape[1], v[0, 0].numel()))
+            pv, npv = data["priv"], data["next_priv"]
+            fl.append((pv, self._xv[:self.N], T, pv.shape[1], pv.shape[-1]))
+            fl.append((npv[-1], self._xv[self.N:], 1, npv.shape[1], npv.shape[-1]))
+            for v, _, _, _, _ in fl:
+                if v.dtype != torch.float32 or not v.is_contiguous():
+                    raise ValueError("duck_gather_columns needs contiguous float32 rollout buffers")
+            self._gfields = (DuckGatherField * len(fl))(*[DuckGatherField(v.data_ptr(), d.data_ptr(), t, b, w)
+                                                          for v, d, t, b, w in fl])
+            self._gkey = key
+        if idx.dtype != torch.int64:
+            raise ValueError("minibatch indices must be int64")
+        st = torch.cuda.current_stream(idx.device).cuda_stream
+        check(self.lib.duck_gather_columns(len(self._gfields), self._gfields, idx.data_ptr(), mb, st))
         return {**self._mb, "xv": self._xv}
 
     def __call__(self, mb: Dict[str, torch.Tensor], cfg: PPOConfig, gen: Optional[torch.Generator]):

@@ -138,7 +138,7 @@ def test_cabi_exports_every_declared_symbol():
 def test_ppo_loss_sizes_and_argument_checks():
     """Host-side contract of duck_ppo_loss (no GPU call): the out array's length and the refusals."""
     lib = native.lib()
-    assert [lib.duck_ppo_loss_out_size(n) for n in (0, 1, 128, 129, 5120)] == [6, 9, 9, 12, 126]
+    assert [lib.duck_ppo_loss_out_size(n) for n in (0, 1, 128, 129, 5120)] == [6, 9, 30, 33, 966]
     assert lib.duck_ppo_loss(0, 14, *([None] * 7), 0.2, 0.005, 1, None, None, None, None) < 0
     assert b"empty batch" in lib.duck_last_error()
     assert lib.duck_ppo_loss(8, 14, *([None] * 7), 0.2, 0.005, 1, None, None, None, None) < 0

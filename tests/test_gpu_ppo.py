@@ -250,3 +250,27 @@ def test_clip_adam_matches_torch(gpu):
         assert int(step.item()) == 5
         err = float((p - ref.detach()).abs().max())
         assert err <= 1e-6, (scale, err)
+
+
+def test_gather_columns_matches_index_select(gpu):
+    """duck_gather_columns (one launch for every field of a minibatch) == torch.index_select per field,
+    including a one-row field (the bootstrap observation) and a field of width 1."""
+    import ctypes as C
+    from open_duck_playground_amd.native import DuckGatherField, check, lib
+    g = torch.Generator(device=gpu)
+    g.manual_seed(3)
+    T, B, m = 20, 300, 37
+    src = {"obs": torch.rand(T, B, 101, device=gpu, generator=g), "r": torch.rand(T, B, device=gpu, generator=g),
+           "a": torch.rand(T, B, 14, device=gpu, generator=g), "np": torch.rand(T, B, 172, device=gpu, generator=g)}
+    idx = torch.randperm(B, device=gpu, generator=g)[:m]
+    dst = {"obs": torch.empty(T, m, 101, device=gpu), "r": torch.empty(T, m, device=gpu),
+           "a": torch.empty(T, m, 14, device=gpu), "np": torch.empty(m, 172, device=gpu)}
+    f = [DuckGatherField(src[k].data_ptr(), dst[k].data_ptr(), T, B, w) for k, w in (("obs", 101), ("r", 1), ("a", 14))]
+    f.append(DuckGatherField(src["np"][-1].data_ptr(), dst["np"].data_ptr(), 1, B, 172))
+    arr = (DuckGatherField * len(f))(*f)
+    check(lib().duck_gather_columns(len(f), arr, idx.data_ptr(), m, torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    for k in ("obs", "r", "a"):
+        assert torch.equal(dst[k], torch.index_select(src[k], 1, idx)), k
+    assert torch.equal(dst["np"], torch.index_select(src["np"][-1], 0, idx))
+    assert lib().duck_gather_columns(9, arr, idx.data_ptr(), m, None) < 0

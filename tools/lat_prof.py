@@ -22,6 +22,8 @@ NAMES = {0: "w0 start (Euler of s-1 seen)", 1: "w0 kinematics+com_pos done", 2: 
          16: "w1 warm start done", 17: "w1 Newton + line search done", 18: "w1 Euler done",
          20: "w2 com_pos seen", 21: "w2 collision done", 22: "w2 rne velocities seen", 23: "w2 rows done",
          30: "w3 crb seen", 31: "w3 M factored", 32: "w3 qfrc_smooth seen", 33: "w3 qacc_smooth done"}
+LAUNCH = {40: "kernel start", 41: "model blob in LDS", 42: "hot state staged", 43: "w0 env code before the substeps done",
+          44: "w0 last Euler seen", 45: "w0 env code after the substeps done", 46: "final barrier"}
 NSTAGE = 56
 
 
@@ -47,9 +49,15 @@ def main():
         if env._lib.duck_debug_stage_cycles(env._sim, buf, 1) != 0:
             raise SystemExit("not a DUCK_LAT_PROF build")
         if t >= 10:
-            v = np.array([buf[NSTAGE + k] for k in range(40)], dtype=np.float64)
-            rows.append(v - v[0])
+            v = np.array([buf[NSTAGE + k] for k in range(48)], dtype=np.float64)
+            v[:40] -= v[0]
+            v[40:] -= v[40]
+            rows.append(v)
     r = np.mean(rows, axis=0)
+    print("launch (wave 0 of workgroup 0, cycles after its start):")
+    for k in sorted(LAUNCH):
+        print(f"{r[k]:9.0f}  {LAUNCH[k]}")
+    print("substep 5:")
     for k in sorted(NAMES, key=lambda k: r[k]):
         print(f"{r[k]:9.0f}  {NAMES[k]}")
     print(f"substep (w0 start -> w1 Euler): {r[18]:.0f} cycles")
