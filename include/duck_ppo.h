@@ -69,6 +69,20 @@ int duck_mlp_gemm(int mode, int N, int R, int M, const float* A, const float* W,
  * layers of the networks share one partial array and one duck_mlp_wgrad_reduce. */
 int duck_mlp_wgrad(int N, int M, int K, const float* dZ, const float* H, const float* mean, const float* istd,
                    int splits, float* partial, int P, int off_w, int off_b, void* stream);
+/* Up to DUCK_MLP_GROUP_MAX independent layer problems in one launch (the policy's and the value
+ * network's layers at one depth): kind 0, 1, 2 = duck_mlp_gemm's mode with (N, R, M, A, W, bias, aux,
+ * Y, Y2, mean, istd); kind 3 = duck_mlp_wgrad with N rows, R = K inputs, M outputs, A = dZ, W = H,
+ * mean, istd, splits, partial, P, off_w, off_b. The same results as the separate calls. */
+#define DUCK_MLP_GROUP_MAX 4
+typedef struct {
+  int kind, N, R, M;
+  const float *A, *W, *bias, *aux;
+  float *Y, *Y2;
+  const float *mean, *istd;
+  int splits, P, off_w, off_b;
+  float* partial;
+} duck_mlp_problem;
+int duck_mlp_group(int n, const duck_mlp_problem* problems, void* stream);
 /* grad[i] = sum_{s < splits} partial[s][i] in order (deterministic), i < P */
 int duck_mlp_wgrad_reduce(int P, int splits, const float* partial, float* grad, void* stream);
 /* The rollout's policy sample (brax NormalTanhDistribution): for each of N rows of logits [N][2A]

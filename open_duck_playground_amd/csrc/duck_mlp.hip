@@ -174,14 +174,13 @@ __device__ __forceinline__ void mma_chunk(const float* As, const float* Bs, int 
 // Forward (MODE 0: Y = op(A) W^T + b; MODE 1: the same, Y = Z and Y2 = silu(Z)) and the data gradient
 // (MODE 2: Y = (A W) * silu'(aux), A = dZ [N][R], W [R][Mo], aux = Z_prev). Output [N][Mo].
 template <int MODE>
-__global__ __launch_bounds__(256) void mlp_gemm_kernel(int N, int R, int Mo, const float* __restrict__ A,
-                                                       const float* __restrict__ W, const float* __restrict__ bias,
-                                                       const float* __restrict__ aux, float* __restrict__ Y,
-                                                       float* __restrict__ Y2, const float* __restrict__ mean,
-                                                       const float* __restrict__ istd) {
+__device__ __forceinline__ void gemm_tile(int bx, int by, float* As, float* Bs, int N, int R, int Mo,
+                                          const float* __restrict__ A, const float* __restrict__ W,
+                                          const float* __restrict__ bias, const float* __restrict__ aux,
+                                          float* __restrict__ Y, float* __restrict__ Y2,
+                                          const float* __restrict__ mean, const float* __restrict__ istd) {
   constexpr int TI = BM / 32, TJ = BN / 32;
-  __shared__ float As[BM * LDP], Bs[BN * LDP];
-  const int r0 = blockIdx.x * BM, c0 = blockIdx.y * BN;
+  const int r0 = bx * BM, c0 = by * BN;
   const int w = threadIdx.x >> 6, wr = (BM / 2) * (w >> 1), wc = (BN / 2) * (w & 1);
   f4 acc[TI][TJ];
 #pragma unroll
@@ -258,16 +257,25 @@ __global__ __launch_bounds__(256) void mlp_gemm_kernel(int N, int R, int Mo, con
     }
 }
 
+template <int MODE>
+__global__ __launch_bounds__(256) void mlp_gemm_kernel(int N, int R, int Mo, const float* __restrict__ A,
+                                                       const float* __restrict__ W, const float* __restrict__ bias,
+                                                       const float* __restrict__ aux, float* __restrict__ Y,
+                                                       float* __restrict__ Y2, const float* __restrict__ mean,
+                                                       const float* __restrict__ istd) {
+  __shared__ float As[BM * LDP], Bs[BN * LDP];
+  gemm_tile<MODE>(blockIdx.x, blockIdx.y, As, Bs, N, R, Mo, A, W, bias, aux, Y, Y2, mean, istd);
+}
+
 // [dW | db][m][k] = sum over this workgroup's rows n of dZ[n][m] [op(H) | 1][n][k]: partial s =
 // blockIdx.z, written to part + s * P at the layer's offsets (weights at offw, bias at offb; P = the
 // parameter count of the networks sharing the partial array).
-__global__ __launch_bounds__(256) void mlp_wgrad_kernel(int N, int Mo, int Ki, const float* __restrict__ dZ,
-                                                        const float* __restrict__ H, const float* __restrict__ mean,
-                                                        const float* __restrict__ istd, int rows_per_split,
-                                                        float* __restrict__ part, int P, int offw, int offb) {
+__device__ __forceinline__ void wgrad_tile(int bx, int by, int bz, float* As, float* Bs, int N, int Mo, int Ki,
+                                           const float* __restrict__ dZ, const float* __restrict__ H,
+                                           const float* __restrict__ mean, const float* __restrict__ istd,
+                                           int rows_per_split, float* __restrict__ part, int P, int offw, int offb) {
   constexpr int TI = BM / 32, TJ = BN / 32;
-  __shared__ float As[BM * LDP], Bs[BN * LDP];
-  const int m0 = blockIdx.x * BM, k0c = blockIdx.y * BN, s = blockIdx.z;
+  const int m0 = bx * BM, k0c = by * BN, s = bz;
   const int n_lo = s * rows_per_split, R = min(N, n_lo + rows_per_split) - n_lo;
   const int w = threadIdx.x >> 6, wr = (BM / 2) * (w >> 1), wc = (BN / 2) * (w & 1);
   f4 acc[TI][TJ];
@@ -325,6 +333,44 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(int N, int Mo, int Ki, c
         if (row < Mo) out[col < Ki ? offw + (size_t)row * Ki + col : offb + row] = acc[i][j][q];
       }
     }
+}
+
+__global__ __launch_bounds__(256) void mlp_wgrad_kernel(int N, int Mo, int Ki, const float* __restrict__ dZ,
+                                                        const float* __restrict__ H, const float* __restrict__ mean,
+                                                        const float* __restrict__ istd, int rows_per_split,
+                                                        float* __restrict__ part, int P, int offw, int offb) {
+  __shared__ float As[BM * LDP], Bs[BN * LDP];
+  wgrad_tile(blockIdx.x, blockIdx.y, blockIdx.z, As, Bs, N, Mo, Ki, dZ, H, mean, istd, rows_per_split, part, P, offw,
+             offb);
+}
+
+// Several independent layer problems in one launch (duck_mlp_group): the learner's GEMMs are short
+// chains of dependent memory round trips (a few reduction chunks each), so two or four of them
+// side by side take about as long as one; the policy's and the value network's layers at the same
+// depth, forward and backward, share a launch. A workgroup finds its problem by the tile prefix sums.
+struct MlpGroupArgs {
+  int n;
+  int start[DUCK_MLP_GROUP_MAX + 1];
+  int gx[DUCK_MLP_GROUP_MAX], gy[DUCK_MLP_GROUP_MAX], rps[DUCK_MLP_GROUP_MAX];
+  duck_mlp_problem p[DUCK_MLP_GROUP_MAX];
+};
+__global__ __launch_bounds__(256) void mlp_group_kernel(MlpGroupArgs g) {
+  __shared__ float As[BM * LDP], Bs[BN * LDP];
+  const int b = blockIdx.x;
+  int q = 0;
+#pragma unroll
+  for (int k = 1; k < DUCK_MLP_GROUP_MAX; k++) q += (k < g.n && b >= g.start[k]) ? 1 : 0;
+  const duck_mlp_problem& p = g.p[q];
+  const int t = b - g.start[q], gx = g.gx[q], gy = g.gy[q];
+  const int bz = t / (gx * gy), rem = t - bz * gx * gy, by = rem / gx, bx = rem - by * gx;
+  switch (p.kind) {
+    case 0: gemm_tile<0>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, p.mean, p.istd); break;
+    case 1: gemm_tile<1>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, p.mean, p.istd); break;
+    case 2: gemm_tile<2>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, nullptr, nullptr); break;
+    default:
+      wgrad_tile(bx, by, bz, As, Bs, p.N, p.M, p.R, p.A, p.W, p.mean, p.istd, g.rps[q], p.partial, p.P, p.off_w,
+                 p.off_b);
+  }
 }
 
 // grad[i] = sum_s part[s * P + i], s in order (deterministic)
@@ -477,6 +523,47 @@ extern "C" int duck_mlp_wgrad(int N, int M, int K, const float* dZ, const float*
   const dim3 grid((M + BM - 1) / BM, (K + 1 + BN - 1) / BN, splits);  // K + 1: the bias column
   hipLaunchKernelGGL(mlp_wgrad_kernel, grid, dim3(256), 0, (hipStream_t)stream, N, M, K, dZ, H, mean, istd, rps,
                      partial, P, off_w, off_b);
+  HIPCHECK(hipGetLastError());
+  return DUCK_OK;
+}
+
+extern "C" int duck_mlp_group(int n, const duck_mlp_problem* probs, void* stream) {
+  if (n < 0 || n > DUCK_MLP_GROUP_MAX) return duck_fail(DUCK_EINVAL, "duck_mlp_group: 0 .. DUCK_MLP_GROUP_MAX problems");
+  if (n == 0) return DUCK_OK;
+  if (!probs) return duck_fail(DUCK_EINVAL, "duck_mlp_group: null pointer");
+  MlpGroupArgs g;
+  memset(&g, 0, sizeof(g));
+  g.n = n;
+  long long tot = 0;
+  for (int k = 0; k < n; k++) {
+    const duck_mlp_problem& p = probs[k];
+    g.p[k] = p;
+    g.start[k] = (int)tot;
+    if (p.kind >= 0 && p.kind <= 2) {  // the checks of duck_mlp_gemm
+      if (p.N < 0 || p.R <= 0 || p.M <= 0) return duck_fail(DUCK_EINVAL, "duck_mlp_group: bad gemm size");
+      if (!p.A || !p.W || !p.Y || (p.kind == 1 && !p.Y2) || (p.kind == 2 && !p.aux) || (!p.mean) != (!p.istd) ||
+          (p.kind == 2 && p.mean))
+        return duck_fail(DUCK_EINVAL, "duck_mlp_group: bad gemm operands");
+      g.gx[k] = (p.N + BM - 1) / BM;
+      g.gy[k] = (p.M + BN - 1) / BN;
+      tot += (long long)g.gx[k] * g.gy[k];
+    } else if (p.kind == 3) {  // the checks of duck_mlp_wgrad (R = K inputs, M outputs)
+      if (p.N <= 0 || p.M <= 0 || p.R <= 0 || p.splits <= 0) return duck_fail(DUCK_EINVAL, "duck_mlp_group: bad wgrad size");
+      if (!p.A || !p.W || !p.partial || (!p.mean) != (!p.istd)) return duck_fail(DUCK_EINVAL, "duck_mlp_group: null pointer");
+      if (p.off_w < 0 || p.off_b < 0 || (long long)p.off_w + (long long)p.M * p.R > p.P || p.off_b + p.M > p.P)
+        return duck_fail(DUCK_EINVAL, "duck_mlp_group: offsets outside the parameter vector");
+      g.gx[k] = (p.M + BM - 1) / BM;
+      g.gy[k] = (p.R + 1 + BN - 1) / BN;
+      g.rps[k] = (p.N + p.splits - 1) / p.splits;
+      tot += (long long)g.gx[k] * g.gy[k] * p.splits;
+    } else {
+      return duck_fail(DUCK_EINVAL, "duck_mlp_group: kind must be 0, 1, 2 or 3");
+    }
+  }
+  g.start[n] = (int)tot;
+  for (int k = n; k <= DUCK_MLP_GROUP_MAX; k++) g.start[k] = (int)tot;
+  if (tot == 0) return DUCK_OK;
+  hipLaunchKernelGGL(mlp_group_kernel, dim3((unsigned)tot), dim3(256), 0, (hipStream_t)stream, g);
   HIPCHECK(hipGetLastError());
   return DUCK_OK;
 }

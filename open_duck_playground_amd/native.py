@@ -24,7 +24,15 @@ EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get"
            "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae", "duck_ppo_loss",
            "duck_ppo_loss_out_size", "duck_mlp_gemm", "duck_mlp_wgrad", "duck_mlp_wgrad_reduce",
            "duck_policy_sample", "duck_clip_adam", "duck_clip_adam_scratch_size", "duck_set_step_mode",
-           "duck_step_kernel_for", "duck_debug_lat_timeouts", "duck_gather_columns"]
+           "duck_step_kernel_for", "duck_debug_lat_timeouts", "duck_gather_columns", "duck_mlp_group"]
+
+
+class DuckMlpProblem(C.Structure):
+    """include/duck_ppo.h duck_mlp_problem"""
+    _fields_ = [("kind", C.c_int), ("N", C.c_int), ("R", C.c_int), ("M", C.c_int),
+                ("A", C.c_void_p), ("W", C.c_void_p), ("bias", C.c_void_p), ("aux", C.c_void_p),
+                ("Y", C.c_void_p), ("Y2", C.c_void_p), ("mean", C.c_void_p), ("istd", C.c_void_p),
+                ("splits", C.c_int), ("P", C.c_int), ("off_w", C.c_int), ("off_b", C.c_int), ("partial", C.c_void_p)]
 
 
 class DuckGatherField(C.Structure):
@@ -254,6 +262,8 @@ def lib(path: str = None):
             L.duck_ppo_loss.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_int,
                                         vp, vp, vp, vp]
             L.duck_ppo_loss_out_size.argtypes = [C.c_int]
+        if hasattr(L, "duck_mlp_group"):
+            L.duck_mlp_group.argtypes = [C.c_int, C.POINTER(DuckMlpProblem), vp]
         if hasattr(L, "duck_gather_columns"):
             L.duck_gather_columns.argtypes = [C.c_int, C.POINTER(DuckGatherField), vp, C.c_int, vp]
         if hasattr(L, "duck_mlp_gemm"):

@@ -404,6 +404,40 @@ class FusedGrad:
                 inp = b["H"][i]
         return b["out"]
 
+    # grouped launches (duck_mlp_group): the policy's and the value network's layers at one depth share a
+    # launch, forward and backward (4 + 4 launches per minibatch instead of 8 + 14)
+    def _prob_fwd(self, layers, b, x, norm, n, i):
+        from .native import DuckMlpProblem
+        m = layers[i]
+        last = i == len(layers) - 1
+        inp = x if i == 0 else b["H"][i - 1]
+        mean, istd = (norm.mean32.data_ptr(), norm.istd32.data_ptr()) if (i == 0 and norm is not None) else (None, None)
+        return DuckMlpProblem(0 if last else 1, n, m.in_features, m.out_features, inp.data_ptr(), m.weight.data_ptr(),
+                              m.bias.data_ptr(), None, (b["out"] if last else b["Z"][i]).data_ptr(),
+                              None if last else b["H"][i].data_ptr(), mean, istd, 0, 0, 0, 0, None)
+
+    def _probs_bwd(self, layers, b, x, norm, dout, n, i):
+        from .native import DuckMlpProblem
+        m = layers[i]
+        d = dout if i == len(layers) - 1 else b["dZ"][i]
+        h = x if i == 0 else b["H"][i - 1]
+        mean, istd = (norm.mean32.data_ptr(), norm.istd32.data_ptr()) if (i == 0 and norm is not None) else (None, None)
+        tiles = -(-m.out_features // 64) * -(-(m.in_features + 1) // 32)
+        splits = max(1, min(self.SPLITS, -(-768 // tiles), n // 64))
+        out = [DuckMlpProblem(3, n, m.in_features, m.out_features, d.data_ptr(), h.data_ptr(), None, None, None, None,
+                              mean, istd, splits, self.P, self.off[id(m.weight)], self.off[id(m.bias)],
+                              self.part.data_ptr())]
+        if i > 0:
+            out.append(DuckMlpProblem(2, n, m.out_features, m.in_features, d.data_ptr(), m.weight.data_ptr(), None,
+                                      b["Z"][i - 1].data_ptr(), b["dZ"][i - 1].data_ptr(), None, None, None,
+                                      0, 0, 0, 0, None))
+        return out
+
+    def _group(self, probs, stream):
+        from .native import DuckMlpProblem, check
+        arr = (DuckMlpProblem * len(probs))(*probs)
+        check(self.lib.duck_mlp_group(len(probs), arr, stream))
+
     def _backward(self, layers, b, x, norm, dout, n, stream):
         from .native import check
         d = dout
@@ -474,8 +508,15 @@ class FusedGrad:
         on, pn = (net.obs_norm, net.priv_norm) if net.normalize else (None, None)
         obs = mb["obs"].reshape(N, -1)
         xv = mb["xv"] if "xv" in mb else torch.cat([mb["priv"].reshape(N, -1), mb["next_priv"][-1]], 0)
-        logits = self._forward(self.pol, self.bp, obs, on, N, st)
-        v_all = self._forward(self.val, self.bv, xv, pn, self.Nv, st).view(-1)
+        grouped = hasattr(self.lib, "duck_mlp_group") and len(self.pol) == len(self.val)
+        if grouped:
+            for i in range(len(self.pol)):
+                self._group([self._prob_fwd(self.pol, self.bp, obs, on, N, i),
+                             self._prob_fwd(self.val, self.bv, xv, pn, self.Nv, i)], st)
+            logits, v_all = self.bp["out"], self.bv["out"].view(-1)
+        else:
+            logits = self._forward(self.pol, self.bp, obs, on, N, st)
+            v_all = self._forward(self.val, self.bv, xv, pn, self.Nv, st).view(-1)
         baseline, bootstrap = v_all[:N].view(T, B), v_all[N:]
         truncation = mb["truncation"]
         termination = mb["done"] * (1.0 - truncation)
@@ -488,8 +529,13 @@ class FusedGrad:
                                      vs.data_ptr(), baseline.data_ptr(), eps.data_ptr(), float(cfg.clipping_epsilon),
                                      float(cfg.entropy_cost), int(bool(cfg.normalize_advantage)),
                                      self.loss_out.data_ptr(), self.g_lg.data_ptr(), self.d_val.data_ptr(), st))
-        self._backward(self.pol, self.bp, obs, on, self.g_lg, N, st)
-        self._backward(self.val, self.bv, xv, pn, self.d_val, self.Nv, st)
+        if grouped:
+            for i in range(len(self.pol) - 1, -1, -1):
+                self._group(self._probs_bwd(self.pol, self.bp, obs, on, self.g_lg, N, i) +
+                            self._probs_bwd(self.val, self.bv, xv, pn, self.d_val, self.Nv, i), st)
+        else:
+            self._backward(self.pol, self.bp, obs, on, self.g_lg, N, st)
+            self._backward(self.val, self.bv, xv, pn, self.d_val, self.Nv, st)
         check(self.lib.duck_mlp_wgrad_reduce(self.P, self.SPLITS, self.part.data_ptr(), self.flat.data_ptr(), st))
         o = self.loss_out
         return {"loss": o[0], "policy_loss": o[1], "v_loss": o[2], "entropy": o[3]}

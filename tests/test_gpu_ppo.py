@@ -274,3 +274,46 @@ def test_gather_columns_matches_index_select(gpu):
         assert torch.equal(dst[k], torch.index_select(src[k], 1, idx)), k
     assert torch.equal(dst["np"], torch.index_select(src["np"][-1], 0, idx))
     assert lib().duck_gather_columns(9, arr, idx.data_ptr(), m, None) < 0
+
+
+def test_mlp_group_equals_separate_launches(gpu):
+    """duck_mlp_group (several layer problems in one launch) writes what the separate duck_mlp_gemm /
+    duck_mlp_wgrad calls write, bit for bit: a forward layer with the normaliser, a data gradient and a
+    weight gradient side by side."""
+    from open_duck_playground_amd.native import DuckMlpProblem, check, lib
+    L = lib()
+    g = torch.Generator(device=gpu)
+    g.manual_seed(5)
+    st = torch.cuda.current_stream().cuda_stream
+    N, R, M = 700, 101, 96
+    x = torch.randn(N, R, device=gpu, generator=g)
+    W = torch.randn(M, R, device=gpu, generator=g) * 0.1
+    bias = torch.randn(M, device=gpu, generator=g)
+    mean, istd = torch.randn(R, device=gpu, generator=g), torch.rand(R, device=gpu, generator=g) + 0.5
+    dZ = torch.randn(N, M, device=gpu, generator=g)
+    Zp = torch.randn(N, R, device=gpu, generator=g)
+    P = M * R + M + 16
+    outs = {}
+    for how in ("separate", "group"):
+        Y, Y2, dX = torch.empty(N, M, device=gpu), torch.empty(N, M, device=gpu), torch.empty(N, R, device=gpu)
+        part = torch.zeros(3 * P, device=gpu)
+        if how == "separate":
+            check(L.duck_mlp_gemm(1, N, R, M, x.data_ptr(), W.data_ptr(), bias.data_ptr(), None, Y.data_ptr(),
+                                  Y2.data_ptr(), mean.data_ptr(), istd.data_ptr(), st))
+            check(L.duck_mlp_gemm(2, N, M, R, dZ.data_ptr(), W.data_ptr(), None, Zp.data_ptr(), dX.data_ptr(),
+                                  None, None, None, st))
+            check(L.duck_mlp_wgrad(N, M, R, dZ.data_ptr(), x.data_ptr(), mean.data_ptr(), istd.data_ptr(), 3,
+                                   part.data_ptr(), P, M, 0, st))
+        else:
+            probs = [DuckMlpProblem(1, N, R, M, x.data_ptr(), W.data_ptr(), bias.data_ptr(), None, Y.data_ptr(),
+                                    Y2.data_ptr(), mean.data_ptr(), istd.data_ptr(), 0, 0, 0, 0, None),
+                     DuckMlpProblem(2, N, M, R, dZ.data_ptr(), W.data_ptr(), None, Zp.data_ptr(), dX.data_ptr(),
+                                    None, None, None, 0, 0, 0, 0, None),
+                     DuckMlpProblem(3, N, R, M, dZ.data_ptr(), x.data_ptr(), None, None, None, None,
+                                    mean.data_ptr(), istd.data_ptr(), 3, P, M, 0, part.data_ptr())]
+            check(L.duck_mlp_group(3, (DuckMlpProblem * 3)(*probs), st))
+        torch.cuda.synchronize()
+        outs[how] = (Y, Y2, dX, part)
+    for a, b in zip(outs["separate"], outs["group"]):
+        assert torch.equal(a, b)
+    assert L.duck_mlp_group(5, (DuckMlpProblem * 5)(), st) < 0
