@@ -196,7 +196,9 @@ struct TLay {
   // the subtree pass's lanes that a latency-mode wave does not own write here (forces / inertias)
   static constexpr int XDUM0 = LAT ? XCIN + 10 * Md::NB : 0, XDUM1 = LAT ? XDUM0 + 10 * Md::NB : 0;
   static constexpr int XSIL = LAT ? ((XDUM1 + 6 * Md::NB + 3) & ~3) : ((Ly::CIN + 3) & ~3);
-  static constexpr int USED = LAT ? XSIL + (Md::FLOOR_TYPE == 1 ? 2 * HF_SLSZ : 0) : USED0;
+  // the speculative Newton direction of wave 3 (latency mode): NV floats, then the team's valid flag
+  static constexpr int XDIR = LAT ? ((XSIL + (Md::FLOOR_TYPE == 1 ? 2 * HF_SLSZ : 0) + 3) & ~3) : 0;
+  static constexpr int USED = LAT ? XDIR + Md::NV + 4 : USED0;
   static constexpr int STRIDE = ((USED + 15) / 32) * 32 + 16;  // = 16 (mod 32), >= USED
   static constexpr int NWG = LAT ? LAT_WG : TEAM_WG;          // envs per workgroup
   static_assert(STRIDE >= USED && STRIDE % 32 == 16, "stride");
@@ -220,7 +222,7 @@ struct TLay {
   static constexpr int ES_FLOATS = ESTRIDE * NWG;
   // latency mode: the cross-wave event counters, one 16-B word group each, in front of the slices'
   // end of LDS (LDS_FLOATS counts them)
-  static constexpr int NEV = LAT ? 8 : 0;
+  static constexpr int NEV = LAT ? 10 : 0;
   static constexpr size_t LDS_MAX = 160 * 1024 / 4 - 4 * NEV;
   // LDS priority: model blob (read every substep), then the hot state (read once per env-step)
   static constexpr bool TAB_LDS = (size_t)(TAB + Md::NBLOB) <= LDS_MAX;
@@ -1181,7 +1183,7 @@ struct TPhys {
   // FF = false: the common case, tree-sparse H (returns false, nothing written, when foot/foot
   // contact rows are active). FF = true: those rows included — their Jacobian J_geom2 - J_geom1
   // couples the two legs, so H is assembled densely and factored by factor_solve_dense.
-  template <bool FF>
+  template <bool FF, int OUT = Ly::SRCH>
   static DK bool newton_fused(LP L, int lane, const float (*Mc)[NV]) {
     STAGE_T0();
     if constexpr (!FF) {
@@ -1350,7 +1352,7 @@ struct TPhys {
 #pragma unroll
     for (int s = 0; s < NC; s++) {
       const int c = TEAM * s + lane;
-      if (c < NV) L[Ly::SRCH + c] = -g[s];
+      if (c < NV) L[OUT + c] = -g[s];
     }
     TSYNC();
     return true;
@@ -2779,7 +2781,7 @@ struct TPhys {
       }
     }
   }
-  static DK float warm_start_b(LP L, int lane, float cwp) {
+  static DK float warm_start_b(LP L, int lane, float cwp, bool& warm) {
     float ss, s2;
     spatial2(L, lane, Ly::QSM, -1, ss, s2);
     TSYNC();
@@ -2817,7 +2819,8 @@ struct TPhys {
     const float gw = tsum(gwp);
     const float cw = gw + tsum(cwp), cs = tsum(csp);
     float g0;
-    if (cw < cs) {
+    warm = cw < cs;
+    if (warm) {
       for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] = L[Ly::WARM + i];
       g0 = gw;
     } else {
@@ -2899,12 +2902,22 @@ struct TPhys {
     return g0;
   }
   // Md::iterations Newton steps from the start in QACC / MA / JA (Gauss cost g0 there)
-  static DK void newton(LP L, int lane, float* scratch, int stride, const float (*Mc)[NV], float g0) {
+  // pre_dir (latency mode): the first direction is already in TL::XDIR (wave 3's, from the same inputs);
+  // used when every team of the wave has one, else the wave computes it (the same values for those teams)
+  static DK void newton(LP L, int lane, float* scratch, int stride, const float (*Mc)[NV], float g0,
+                        bool pre_dir = false) {
     STAGE_T0();
     (void)scratch;
     (void)stride;
     for (int newton_it = 0;;) {
-    const bool sparse_ok = newton_fused<false>(L, lane, Mc);
+    bool sparse_ok;
+    if (LAT && newton_it == 0 && __ballot(!pre_dir) == 0ull) {
+      for (int i = lane; i < NV; i += TEAM) L[Ly::SRCH + i] = L[TL::XDIR + i];
+      TSYNC();
+      sparse_ok = true;
+    } else {
+      sparse_ok = newton_fused<false>(L, lane, Mc);
+    }
     STAGE_MARK(10);
     if (sparse_ok) {
       STAGE_MARK(11);
@@ -3250,7 +3263,7 @@ struct TPhys {
   // grow within a launch, so no event is reset between substeps. A spin is bounded (~40 ms, far
   // beyond a substep) so that a broken schedule ends the launch instead of hanging the device;
   // g_lat_timeouts counts such exits (tests read it: it must stay 0).
-  enum { EV_KIN = 0, EV_VEL = 1, EV_FSM = 2, EV_ROWS = 3, EV_EULER = 4, EV_M = 5, EV_QSM = 6 };
+  enum { EV_KIN = 0, EV_VEL = 1, EV_FSM = 2, EV_ROWS = 3, EV_EULER = 4, EV_M = 5, EV_QSM = 6, EV_WA = 7, EV_DIR = 8 };
   static DK lds_int* ev_ptr(int k) {
     extern __shared__ float lds_dyn[];
     return (lds_int*)(lds_dyn + TL::EV) + 4 * k;
@@ -3306,12 +3319,22 @@ struct TPhys {
       ev_wait(EV_ROWS, s + 1);
       LAT_T(13, s);
       warm_start_a1(L, lane, SL, SR, cwp);
+      ev_signal(EV_WA, s + 1);
       LAT_T(14, s);
       ev_wait(EV_QSM, s + 1);
       LAT_T(15, s);
-      const float g0 = warm_start_b(L, lane, cwp);
+      bool warm;
+      const float g0 = warm_start_b(L, lane, cwp, warm);
       LAT_T(16, s);
-      newton(L, lane, scratch, sstride, Mc, g0);
+      // every team starts from qacc_warmstart (the common case): wave 3 has computed the Newton direction
+      // there meanwhile; otherwise this wave computes it (no wait)
+      bool pre = false;
+      if (__ballot(!warm) == 0ull) {
+        ev_wait(EV_DIR, s + 1);
+        pre = L[TL::XDIR + NV] != 0.0f;
+      }
+      LAT_T(19, s);
+      newton(L, lane, scratch, sstride, Mc, g0, pre);
       LAT_T(17, s);
     }
     if (want_out) sensors(L, lane);
@@ -3350,5 +3373,14 @@ struct TPhys {
     smooth_solve(L, lane, F);
     ev_signal(EV_QSM, s + 1);
     LAT_T(33, s);
+    // the Newton direction at qacc_warmstart, speculatively (wave 1 uses it when the warm start wins
+    // everywhere in the wave): the rows' values there and M qacc_warmstart come from wave 1's warm start
+    ev_wait(EV_WA, s + 1);
+    LAT_T(34, s);
+    const bool ok = newton_fused<false, TL::XDIR>(L, lane, Mc);
+    if (lane == 0) L[TL::XDIR + NV] = ok ? 1.0f : 0.0f;
+    TSYNC();
+    ev_signal(EV_DIR, s + 1);
+    LAT_T(35, s);
   }
 };

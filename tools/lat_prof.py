@@ -21,7 +21,8 @@ NAMES = {0: "w0 start (Euler of s-1 seen)", 1: "w0 kinematics+com_pos done", 2: 
          13: "w1 rows seen", 14: "w1 warm start (qacc_warmstart) done", 15: "w1 qacc_smooth seen",
          16: "w1 warm start done", 17: "w1 Newton + line search done", 18: "w1 Euler done",
          20: "w2 com_pos seen", 21: "w2 collision done", 22: "w2 rne velocities seen", 23: "w2 rows done",
-         30: "w3 crb seen", 31: "w3 M factored", 32: "w3 qfrc_smooth seen", 33: "w3 qacc_smooth done"}
+         30: "w3 crb seen", 31: "w3 M factored", 32: "w3 qfrc_smooth seen", 33: "w3 qacc_smooth done",
+         34: "w3 warm start's rows seen", 35: "w3 speculative Newton direction done", 19: "w1 direction seen"}
 LAUNCH = {40: "kernel start", 41: "model blob in LDS", 42: "hot state staged", 43: "w0 env code before the substeps done",
           44: "w0 last Euler seen", 45: "w0 env code after the substeps done", 46: "final barrier"}
 NSTAGE = 56
