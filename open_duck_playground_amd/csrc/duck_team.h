@@ -2747,9 +2747,8 @@ struct TPhys {
     {
       float xw[NC];
       lane_vec(L, lane, Ly::WARM, xw);
-      mul_cols(L, lane, Mc, xw, Ly::MA);
+      mul_cols(L, lane, Mc, xw, Ly::MA);  // (MA is read after the next team sync)
     }
-    TSYNC();
     sp_bcast(sw, SL, SR);
   }
   static DK void warm_start_a1(LP L, int lane, const float* SL, const float* SR, float& cwp) {
