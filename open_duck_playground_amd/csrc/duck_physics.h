@@ -50,6 +50,19 @@ static __device__ unsigned long long g_stage_wg[DUCK_NSTAGE * 256];
     _c0 = _c1;                                                                    \
     (void)_t0;                                                                    \
   } while (0)
+#elif defined(DUCK_LAT_PROF)
+// latency-kernel builds (tools/lat_prof.py): each stage's cycles summed over the launch in workgroup 0
+// (lane 0 of the wave that runs it; in the latency kernel every stage runs on one wave) into
+// g_stage_cycles[DUCK_NSTAGE + 64 + k]; the waits between stages are outside every stage
+#define STAGE_T0() unsigned long long _c0 = clock64()
+#define STAGE_RESET() (_c0 = clock64())
+#define STAGE_MARK(k)                                                                  \
+  do {                                                                                 \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                 \
+    const unsigned long long _c1 = clock64();                                          \
+    if (blockIdx.x == 0 && ((int)threadIdx.x & 63) == 0) g_stage_cycles[DUCK_NSTAGE + 64 + (k)] += _c1 - _c0; \
+    _c0 = _c1;                                                                         \
+  } while (0)
 #else
 #define STAGE_T0() \
   do {             \

@@ -9,6 +9,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -44,12 +45,16 @@ def main():
     g.manual_seed(1)
     buf = (C.c_ulonglong * (NSTAGE + 3 * 1024))()
     rows = []
+    stage = np.zeros(64)
+    nl = 0
     for t in range(a.steps):
         st = env.step(st, torch.rand(a.envs, 14, device=dev, generator=g) * 2 - 1, inplace=True)
         torch.cuda.synchronize()
         if env._lib.duck_debug_stage_cycles(env._sim, buf, 1) != 0:
             raise SystemExit("not a DUCK_LAT_PROF build")
         if t >= 10:
+            stage += np.array([buf[NSTAGE + 64 + k] for k in range(64)], dtype=np.float64)
+            nl += 1
             v = np.array([buf[NSTAGE + k] for k in range(48)], dtype=np.float64)
             v[:40] -= v[0]
             v[40:] -= v[40]
@@ -62,6 +67,14 @@ def main():
     for k in sorted(NAMES, key=lambda k: r[k]):
         print(f"{r[k]:9.0f}  {NAMES[k]}")
     print(f"substep (w0 start -> w1 Euler): {r[18]:.0f} cycles")
+    # per-stage cycles (STAGE_MARK sums, workgroup 0), per substep
+    from stage_prof import ENV, SUB, TOP  # noqa: E402
+    names = {**TOP, **SUB, **ENV}
+    per = stage / max(nl, 1) / env.n_substeps
+    print("stage cycles per substep (marks from each stage function's start):")
+    for k in np.argsort(-per):
+        if per[k] > 0 and k in names:
+            print(f"{per[k]:9.0f}  {names[k]}")
 
 
 if __name__ == "__main__":
