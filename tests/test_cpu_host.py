@@ -244,3 +244,25 @@ def test_isa_gate_fails_closed(tmp_path):
     subprocess.check_call(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)])
     with pytest.raises(native.DuckError):
         native.isa_exec_faults(str(so))
+
+
+def test_round4_entry_points_refuse_bad_arguments():
+    """Host-side checks of the round-4 C-ABI entries (no GPU call is reached): the grouped MLP launch,
+    the minibatch gather and the step-mode switch refuse malformed arguments with a message."""
+    import ctypes as C
+    from open_duck_playground_amd.native import DuckGatherField, DuckMlpProblem
+    lib = native.lib()
+    assert lib.duck_mlp_group(5, (DuckMlpProblem * 5)(), None) < 0
+    assert b"problems" in lib.duck_last_error()
+    bad = (DuckMlpProblem * 1)(DuckMlpProblem(7, 8, 8, 8))
+    assert lib.duck_mlp_group(1, bad, None) < 0 and b"kind" in lib.duck_last_error()
+    nul = (DuckMlpProblem * 1)(DuckMlpProblem(1, 8, 8, 8))  # operands missing
+    assert lib.duck_mlp_group(1, nul, None) < 0 and b"operands" in lib.duck_last_error()
+    off = (DuckMlpProblem * 1)(DuckMlpProblem(3, 64, 8, 8, 1, 1, None, None, None, None, None, None, 2, 10, 0, 0, 1))
+    assert lib.duck_mlp_group(1, off, None) < 0 and b"offsets" in lib.duck_last_error()
+    assert lib.duck_mlp_group(0, None, None) == 0
+    assert lib.duck_gather_columns(9, (DuckGatherField * 9)(), C.c_void_p(1), 4, None) < 0
+    f = (DuckGatherField * 1)(DuckGatherField(None, None, 2, 4, 3))
+    assert lib.duck_gather_columns(1, f, C.c_void_p(1), 4, None) < 0 and b"bad field" in lib.duck_last_error()
+    assert lib.duck_set_step_mode(None, 0) < 0
+    assert lib.duck_step_kernel_for(None, 4) < 0
