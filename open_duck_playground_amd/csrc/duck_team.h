@@ -1541,6 +1541,14 @@ struct TPhys {
   // the contact point (oracle: the penetration-weighted centroid of the vertices of each shape
   // inside the other, or the midpoint of the support features). Writes (depth, normal, point)
   // over the entry's first 8 floats; depth -1 when separated.
+#ifdef DUCK_DOUBLE
+  // (measurement builds: values the compiler must treat as changed, so that a doubled stage is recomputed)
+  template <int N>
+  static DK void launder(float* x) {
+#pragma unroll
+    for (int i = 0; i < N; i++) asm volatile("" : "+v"(x[i]));
+  }
+#endif
   static DK void hf_exec(lds_float* E, LP L, int tw) {
     STAGE_T0();
     constexpr int NH = Md::NHV, NF = Md::NHF, NE = Md::NHE;
@@ -1591,6 +1599,9 @@ struct TPhys {
       for (int a = 0; a < 3; a++) mu[a] = b ? u[a] : mu[a];
     };
     // vertical-edge pairs: the prism's support along w is its vertical edge at vertex kk
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 15
+    for (int rep_ = 0; rep_ < 2; rep_++)
+#endif
     {
       const lds_float* SL = L + ((foot >> 1) - tw) * TL::STRIDE + HF_CINQ + (foot & 1) * HF_SLSZ;
       const int n = ((const lds_int*)SL)[0];
@@ -1608,7 +1619,19 @@ struct TPhys {
     // CBA DBA < 0, ADC BDC < 0 and CBA BDC > 0 (C = -n_a, D = -n_b, B x A = sm_k x ntm: CBA =
     // -phi_a), all three products negative: the sign bit of their maximum, bit 3 e + k of pm
     unsigned long long pm[3] = {0ull, 0ull, 0ull};
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 12
+    for (int rep_ = 0; rep_ < 2; rep_++)
+#endif
     {
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 12
+      float ntm_l[3] = {ntm[0], ntm[1], ntm[2]}, sm_l[3][3];
+      for (int k = 0; k < 3; k++)
+        for (int a = 0; a < 3; a++) sm_l[k][a] = sm[k][a];
+      launder<3>(ntm_l);
+      launder<9>(&sm_l[0][0]);
+      const auto& ntm = ntm_l;
+      const auto& sm = sm_l;
+#endif
       float hx[3][3];
       for (int k = 0; k < 3; k++) cross3(hx[k], sm[k], ntm);
       // (one prism edge at a time: 30 face products live, not 90)
@@ -1646,6 +1669,11 @@ struct TPhys {
     }
 #endif
     // pass 2: each crossing pair's overlap along ev x em (lowest pair first)
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 11
+    const unsigned long long pm_s[3] = {pm[0], pm[1], pm[2]};
+    for (int rep_ = 0; rep_ < 2; rep_++) {
+      for (int w = 0; w < 3; w++) pm[w] = pm_s[w];
+#endif
     while (pm[0] | pm[1] | pm[2]) {
 #ifdef DUCK_STAGE_PROF
       if (threadIdx.x < 64 && (int)threadIdx.x == __ffsll((long long)__ballot(1)) - 1) STAGE_ADD(48, 1ull);
@@ -1672,6 +1700,9 @@ struct TPhys {
       const float ov = u2 >= 1e-12f * ev4.w * dot3(em, em) ? sg * (dot3(u, tm) - dot3(u, v0)) : 1e30f;
       take(ov, HF_PRIO_T + p, un);
     }
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 11
+    }
+#endif
     STAGE_MARK(47);
     if (!(mo > 0.0f)) {
       E4[0] = f4v{-1.0f, 0.0f, 0.0f, 0.0f};
@@ -1688,6 +1719,23 @@ struct TPhys {
     }
     // the contact point: hull vertices inside the prism and prism top vertices inside the hull,
     // weighted by their penetration
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 13
+    for (int rep_ = 0; rep_ < 2; rep_++) {
+      float Tm_l[3][3], sm_l[3][3], ntm_l[3] = {ntm[0], ntm[1], ntm[2]}, zc_l[3] = {zc[0], zc[1], zc[2]};
+      float mu_l[3] = {mu[0], mu[1], mu[2]};
+      for (int k = 0; k < 3; k++)
+        for (int a = 0; a < 3; a++) Tm_l[k][a] = Tm[k][a], sm_l[k][a] = sm[k][a];
+      launder<9>(&Tm_l[0][0]);
+      launder<9>(&sm_l[0][0]);
+      launder<3>(ntm_l);
+      launder<3>(zc_l);
+      launder<3>(mu_l);
+      const auto& Tm = Tm_l;
+      const auto& sm = sm_l;
+      const auto& ntm = ntm_l;
+      const auto& zc = zc_l;
+      const auto& mu = mu_l;
+#endif
     const float ptop = dot3(ntm, Tm[0]);
     const float smt[3] = {dot3(sm[0], Tm[0]), dot3(sm[1], Tm[1]), dot3(sm[2], Tm[2])};
     float W = 0.0f, Cx[3] = {0.0f, 0.0f, 0.0f};
@@ -1760,6 +1808,9 @@ struct TPhys {
     }
     E4[0] = f4v{mo, mu[0], mu[1], mu[2]};
     E4[1] = f4v{pos[0], pos[1], pos[2], 0.0f};
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 13
+    }
+#endif
   }
 
   static DK void collide_hfield(LP L, int lane, const float* hf) {
@@ -1884,6 +1935,12 @@ struct TPhys {
     float smo[PPL], szt[PPL][3];
     int smp[PPL];
     unsigned surv = 0;
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 14
+    for (int rep_ = 0; rep_ < 2; rep_++) {
+      launder<9>(R);
+      launder<GPL>(zg);
+      launder<3>(lo);
+#endif
 #pragma unroll
     for (int j = 0; j < PPL; j++) {
       const int q = sub + 8 * j;
@@ -1934,6 +1991,9 @@ struct TPhys {
       smp[j] = mp;
       for (int k = 0; k < 3; k++) szt[j][k] = T[k][2];
     }
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 14
+    }
+#endif
     // this foot's silhouette edges (the hull's edges whose faces straddle the field's horizontal
     // plane: the only ones whose Gauss arc crosses a prism's vertical-edge arc), compacted in edge
     // order into the env slice's composite-inertia storage (dead after crb()): the direction w in
