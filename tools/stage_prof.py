@@ -41,15 +41,16 @@ def main():
     g.manual_seed(1234)
     pool = [torch.rand(n, env.action_size, device="cuda:0", generator=g) * 2 - 1 for _ in range(8)] if rand else \
         [torch.zeros(n, env.action_size, device="cuda:0")]
-    for i in range(20):
+    warm = next((int(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--warm=")), 20)
+    for i in range(warm):
         st = env.step(st, pool[i % len(pool)], inplace=True)
     torch.cuda.synchronize()
     buf = (C.c_ulonglong * (NSTAGE + 3 * 1024))()
     lib = native.lib()
     lib.duck_debug_stage_cycles(env._sim, buf, 1)
-    steps = 5
+    steps = next((int(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--steps=")), 5)
     for i in range(steps):
-        st = env.step(st, pool[i % len(pool)], inplace=True)
+        st = env.step(st, pool[(warm + i) % len(pool)], inplace=True)
     torch.cuda.synchronize()
     lib.duck_debug_stage_cycles(env._sim, buf, 1)
     nwg = (n + 15) // 16
