@@ -1591,6 +1591,22 @@ struct TPhys {
         em[a] = vsel(m0, Tm[1][a], vsel(m1, Tm[2][a], Tm[0][a])) - tm[a];
       }
     };
+    // the hull's faces (compile-time normals): the prism's lowest point along n_f, a bottom vertex
+    // where n_f leans up the field's z (priority 5 + f; mu is formed after the SAT for these)
+    {
+      const float hk[3] = {d4.w - base, d5.w - base, d6.w - base};
+      static_for<0, NF>([&](auto fI) {
+        constexpr int f = fI.value;
+        const float nz = fmaxf(nf_dot<f>(zc), 0.0f);
+        float pf = nf_dot<f>(Tm[0]) - hk[0] * nz;
+        pf = fminf(pf, nf_dot<f>(Tm[1]) - hk[1] * nz);
+        pf = fminf(pf, nf_dot<f>(Tm[2]) - hk[2] * nz);
+        const float ov = nf_off_minus<f>(pf);
+        const bool b = (ov < mo) | ((ov == mo) & (5 + f < mp));
+        mo = b ? ov : mo;
+        mp = b ? 5 + f : mp;
+      });
+    }
     float mu[3] = {0.0f, 0.0f, 0.0f};
     auto take = [&](float ov, int pr, const float* u) {
       const bool b = (ov < mo) | ((ov == mo) & (pr < mp));
@@ -1968,22 +1984,8 @@ struct TPhys {
       }
       mp = obot < mo ? 4 : mp;
       mo = fminf(mo, obot);
-      {
-        // the hull's faces (compile-time normals): the prism's lowest point along n_f, a bottom
-        // vertex where n_f leans up the field's z
-        float Tm[3][3], hk[3];
-        for (int k = 0; k < 3; k++) { mulmtv3(Tm[k], R, T[k]); hk[k] = T[k][2] - base; }
-        static_for<0, NF>([&](auto fI) {
-          constexpr int f = fI.value;
-          const float nz = fmaxf(nf_dot<f>(zc), 0.0f);
-          float pm = nf_dot<f>(Tm[0]) - hk[0] * nz;
-          pm = fminf(pm, nf_dot<f>(Tm[1]) - hk[1] * nz);
-          pm = fminf(pm, nf_dot<f>(Tm[2]) - hk[2] * nz);
-          const float ov = nf_off_minus<f>(pm);
-          mp = ov < mo ? 5 + f : mp;
-          mo = fminf(mo, ov);
-        });
-      }
+      // (the hull's 30 face axes are the survivors' first SAT step, hf_exec: per survivor lane once,
+      // instead of per screened prism slot -- they separate ≈ 0.6 prisms per foot-substep more)
       const bool high = !(T[0][2] < lo[2] && T[1][2] < lo[2] && T[2][2] < lo[2]);
       const bool ok = q < np && high && mo > 0.0f;
       surv |= half_bits(__ballot(ok), lane) << (8 * j);
@@ -2086,9 +2088,9 @@ struct TPhys {
           E4[1] = f4v{Tm[1][0], Tm[1][1], Tm[1][2], smo[j]};
           E4[2] = f4v{Tm[2][0], Tm[2][1], Tm[2][2], __int_as_float(smp[j])};
           E4[3] = f4v{ntm[0], ntm[1], ntm[2], __int_as_float(tri | (2 * tw + h) << 1)};
-          E4[4] = f4v{zc[0], zc[1], zc[2], 0.0f};
-          E4[5] = f4v{R[0], R[1], R[2], 0.0f};
-          E4[6] = f4v{R[3], R[4], R[5], 0.0f};
+          E4[4] = f4v{zc[0], zc[1], zc[2], szt[j][0]};
+          E4[5] = f4v{R[0], R[1], R[2], szt[j][1]};
+          E4[6] = f4v{R[3], R[4], R[5], szt[j][2]};
         }
       }
       TSYNC();

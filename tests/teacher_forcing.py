@@ -446,6 +446,8 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     "sat_tie": two separating axes of one height-field prism overlap within 1e-6 m (the kernel's fp32
     error bound on an overlap), and the oracle resolving such ties to the other axis -- the last one in
     the band (oracle_set_hf_tie_last) or the first (oracle_set_hf_tie_first) -- lands on the GPU's result;
+    "dup_selection": the same, around two prisms reporting one contact (the shared edge it lies on):
+    equal in fp64, a few ulp apart in fp32, so the 4-point selection's choice is decided below fp32;
     "onset_selection": the manifold chose other prism contacts around an onset-depth prism -- every GPU
     slot of the differing pairs is one of the oracle's own prism contacts (oracle_hfield_contacts) or
     at the onset depth, and the oracle continued from the GPU's slots lands on the GPU's result
@@ -505,10 +507,20 @@ def declared_difference(env, e: int, om, x: np.ndarray, g: np.ndarray, sub_tol: 
     if pair_differs.any() and _onset_selection(m, om, d, ga, pair_differs, onset) and \
             _state_rel(m, g, oracle_substep_with_contacts(om, x, ga)) <= sub_tol:
         return "onset_selection"
+    # the manifold's selection among duplicate prism contacts: two prisms that share the edge the
+    # contact lies on report the same contact, exactly equal in the oracle's fp64 and a few ulp apart
+    # in the kernel's fp32, so which slots the 4-point selection fills is decided below fp32
+    # resolution. Accepted on the same terms: (a) every active GPU slot of a differing pair is one of
+    # the oracle's own prism contacts, (b) the oracle's candidates of that pair hold such a duplicate
+    # (points within 1e-7 m, depths within 1e-9 m), (c) the oracle continued from the GPU's slots lands
+    # on the GPU's result
+    if pair_differs.any() and _onset_selection(m, om, d, ga, pair_differs, onset, dup=True) and \
+            _state_rel(m, g, oracle_substep_with_contacts(om, x, ga)) <= sub_tol:
+        return "dup_selection"
     return None
 
 
-def _onset_selection(m, om, d, ga, pair_differs, onset) -> bool:
+def _onset_selection(m, om, d, ga, pair_differs, onset, dup: bool = False) -> bool:
     import ctypes as C
     from tests.oracle_ffi import lib
     floor = m.id("geom", "floor")
@@ -525,6 +537,9 @@ def _onset_selection(m, om, d, ga, pair_differs, onset) -> bool:
                                          nrm.ctypes.data_as(C.POINTER(C.c_double)), pt.ctypes.data_as(C.POINTER(C.c_double)))
         dep, nrm, pt = dep[:k], nrm[:3 * k].reshape(k, 3), pt[:3 * k].reshape(k, 3)
         cand_onset = bool((dep <= onset).any())
+        if dup:  # condition (b) of "dup_selection": two of the oracle's candidates coincide
+            cand_onset = any(np.abs(pt[i] - pt[j]).max() <= 1e-7 and abs(dep[i] - dep[j]) <= 1e-9
+                             for i in range(k) for j in range(i + 1, k))
         slot_onset = False
         for sl in range(4 * p, 4 * p + 4):
             if gd[sl] >= 0:

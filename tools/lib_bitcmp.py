@@ -67,8 +67,19 @@ def main():
     ap.add_argument("--every", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/bitcmp.npz")
     ap.add_argument("--cmp", nargs=2)
+    ap.add_argument("--envs-of", type=int, default=0, help="with --cmp: per-env summary (fstate as [nfloat, n])")
     args = ap.parse_args()
     if args.cmp:
+        if args.envs_of:
+            A, B = np.load(args.cmp[0]), np.load(args.cmp[1])
+            for k in sorted((k for k in A.files if k[0] == "f"), key=lambda k: int(k[1:])):
+                x = A[k].reshape(-1, args.envs_of).astype(np.float64)
+                y = B[k].reshape(-1, args.envs_of).astype(np.float64)
+                d = np.abs(x - y)
+                rel = d / np.maximum(np.abs(x), 1e-3)
+                print(f"{k}: envs differing {int((d > 0).any(0).sum())}, rel > 1e-5 {int((rel > 1e-5).any(0).sum())}, "
+                      f"rel > 1e-3 {int((rel > 1e-3).any(0).sum())}, max rel {np.nanmax(rel):.3g}")
+            sys.exit(0)
         sys.exit(cmp(*args.cmp))
     run(args)
 
