@@ -15,8 +15,9 @@ synchronize and the max over ranks is reported.
 Extra JSON objects:
   roofline        the step kernel against HBM: algorithmic bytes per env-step
                   x envs per launch / average launch time from HIP events on the launch stream.
-  issue_roofline  the same kernel against the FP32 VALU issue rate (its real bound: one wave per
-                  SIMD on a dependent chain), from the SQ counters of the committed rocprofv3 run
+  issue_roofline  the same kernel against the chip's FP32 VALU issue rate (78.6 T lane-instr/s; its
+                  real bound: one wave per SIMD on a dependent chain, which can issue at most half
+                  of that -- one_wave_ceiling), from the SQ counters of the committed rocprofv3 run
                   of this library (profiles/, checked against the library's build id).
   cpu_baseline    the fp64 C oracle (oracle/, a restatement of the same step) over OpenMP on the
                   host cores this job may use (affinity, capped by the cgroup CPU quota), on a
@@ -45,9 +46,12 @@ from open_duck_playground_amd.joystick import Joystick, domain_randomize, wrap_f
 from open_duck_playground_amd.sharding import shard_from_env  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# FP32 VALU issue peak: 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz = 39.3 T lane-instructions/s (a wave64
-# VALU instruction occupies a SIMD for 4 cycles); = the 157.3 TFLOPS vector spec / 2 (FMA) / 2 (packed)
-VALU_PEAK_TLANE = 256 * 4 * 16 * 2.4e9 / 1e12
+# FP32 VALU issue peak of the chip: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz = 78.6 T lane-instructions/s
+# (MI355X_MICROARCH.md, v_fma_f32 wave64: 2 cycles on the 32-wide SIMD) = the 157.3 TFLOPS vector spec / 2 (FMA)
+VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12
+# what one wave alone on a SIMD can issue (same row: 4 cycles per wave64 instruction), i.e. the ceiling of a
+# kernel that registers hold at one wave per SIMD: half the chip's rate
+VALU_ONE_WAVE_TLANE = VALU_PEAK_TLANE / 2
 # newest tools/gpu_pmc.sh <rNN> C2 summary; only used when its build id matches the loaded library
 PMC_PROFILE = (sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_c2.json")))
                or [os.path.join(ROOT, "profiles", "r02_pmc_c2.json")])[-1]
@@ -253,7 +257,9 @@ def main():
             traffic = prof["hbm_bytes_per_launch"]
             valu = prof["SQ_INSTS_VALU"] * 64 / (kern_ms * 1e-3) / 1e12     # lane-instructions / s
             issue_rf = {"bound": "valu", "achieved": valu, "peak": VALU_PEAK_TLANE, "unit": "T lane-instr/s",
-                        "frac": valu / VALU_PEAK_TLANE, "valu_insts_per_launch": prof["SQ_INSTS_VALU"],
+                        "frac": valu / VALU_PEAK_TLANE, "one_wave_ceiling": VALU_ONE_WAVE_TLANE,
+                        "frac_of_one_wave_ceiling": valu / VALU_ONE_WAVE_TLANE,
+                        "valu_insts_per_launch": prof["SQ_INSTS_VALU"],
                         "valu_busy_frac": prof["valu_busy_frac"], "waitcnt_frac": prof["waitcnt_frac"], **src}
         else:  # another build's counters: no rate is derived from them
             issue_rf = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_TLANE, "unit": "T lane-instr/s",

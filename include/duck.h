@@ -36,7 +36,7 @@ extern "C" {
 
 typedef struct duck_sim duck_sim;
 
-enum { DUCK_OK = 0, DUCK_EINVAL = -1, DUCK_EUNSUPPORTED = -2, DUCK_EHIP = -3 };
+enum { DUCK_OK = 0, DUCK_EINVAL = -1, DUCK_EUNSUPPORTED = -2, DUCK_EHIP = -3, DUCK_EDEVICE = -4 };
 
 /* library version (major*10000 + minor*100 + patch) */
 int duck_version(void);
@@ -84,6 +84,15 @@ int duck_set_step_mode(duck_sim* sim, int mode);
 int duck_step_kernel_for(const duck_sim* sim, int n_envs);
 /* debug: latency-mode event waits that gave up (a broken cross-wave schedule; must stay 0) */
 int duck_debug_lat_timeouts(const duck_sim* sim, unsigned* out, int reset);
+
+/* Sticky device error word of the handle (bits DUCK_DEVERR_*), set by a kernel that could not
+ * complete its step correctly. It lives in host-mapped memory: duck_reset / duck_step /
+ * duck_physics_step read it on entry WITHOUT synchronising and return DUCK_EDEVICE while it is
+ * non-zero (so a failure surfaces at the first call after the failing launch has been written,
+ * at the latest after the caller's next synchronisation). `clear` resets it. No reference
+ * counterpart: MJX has no failure mode of this kind (its NaN guard is joystick.py:483-485). */
+enum { DUCK_DEVERR_LAT_TIMEOUT = 1 };
+int duck_device_error(duck_sim* sim, unsigned* out, int clear);
 
 /* Joystick.step (+ wrappers if cfg->auto_reset). `dr` (nullable) = per-env randomised
  * model values (duck_dr_layout, SoA [k][n_envs]) written by duck_randomize. `reward`,

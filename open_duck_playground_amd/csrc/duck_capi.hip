@@ -22,6 +22,21 @@ int duck_fail(int code, const std::string& msg) {
   return code;
 }
 
+// a kernel of this handle set the sticky device error word (DUCK_DEVERR_*): every later launch on the
+// handle is refused until duck_device_error(clear) -- the state the failed launch wrote is not valid
+static int device_error_fail(const duck_sim* s) {
+  const unsigned w = *s->err_h;
+  std::string why;
+  if (w & DUCK_DEVERR_LAT_TIMEOUT)
+    why += "a latency-kernel cross-wave event wait timed out (broken stage schedule); the envs of that "
+           "workgroup were written with NaN qpos";
+  return duck_fail(DUCK_EDEVICE, "device error word 0x" + [&] {
+    char b[16];
+    snprintf(b, sizeof(b), "%x", w);
+    return std::string(b);
+  }() + " set by an earlier launch: " + why);
+}
+
 // FNV-1a 64 over the model values a compiled variant bakes (duck_model_fingerprint)
 namespace {
 struct Fnv {
@@ -112,6 +127,7 @@ void duck_destroy(duck_sim* s) {
   if (!s) return;
   if (s->frames_d) (void)hipFree(s->frames_d);
   if (s->hfield_d) (void)hipFree(s->hfield_d);
+  if (s->err_h) (void)hipHostFree((void*)s->err_h);
   delete s;
 }
 
@@ -146,6 +162,20 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
       delete s;
       return duck_fail(DUCK_EHIP, std::string("hipDeviceGetAttribute: ") + hipGetErrorString(e));
     }
+  }
+  {
+    // the sticky device error word: host memory the kernels write through their device mapping, so
+    // that the next call reads it without synchronising (duck_device_error)
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s->err_d, p, 0);
+    if (e != hipSuccess) {
+      if (p) (void)hipHostFree(p);
+      delete s;
+      return duck_fail(DUCK_EHIP, std::string("device error word: ") + hipGetErrorString(e));
+    }
+    s->err_h = (volatile unsigned*)p;
+    *s->err_h = 0;
   }
   s->cfg = *cfg;
   s->nq = model->nq; s->nv = model->nv; s->nu = model->nu;
@@ -192,6 +222,7 @@ int duck_reset(duck_sim* s, int n, float* fstate, int32_t* istate, const uint8_t
                int64_t env_offset, const float* dr, float* obs, float* priv, void* stream) {
   g_err.clear();
   if (!s || n < 0 || !fstate || !istate || !obs || !priv) return duck_fail(DUCK_EINVAL, "bad argument");
+  if (*s->err_h) return device_error_fail(s);
   if (n == 0) return DUCK_OK;
   HIPCHECK(hipSetDevice(s->device));
   return kVariants[s->variant]->reset(s, n, fstate, istate, mask, seed, env_offset, dr, obs, priv,
@@ -203,6 +234,7 @@ int duck_step(duck_sim* s, int n, float* fstate, int32_t* istate, const float* d
   g_err.clear();
   if (!s || n < 0 || !fstate || !istate || !action || !obs || !priv || !reward || !done)
     return duck_fail(DUCK_EINVAL, "bad argument");
+  if (*s->err_h) return device_error_fail(s);
   if (n == 0) return DUCK_OK;
   HIPCHECK(hipSetDevice(s->device));
   return kVariants[s->variant]->step(s, n, fstate, istate, dr, action, obs, priv, reward, done, scratch,
@@ -221,6 +253,7 @@ int duck_physics_step(duck_sim* s, int n, float* qpos, float* qvel, float* warm,
                       int nsub, float* aux, float* scratch, void* stream) {
   g_err.clear();
   if (!s || n < 0 || !qpos || !qvel || !warm || !ctrl || nsub < 0) return duck_fail(DUCK_EINVAL, "bad argument");
+  if (*s->err_h) return device_error_fail(s);
   if (n == 0) return DUCK_OK;
   HIPCHECK(hipSetDevice(s->device));
   return kVariants[s->variant]->physics(s, n, qpos, qvel, warm, ctrl, dr, nsub, aux, scratch, (hipStream_t)stream);
@@ -237,6 +270,13 @@ int duck_step_kernel_for(const duck_sim* s, int n) {
   if (!s || n < 0) return duck_fail(DUCK_EINVAL, "bad argument");
   const bool lat = s->step_mode == DUCK_STEP_LATENCY || (s->step_mode == DUCK_STEP_AUTO && n <= LAT_WG_HOST * s->n_cu);
   return lat ? DUCK_STEP_LATENCY : DUCK_STEP_THROUGHPUT;
+}
+
+int duck_device_error(duck_sim* s, unsigned* out, int clear) {
+  if (!s || !out) return duck_fail(DUCK_EINVAL, "bad argument");
+  *out = *s->err_h;
+  if (clear) *s->err_h = 0;
+  return DUCK_OK;
 }
 
 int duck_debug_lat_timeouts(const duck_sim* s, unsigned* out, int reset) {

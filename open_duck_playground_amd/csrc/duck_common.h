@@ -41,6 +41,8 @@ struct duck_sim {
   int nq, nv, nu;
   int step_mode;  // DUCK_STEP_*
   int n_cu;       // compute units of the device (DUCK_STEP_AUTO)
+  volatile unsigned* err_h;  // sticky device error word (DUCK_DEVERR_*), host-mapped pinned memory
+  unsigned* err_d;           // its device mapping (KArgs::err)
 };
 
 // per-variant entry points, one table per compiled model variant (variant_*.hip)

@@ -43,6 +43,7 @@ struct KArgs {
   duck_env_config cfg;
   duck_layout lay;
   duck_dr_layout drl;
+  unsigned* err;  // the handle's sticky device error word (host-mapped; duck_device_error)
 };
 
 // Launch geometry: 16 lanes per env (a team), 16 envs (4 waves) per workgroup, so 4096 envs are
@@ -945,12 +946,19 @@ __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
   }
   __syncthreads();
   LAT_T(46, 5);
+  // a cross-wave wait that gave up: this workgroup's results are not valid. Raise the sticky error
+  // word (the next duck_* call on the handle returns DUCK_EDEVICE) and store NaN qpos, which the
+  // termination check turns into done, as the reference does for NaN physics (joystick.py:483-485)
+  const bool timed_out = TPL::ev_timed_out();
+  if (timed_out && threadIdx.x == 0 && A.err)
+    __hip_atomic_fetch_or(A.err, (unsigned)DUCK_DEVERR_LAT_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   {
     float hv[NK];
 #pragma unroll
     for (int kk = 0; kk < NK; kk++) {
       const int k = (int)threadIdx.x / WGL + (TPB / WGL) * kk;
       hv[kk] = esj[k < TL::HOT ? k : TL::HOT - 1];
+      if (timed_out && k >= A.lay.qpos && k < A.lay.qpos + Md::NQ) hv[kk] = __builtin_nanf("");
     }
 #pragma unroll
     for (int kk = 0; kk < NK; kk++) {
@@ -1053,6 +1061,7 @@ static KArgs make_args(duck_sim* s, int n) {
   A.ref = s->ref;
   A.frames = s->frames_d;
   A.hfield = s->hfield_d;
+  A.err = s->err_d;
   return A;
 }
 

@@ -144,9 +144,6 @@ DK float cfma(float x, float a) {
 constexpr float HF_WITNESS_BAND = 1e-3f;
 // depths within this (m) of the deepest prism contact count as equal (oracle HF_DEPTH_TIE)
 constexpr float HF_DEPTH_TIE = 1e-6f;
-// a prism's contact point moves towards the support midpoint while the total penetration weight is
-// below this (m; oracle HF_POINT_BAND): continuous where the weighted centroid of ~1e-7 m weights is not
-constexpr float HF_POINT_BAND = 1e-4f;
 
 #ifndef DUCK_LS_DFLOOR
 #define DUCK_LS_DFLOOR 1e-6f
@@ -1373,6 +1370,9 @@ struct TPhys {
   // plane floor vs hull for both feet at once (mjx collision_convex.plane_convex): lanes 0-7 take
   // the first floor pair, 8-15 the second
   static DK void collide_planes(LP L, int lane) {
+#ifdef DUCK_PLANE_NO_CONTRACT
+#pragma clang fp contract(off)
+#endif
     constexpr int NH = Md::NHV;
     const int h = lane >> 3, sub = lane & 7;
     const int p = Md::PLANE_PAIR[0] * (1 - h) + Md::PLANE_PAIR[1] * h;
@@ -1790,12 +1790,13 @@ struct TPhys {
       }
     }
     float pos[3];
-    if (W >= HF_POINT_BAND) {
+    if (W > 0.0f) {
       const float iw = 1.0f / W;
       for (int a = 0; a < 3; a++) pos[a] = Cx[a] * iw;
     } else {
-      // below the band (no vertex inside at all: crossing edges) the point moves towards the
-      // midpoint of the two shapes' support features along mu: Cx / band + (1 - W / band) mid
+      // no vertex inside at all (crossing edges): the midpoint of the two shapes' support features
+      // along mu. (Round 4 blended towards it below a total weight of 1e-4 m -- a "point band" for
+      // onset prisms; fp32 and fp64 then disagreed 2-3x as often)
       float hmu = 1e30f;
       float hv[NH];
       static_for<0, NH>([&](auto kI) { hv[kI.value] = hv_dot<kI.value>(mu); });
@@ -1818,8 +1819,7 @@ struct TPhys {
         wp_ += w;
         for (int a = 0; a < 3; a++) cq[a] += w * Tm[k][a];
       }
-      const float fq = 0.5f * (1.0f - W * (1.0f / HF_POINT_BAND));
-      for (int a = 0; a < 3; a++) pos[a] = Cx[a] * (1.0f / HF_POINT_BAND) + fq * (ch[a] / wh_ + cq[a] / wp_);
+      for (int a = 0; a < 3; a++) pos[a] = 0.5f * (ch[a] / wh_ + cq[a] / wp_);
     }
     E4[0] = f4v{mo, mu[0], mu[1], mu[2]};
     E4[1] = f4v{pos[0], pos[1], pos[2], 0.0f};
@@ -3323,7 +3323,11 @@ struct TPhys {
   // grow within a launch, so no event is reset between substeps. A spin is bounded (~40 ms, far
   // beyond a substep) so that a broken schedule ends the launch instead of hanging the device;
   // g_lat_timeouts counts such exits (tests read it: it must stay 0).
-  enum { EV_KIN = 0, EV_VEL = 1, EV_FSM = 2, EV_ROWS = 3, EV_EULER = 4, EV_M = 5, EV_QSM = 6, EV_WA = 7, EV_DIR = 8 };
+  // EV_TIMEOUT is not an event: a wait that gave up sets it, and step_kernel_lat then raises the
+  // handle's sticky device error word and writes NaN qpos for the workgroup's envs (duck_device_error)
+  enum { EV_KIN = 0, EV_VEL = 1, EV_FSM = 2, EV_ROWS = 3, EV_EULER = 4, EV_M = 5, EV_QSM = 6, EV_WA = 7, EV_DIR = 8,
+         EV_TIMEOUT = 9 };
+  static_assert(EV_TIMEOUT < TL::NEV || !LAT, "event slots");
   static DK lds_int* ev_ptr(int k) {
     extern __shared__ float lds_dyn[];
     return (lds_int*)(lds_dyn + TL::EV) + 4 * k;
@@ -3335,13 +3339,26 @@ struct TPhys {
     __hip_atomic_store(ev_ptr(k), v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   static DK void ev_wait(int k, int v) {
+#ifdef DUCK_LAT_FORCE_TIMEOUT
+    // test build (tests/test_gpu_env.py::test_latency_timeout_surfaces): workgroup 1's M event never
+    // arrives for wave 3, whose wait for it gives up after a few polls
+    const bool forced = blockIdx.x == 1 && k == EV_M;
+    const int LIMIT = forced ? 1 << 6 : 1 << 20;
+    if (forced) v += 1 << 24;
+#else
+    constexpr int LIMIT = 1 << 20;
+#endif
     for (int it = 0; __hip_atomic_load(ev_ptr(k), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v; it++) {
-      if (it > (1 << 20)) {
+      if (it > LIMIT) {
         if ((threadIdx.x & 63) == 0) atomicAdd(&g_lat_timeouts, 1u);
+        __hip_atomic_store(ev_ptr(EV_TIMEOUT), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
+  }
+  static DK bool ev_timed_out() {
+    return __hip_atomic_load(ev_ptr(EV_TIMEOUT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
   }
   // wave 0, substep s: kinematics and com_pos (everything else waits for them), rne's velocities
   // (the contact rows need the feet's), then the rest of rne and the actuation (qfrc_smooth)

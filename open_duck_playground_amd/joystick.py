@@ -238,6 +238,14 @@ class Joystick(OpenDuckMiniV2Env):
         check(min(k, 0), self._lib)
         return {1: "throughput", 2: "latency"}[k]
 
+    def device_error(self, clear: bool = False) -> int:
+        """The handle's sticky device error word (duck_device_error; DUCK_DEVERR_* bits, 0 = none). While
+        it is set, reset/step/physics_step raise DuckError (DUCK_EDEVICE): a latency-kernel launch whose
+        cross-wave wait gave up has written invalid state (NaN qpos) for its workgroup's envs."""
+        out = C.c_uint(0)
+        check(self._lib.duck_device_error(self._sim, C.byref(out), int(clear)), self._lib)
+        return int(out.value)
+
     def lat_timeouts(self, reset: bool = False) -> int:
         """Latency-mode event waits that gave up since the last reset (a broken schedule; must be 0)."""
         out = C.c_uint(0)

@@ -24,7 +24,8 @@ EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get"
            "duck_reset", "duck_step", "duck_randomize", "duck_physics_step", "duck_gae", "duck_ppo_loss",
            "duck_ppo_loss_out_size", "duck_mlp_gemm", "duck_mlp_wgrad", "duck_mlp_wgrad_reduce",
            "duck_policy_sample", "duck_clip_adam", "duck_clip_adam_scratch_size", "duck_set_step_mode",
-           "duck_step_kernel_for", "duck_debug_lat_timeouts", "duck_gather_columns", "duck_mlp_group"]
+           "duck_step_kernel_for", "duck_debug_lat_timeouts", "duck_gather_columns", "duck_mlp_group",
+           "duck_device_error"]
 
 
 class DuckMlpProblem(C.Structure):
@@ -113,7 +114,9 @@ def _build_unlocked(verbose, defines, out, extra_flags, no_ilp, isa_check, gen_d
         [os.path.join(inc, f) for f in os.listdir(inc)] + \
         [os.path.join(ROOT, "include", f) for f in sorted(os.listdir(os.path.join(ROOT, "include"))) if f.endswith(".h")] + \
         [os.path.abspath(__file__)]  # the compile flags live here
-    if not defines and not extra_flags and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
+    # (a define/flag build into the shared output is never "fresh"; a unit directory's own output is)
+    if (gen_dir is not None or not defines and not extra_flags) and os.path.exists(out) and \
+            os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
     import hashlib
     import tempfile
@@ -193,6 +196,26 @@ def model_library(m, verbose: bool = False) -> str:
             fcntl.flock(lock, fcntl.LOCK_UN)
 
 
+def debug_library(name: str, defines, variants=("flat",), verbose: bool = False) -> str:
+    """build/libduck_<name>.so: the shipped scene variants in `variants` compiled with extra `defines`
+    (test builds, e.g. DUCK_LAT_FORCE_TIMEOUT for test_gpu_env.py::test_latency_timeout_surfaces).
+    One scene instead of four keeps the build short; built by __graft_entry__.build(), never on a GPU box."""
+    from . import codegen
+    gen = os.path.join(BUILD, f"gen_{name}")
+    os.makedirs(gen, exist_ok=True)
+    # (the defines are a file of the unit directory: a change of them makes build() recompile)
+    files = {"duck_variants.inc": codegen.variant_registry(variants), "defines.txt": "\n".join(defines) + "\n"}
+    for v in variants:
+        files[f"duck_model_{v}.h"] = open(os.path.join(CSRC, "generated", f"duck_model_{v}.h")).read()
+        files[f"variant_{v}.hip"] = codegen.variant_unit(v, f"duck_model_{v}.h")
+    for fn, text in files.items():
+        path = os.path.join(gen, fn)
+        if not os.path.exists(path) or open(path).read() != text:
+            with open(path, "w") as f:
+                f.write(text)
+    return build(verbose=verbose, defines=tuple(defines), out=os.path.join(BUILD, f"libduck_{name}.so"), gen_dir=gen)
+
+
 def isa_kernels(texts) -> list:
     """The kernel symbols (amdgpu_kernel entry labels) in disassembled code objects."""
     import re
@@ -256,6 +279,8 @@ def lib(path: str = None):
             L.duck_set_step_mode.argtypes = [vp, C.c_int]
             L.duck_step_kernel_for.argtypes = [vp, C.c_int]
             L.duck_debug_lat_timeouts.argtypes = [vp, C.POINTER(C.c_uint), C.c_int]
+        if hasattr(L, "duck_device_error"):
+            L.duck_device_error.argtypes = [vp, C.POINTER(C.c_uint), C.c_int]
         if hasattr(L, "duck_gae"):
             L.duck_gae.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp]
         if hasattr(L, "duck_ppo_loss"):

@@ -116,6 +116,7 @@ def mlp(sizes: Sequence[int], out: int) -> nn.Sequential:
 
 
 MIN_STD = 1e-3
+POLICY_SAMPLE_MAX_ACTIONS = 16  # duck_policy_sample (csrc/duck_mlp.hip): one lane per action dim of a 16-lane row
 
 
 def _log_det_jac_tanh(x: torch.Tensor) -> torch.Tensor:
@@ -813,9 +814,10 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
     data = {k: torch.zeros((T, B) + sh, dtype=torch.float32, device=device) for k, sh in shapes.items()}
     learner = _Learner(net, opt, cfg, data, mb, device, use_graph)
     # the GPU unroll through the duck_mlp / duck_policy_sample kernels, graph-captured (DUCK_PPO_FUSED_MLP=0:
-    # the torch policy and torch's normal sampler)
+    # the torch policy and torch's normal sampler; also for models with more than 16 actuators, which
+    # duck_policy_sample's one-lane-per-action-dim layout does not take)
     roller = _Rollout(env, net, cfg, data, unrolls_per_update, device, use_graph, cfg.seed * 7919 + rank) \
-        if fused_grad_available(device) else None
+        if fused_grad_available(device) and A <= POLICY_SAMPLE_MAX_ACTIONS else None
     state = env.reset(rng=cfg.seed)  # streams are keyed by global env id: ranks draw disjoint envs
     result = TrainResult(net=net)
     # brax: num_evals evaluations spread evenly over training, the first before any update

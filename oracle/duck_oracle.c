@@ -690,13 +690,12 @@ static void collide_plane_convex(const oracle_model* m, oracle_data* d, int g1, 
  * prism contacts by MJX's _manifold_points starting at the deepest (within HF_DEPTH_TIE). Declared choices (DESIGN.md
  * §5 item 6): equal overlaps resolve to the first axis in the order prism top, sides, bottom, hull
  * faces, top-edge pairs, vertical-edge pairs, bottom-edge pairs; the contact point of a prism
- * is the penetration-weighted centroid of the vertices of each shape inside the other, moved towards
- * the midpoint of the two shapes' support features (the centroid of each shape's vertices within
- * HF_WITNESS_BAND of its support plane along the normal, weighted 1 at the plane to 0 at the band
- * edge; the prism's top vertices only) while the total weight is below HF_POINT_BAND, and that
- * midpoint alone when no vertex is inside (crossing edges). */
+ * is the penetration-weighted centroid of the vertices of each shape inside the other, or, when no
+ * vertex is inside (crossing edges), the midpoint of the two shapes' support features (the centroid
+ * of each shape's vertices within HF_WITNESS_BAND of its support plane along the normal, weighted 1
+ * at the plane to 0 at the band edge; the prism's top vertices only). */
 #define HF_WITNESS_BAND 1e-3 /* m; = TPhys HF_WITNESS_BAND */
-#define HF_POINT_BAND 1e-4   /* m; = TPhys HF_POINT_BAND: a total penetration weight below this blends the point towards the support midpoint */
+#define HF_POINT_BAND 1e-4   /* m; test aid only (oracle_set_hf_band_scale): round 4's "point band", see below */
 #define HF_DEPTH_TIE 1e-6    /* m; = TPhys HF_DEPTH_TIE: prisms sharing a grid vertex or edge often tie exactly */
 #define HF_MAXPRISM 128      /* prisms under one hull (the sub-grid of a 0.11 m foot: <= 18) */
 
@@ -720,10 +719,34 @@ void oracle_set_hf_tie_last(double band) { g_hf_tie_last = band; }
 static _Thread_local double g_hf_tie_first;
 void oracle_set_hf_tie_first(double band) { g_hf_tie_first = band; }
 
-/* test aid (oracle_set_hf_band_scale): scales HF_POINT_BAND (default 1; 0 = the plain weighted
- * centroid, round 3's point rule): tools/hfield_deviation.py compares the two. */
-static _Thread_local double g_hf_band_scale = 1.0;
+/* test aid (oracle_set_hf_band_scale): with s > 0 a prism contact whose total penetration weight W
+ * is below s * HF_POINT_BAND moves towards the support midpoint (pos = C / band + (1 - W / band) mid),
+ * round 4's "point band" for onset prisms. Default 0: the declared rule (the plain weighted centroid),
+ * which the kernel computes; the band made fp32 and fp64 disagree 2-3x as often
+ * and now serves as a contact-generation-only injected defect (teacher_forcing.DEFECTS) and for
+ * tools/hfield_deviation.py. Process-wide, not thread-local: the batched entry points run envs on
+ * OpenMP workers, which must all see it. */
+static double g_hf_band_scale = 0.0;
 void oracle_set_hf_band_scale(double s) { g_hf_band_scale = s; }
+double oracle_get_hf_band_scale(void) { return g_hf_band_scale; }
+
+/* test aids: injected contact-generation defects for the teacher-forcing classifier's teeth
+ * (teacher_forcing.DEFECTS; the kernel keeps the declared rules): which = 0 the point band scale
+ * (above), 1 a scale of HF_WITNESS_BAND, 2 a scale of HF_DEPTH_TIE, 3 the rank of the prism contact
+ * the 4-slot manifold starts from (0: the deepest, the declared rule; 1: the second deepest).
+ * Process-wide, like the band scale. */
+static double g_hf_witness_scale = 1.0, g_hf_depth_tie_scale = 1.0;
+static int g_hf_manifold_start = 0;
+void oracle_set_hf_defect(int which, double v) {
+  if (which == 0) g_hf_band_scale = v;
+  else if (which == 1) g_hf_witness_scale = v;
+  else if (which == 2) g_hf_depth_tie_scale = v;
+  else if (which == 3) g_hf_manifold_start = (int)v;
+}
+double oracle_get_hf_defect(int which) {
+  return which == 0 ? g_hf_band_scale
+                    : (which == 1 ? g_hf_witness_scale : (which == 2 ? g_hf_depth_tie_scale : (double)g_hf_manifold_start));
+}
 
 /* the hull in the local frame (the height field's axes, origin at the hull's frame) */
 typedef struct {
@@ -868,11 +891,9 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
   const double* u = ax[w];
   /* the contact point: the centroid of the vertices of each shape inside the other (hull vertices
    * inside the prism, prism top vertices inside the hull), each weighted by its penetration (distance
-   * to the nearest face of the other shape), blended towards the midpoint of the two shapes' support
-   * features along u when the total weight W is below HF_POINT_BAND: pos = C / W for W >= band, else
-   * C / band + (1 - W / band) mid (continuous at W = band; mid alone when no vertex is inside, i.e.
-   * crossing edges). The plain centroid of ~1e-7 m weights is ill-conditioned: fp32 and fp64 put an
-   * onset prism's point centimetres apart. */
+   * to the nearest face of the other shape); the midpoint of the two shapes' support features along u
+   * when no vertex is inside (crossing edges). (Test aid: with the band scale > 0, a weight W below
+   * the band blends towards that midpoint, C / band + (1 - W / band) mid.) */
   double wsum = 0, c[3] = {0, 0, 0};
   const double ptop = dot3(nt, T[0]);
   for (int k = 0; k < H->nv; k++) {
@@ -893,12 +914,12 @@ static int hf_prism_contact(const oracle_model* m, const hf_hull* H, const doubl
     const double hmin = pts_min(u, (const double(*)[3])H->V, H->nv), pmax = pts_max(u, T, 3);
     double wh = 0, wp = 0, ch[3] = {0, 0, 0}, cp[3] = {0, 0, 0};
     for (int k = 0; k < H->nv; k++) {
-      const double wk = fmax(0.0, 1.0 - (dot3(u, H->V[k]) - hmin) / HF_WITNESS_BAND);
+      const double wk = fmax(0.0, 1.0 - (dot3(u, H->V[k]) - hmin) / (HF_WITNESS_BAND * g_hf_witness_scale));
       wh += wk;
       for (int a = 0; a < 3; a++) ch[a] += wk * H->V[k][a];
     }
     for (int k = 0; k < 3; k++) {
-      const double wk = fmax(0.0, 1.0 - (pmax - dot3(u, T[k])) / HF_WITNESS_BAND);
+      const double wk = fmax(0.0, 1.0 - (pmax - dot3(u, T[k])) / (HF_WITNESS_BAND * g_hf_witness_scale));
       wp += wk;
       for (int a = 0; a < 3; a++) cp[a] += wk * T[k][a];
     }
@@ -1010,23 +1031,43 @@ int oracle_hfield_contacts(const oracle_model* m, const oracle_data* d, int g_hf
   return k;
 }
 
+/* the 4 slots' prism contacts (indices into the candidates, strip order): mjx's _manifold_points over
+ * their points, from the deepest (the first in strip order within HF_DEPTH_TIE of the deepest: prisms
+ * that share a grid vertex or edge often reach the same depth through it), areas taken in the plane of
+ * its normal. Frame-free (differences and cross products only). */
+static void hf_select(const double* dep, const double (*pt)[3], const double (*nrm)[3], int n, int idx[4]) {
+  double dmax = dep[0];
+  for (int i = 1; i < n; i++) dmax = fmax(dmax, dep[i]);
+  int a = 0;
+  while (dep[a] < dmax - HF_DEPTH_TIE * g_hf_depth_tie_scale) a++;
+  if (g_hf_manifold_start == 1 && n > 1) { /* test aid (injected defect): the second deepest */
+    int b = a == 0 ? 1 : 0;
+    for (int i = 0; i < n; i++)
+      if (i != a && dep[i] > dep[b]) b = i;
+    a = b;
+  }
+  int mask[HF_MAXPRISM];
+  for (int i = 0; i < n; i++) mask[i] = 1;
+  manifold_points_from(pt, mask, n, nrm[a], a, idx);
+}
+
+/* test aid: hf_select over caller-given candidates (n <= 128; depth [n], point [n][3], normal [n][3],
+ * any one frame): the teacher-forcing selection rules replay the oracle's own choice under fp32 noise */
+int oracle_hfield_select(const double* depth, const double* point, const double* normal, int n, int idx[4]) {
+  if (n < 1 || n > HF_MAXPRISM) return -1;
+  hf_select(depth, (const double(*)[3])point, (const double(*)[3])normal, n, idx);
+  return 0;
+}
+
 static void collide_hfield_convex(const oracle_model* m, oracle_data* d, int g1, int g2, int slot0) {
   for (int c = 0; c < DUCK_CON_PER_PAIR; c++) set_inactive(d, slot0 + c, g1, g2);
   hf_frame F;
   double dep[HF_MAXPRISM], nrm[HF_MAXPRISM][3], pt[HF_MAXPRISM][3];
   const int n = hf_contacts(m, d, g1, g2, &F, dep, nrm, pt);
   if (n == 0) return;
-  /* 4 of the prism contacts by mjx's _manifold_points over their points, from the deepest (the
-   * first in strip order within HF_DEPTH_TIE of the deepest: prisms that share a grid vertex or
-   * edge often reach the same depth through it), areas taken in the plane of its normal; repeats
-   * stay inactive (plane_convex's rule) */
-  double dmax = dep[0];
-  for (int i = 1; i < n; i++) dmax = fmax(dmax, dep[i]);
-  int a = 0;
-  while (dep[a] < dmax - HF_DEPTH_TIE) a++;
-  int mask[HF_MAXPRISM], idx[4];
-  for (int i = 0; i < n; i++) mask[i] = 1;
-  manifold_points_from((const double(*)[3])pt, mask, n, nrm[a], a, idx);
+  /* 4 of the prism contacts (hf_select); repeats stay inactive (plane_convex's rule) */
+  int idx[4];
+  hf_select(dep, (const double(*)[3])pt, (const double(*)[3])nrm, n, idx);
   const double *hp = d->geom_xpos[g1], *HR = d->geom_xmat[g1];
   for (int s = 0; s < DUCK_CON_PER_PAIR; s++) {
     const int b = idx[s];

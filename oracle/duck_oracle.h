@@ -80,6 +80,13 @@ void oracle_set_trace(double* buf); /* test aid: record substep inputs of oracle
 void oracle_set_ls_floor(double floor); /* test aid: the HIP line search's fp32 stop rule (0 = off) */
 void oracle_set_hdump(double* buf); /* test aid: dump the next solve's first Newton Hessian and row margins */
 void oracle_set_hf_band_scale(double s); /* test aid: scales HF_POINT_BAND (0: the plain weighted centroid) */
+double oracle_get_hf_band_scale(void);
+/* test aids: injected contact-generation defects (0 point band scale, 1 witness band scale, 2 depth
+ * tie scale, 3 manifold start rank) */
+void oracle_set_hf_defect(int which, double value);
+double oracle_get_hf_defect(int which);
+/* test aid: the height-field 4-slot choice (collide_hfield_convex's) over caller-given candidates */
+int oracle_hfield_select(const double* depth, const double* point, const double* normal, int n, int idx[4]);
 void oracle_set_hf_tie_last(double band); /* test aid: height-field SAT near-ties resolve to the last axis in the band */
 void oracle_set_hf_tie_first(double band); /* test aid: height-field SAT near-ties resolve to the first axis in the band */
 int oracle_hfield_contacts(const oracle_model* m, const oracle_data* d, int g_hf, int g_cvx, int max, double* depth,

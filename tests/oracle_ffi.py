@@ -85,6 +85,13 @@ def lib():
         L.oracle_set_force_start.argtypes = [C.c_int]
         L.oracle_set_hdump.argtypes = [dp]
         L.oracle_set_hf_band_scale.argtypes = [C.c_double]
+        L.oracle_get_hf_band_scale.restype = C.c_double
+        L.oracle_set_hf_defect.argtypes = [C.c_int, C.c_double]
+        L.oracle_get_hf_defect.argtypes = [C.c_int]
+        L.oracle_get_hf_defect.restype = C.c_double
+        L.oracle_hfield_select.argtypes = [dp, dp, dp, C.c_int, ip]
+        if os.environ.get("ORACLE_HF_BAND_SCALE"):  # A/B of a kernel built with -DDUCK_HF_POINT_BAND=...
+            L.oracle_set_hf_band_scale(float(os.environ["ORACLE_HF_BAND_SCALE"]))
         L.oracle_set_hf_tie_last.argtypes = [C.c_double]
         L.oracle_set_hf_tie_first.argtypes = [C.c_double]
         L.oracle_hfield_contacts.argtypes = [vp, C.POINTER(OracleData), C.c_int, C.c_int, C.c_int, dp, dp, dp]

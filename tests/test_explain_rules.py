@@ -12,30 +12,46 @@ from open_duck_playground_amd import joystick
 from open_duck_playground_amd.config import default_config, env_config_struct
 from open_duck_playground_amd.mjcf import Model
 from tests.oracle_ffi import OracleBatch, OracleModel
-from tests.teacher_forcing import (DEFECTS, _state_rel, backward_error_landing, copy_model, flip_level,
-                                   oracle_substep)
+from collections import Counter
+
+from tests.oracle_ffi import lib
+from tests.teacher_forcing import (DEFECTS, _state_rel, backward_error_landing, copy_model, declared_difference,
+                                   flip_level, oracle_contact_aux, oracle_knob, oracle_substep)
 
 ASSETS = os.path.join(os.path.dirname(joystick.__file__), "assets")
 
 
-def _states(task: str, n: int = 24, steps: int = 12, seed: int = 3):
-    """substep inputs (qpos, qvel, qacc_warmstart, ctrl) of an oracle rollout with U(-1,1) actions"""
+def _states(task: str, n: int = 24, steps: int = 12, seed: int = 3, substeps: bool = False):
+    """substep inputs (qpos, qvel, qacc_warmstart, ctrl) of an oracle rollout with U(-1,1) actions: the
+    final env-step boundary of every env, or (substeps=True) every substep's input of every env-step"""
     m = Model.load(os.path.join(ASSETS, task + ".npz"))
     ob = OracleBatch(OracleModel(m), env_config_struct(m, default_config(), False), n)
     ob.reset(seed=seed)
     rng = np.random.default_rng(seed)
-    for _ in range(steps):
-        ob.step(rng.uniform(-1, 1, (n, 14)))
     L = ob.L
-    F = ob.fs.reshape(L.nfloat, n)
     o = L.off
-    xs = [np.concatenate([F[o["qpos"]:o["qpos"] + m.nq, e], F[o["qvel"]:o["qvel"] + m.nv, e],
-                          F[o["qacc_warmstart"]:o["qacc_warmstart"] + m.nv, e], F[o["ctrl"]:o["ctrl"] + m.nu, e]])
-          for e in range(n)]
-    return m, xs
+
+    def boundary():
+        F = ob.fs.reshape(L.nfloat, n)
+        return [np.concatenate([F[o["qpos"]:o["qpos"] + m.nq, e], F[o["qvel"]:o["qvel"] + m.nv, e],
+                                F[o["qacc_warmstart"]:o["qacc_warmstart"] + m.nv, e], F[o["ctrl"]:o["ctrl"] + m.nu, e]])
+                for e in range(n)]
+    xs = []
+    for _ in range(steps):
+        if substeps:
+            xs += boundary()
+        ob.step(rng.uniform(-1, 1, (n, 14)))
+    if not substeps:
+        return m, boundary()
+    om, out = OracleModel(m), []
+    for x in xs:
+        for _ in range(10):
+            out.append(x)
+            x = oracle_substep(om, x)
+    return m, out
 
 
-@pytest.mark.parametrize("defect", [d for d in DEFECTS if DEFECTS[d][0] == "flat"])
+@pytest.mark.parametrize("defect", [d for d in DEFECTS if DEFECTS[d][0] == "flat" and DEFECTS[d][1] is not None])
 def test_backward_error_rule_rejects_model_defects(defect):
     m, xs = _states("flat_terrain")
     om = OracleModel(m)
@@ -68,3 +84,109 @@ def test_backward_error_rule_accepts_perturbed_inputs():
         checked += 1
         landed += backward_error_landing(om, x, g) is not None
     assert checked >= 8 and landed >= 0.9 * checked, (landed, checked)
+
+
+def _differing(m, xs, om, gpu, cap: int = 40):
+    """(x, the stand-in GPU's substep, its contacts) where it differs from the oracle's beyond the
+    teacher-forcing sub_tol (1e-4), at most `cap` of them spread over the rollout"""
+    out = []
+    for x in xs:
+        g, ga = gpu(x)
+        if _state_rel(m, g, oracle_substep(om, x)) > 1e-4:
+            out.append((x, g, ga))
+    pick = np.linspace(0, len(out) - 1, min(cap, len(out))).astype(int) if out else []
+    return len(out), [out[i] for i in pick]
+
+
+def _classify(m, om, cases, seed: int = 0):
+    """what explain() would say at each differing substep: a flip level or a declared rule, else defect"""
+    rng = np.random.default_rng(seed)
+    rules = Counter()
+    for x, g, ga in cases:
+        lev = flip_level(om, x, g, rng)
+        if lev is not None:
+            rules[f"flip{lev:.0e}"] += 1
+            continue
+        why = declared_difference(None, 0, om, x, g, 1e-4, ga=ga)
+        rules[why or "defect"] += 1
+    return rules
+
+
+@pytest.mark.parametrize("defect", [d for d in DEFECTS if DEFECTS[d][2] is not None])
+def test_contact_rules_reject_contact_generation_defects(defect):
+    """The CPU half of test_explain_has_teeth for the contact-generation-only defects (DEFECTS' oracle
+    knobs: round 4's point band, the witness band x 1.5, the deepest-prism tie x 30, the manifold from
+    the second-deepest prism): the stand-in GPU is the oracle WITH the defect (its substep and its
+    contacts), the classifier runs the nominal oracle. The rules that fire on contact generation --
+    onset, sat_tie, onset_selection, dup_selection -- and backward_error and flip_level must call
+    >= 90 % of the differing substeps a defect (per-rule counts printed)."""
+    knob = DEFECTS[defect][2]
+    # (the deepest-prism tie x 30 changes the result rarely: a larger rollout for enough cases)
+    m, xs = _states("rough_terrain", n=64 if knob[0] == 2 else 16, steps=12, substeps=True)
+    om = OracleModel(m)
+
+    def gpu(x):
+        with oracle_knob(knob):
+            return oracle_substep(om, x), oracle_contact_aux(om, x)
+    total, cases = _differing(m, xs, om, gpu)
+    rules = _classify(m, om, cases)
+    print(f"{defect}: {total} of {len(xs)} substeps differ, {len(cases)} classified: {dict(sorted(rules.items()))}")
+    assert len(cases) >= 8, total
+    assert rules["defect"] >= 0.9 * len(cases), dict(rules)
+
+
+@pytest.mark.parametrize("tie", ["last", "first"])
+def test_sat_tie_accepts_fp32_tie_resolution(tie):
+    """The positive side of sat_tie: a stand-in GPU that resolves height-field SAT overlaps within 1e-6 m
+    of the minimum to the other tied axis (oracle_set_hf_tie_last / _first: what the kernel's fp32
+    overlaps may do) is accepted at >= 90 % of the substeps where that changes the result."""
+    m, xs = _states("rough_terrain", n=64, steps=12, substeps=True)
+    om = OracleModel(m)
+    setter = lib().oracle_set_hf_tie_last if tie == "last" else lib().oracle_set_hf_tie_first
+
+    def gpu(x):
+        setter(1e-6)
+        try:
+            return oracle_substep(om, x), oracle_contact_aux(om, x)
+        finally:
+            setter(0.0)
+    total, cases = _differing(m, xs, om, gpu)
+    rules = _classify(m, om, cases)
+    print(f"tie_{tie}: {total} of {len(xs)} substeps differ: {dict(sorted(rules.items()))}")
+    assert len(cases) >= 8, total
+    assert rules["defect"] <= 0.1 * len(cases), dict(rules)
+
+
+def test_manifold_select_is_the_oracles():
+    """teacher_forcing.manifold_select (the selection rules' restatement of collide_hfield_convex's
+    4-slot choice) picks the oracle's own slots from the oracle's candidates (oracle_hfield_contacts),
+    at every height-field pair with a contact over a rough rollout"""
+    import ctypes as C
+    from tests.teacher_forcing import _slots_of, _split, manifold_select
+    m, xs = _states("rough_terrain", n=16, steps=6, substeps=True)
+    om = OracleModel(m)
+    floor = m.id("geom", "floor")
+    pairs = [(p, int(m.pair_geom2[p]) if int(m.pair_geom1[p]) == floor else int(m.pair_geom1[p]))
+             for p in range(m.npair) if floor in (int(m.pair_geom1[p]), int(m.pair_geom2[p]))]
+    checked = 0
+    for x in xs:
+        q, v, w, c = _split(m, x)
+        d = om.new_data(qpos=q, qvel=v, ctrl=c, warm=w)
+        om.forward(d)
+        od = d.arr("con_dist", 4 * m.npair)
+        op = np.ctypeslib.as_array(d.con_pos)[:4 * m.npair]
+        for p, foot in pairs:
+            dep, nrm, pt = np.zeros(128), np.zeros(3 * 128), np.zeros(3 * 128)
+            k = lib().oracle_hfield_contacts(om.ptr, C.byref(d), floor, foot, 128, dep.ctypes.data_as(C.POINTER(C.c_double)),
+                                             nrm.ctypes.data_as(C.POINTER(C.c_double)), pt.ctypes.data_as(C.POINTER(C.c_double)))
+            if k == 0:
+                continue
+            dep, nrm, pt = dep[:k], nrm[:3 * k].reshape(k, 3), pt[:3 * k].reshape(k, 3)
+            got = _slots_of(manifold_select(dep, pt, nrm), dep, pt)
+            for s, (gd_, gp_) in enumerate(got):
+                if gd_ is None:
+                    assert od[4 * p + s] >= 0
+                else:
+                    assert abs(-od[4 * p + s] - gd_) < 1e-12 and np.abs(op[4 * p + s] - gp_).max() < 1e-12
+            checked += 1
+    assert checked >= 200, checked

@@ -237,6 +237,42 @@ def test_latency_mode_matches_throughput_mode(cfg, n, gpu):
     assert envs["latency"].lat_timeouts() == 0
 
 
+def test_latency_timeout_surfaces(gpu, monkeypatch):
+    """A latency-kernel launch whose cross-wave wait gives up is not silent: the test build
+    (native.debug_library "force_timeout", -DDUCK_LAT_FORCE_TIMEOUT: wave 3 of workgroup 1 never sees
+    its M event and gives up after a few polls) sets the handle's sticky device error word, writes NaN
+    qpos for workgroup 1's envs (4..7) and only those, and the next step raises DuckError (DUCK_EDEVICE)
+    until the word is cleared. The shipped library's word stays 0 over the same steps."""
+    import os
+    from open_duck_playground_amd import joystick as jmod
+    from open_duck_playground_amd.native import BUILD, DuckError
+    path = os.path.join(BUILD, "libduck_force_timeout.so")
+    assert os.path.exists(path), "built by __graft_entry__.build()"
+    n = 16
+    ok = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
+    ok.set_step_mode("latency")
+    st = ok.reset(rng=1)
+    for _ in range(2):
+        st = ok.step(st, torch.zeros(n, 14, device=gpu))
+    torch.cuda.synchronize()
+    assert ok.device_error() == 0
+    monkeypatch.setattr(jmod, "model_library", lambda m: path)
+    env = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
+    env.set_step_mode("latency")
+    st = env.reset(rng=1)
+    st = env.step(st, torch.zeros(n, 14, device=gpu))
+    torch.cuda.synchronize()
+    assert env.device_error() == 1          # DUCK_DEVERR_LAT_TIMEOUT
+    L = env._layout
+    q = st.fstate.view(L.nfloat, n)[L.off["qpos"]:L.off["qpos"] + env.mj_model.nq]
+    bad = torch.isnan(q).any(dim=0).cpu().numpy()
+    assert bad[4:8].all() and not bad[:4].any() and not bad[8:].any(), bad
+    with pytest.raises(DuckError, match="device error word"):
+        env.step(st, torch.zeros(n, 14, device=gpu))
+    assert env.device_error(clear=True) == 1 and env.device_error() == 0
+    env.reset(rng=2)                         # usable again once cleared
+
+
 def test_step_mode_auto_selects_by_batch(gpu):
     """AUTO: the latency kernel while the batch leaves a CU per 4 envs, the throughput kernel above."""
     ncu = torch.cuda.get_device_properties(gpu).multi_processor_count

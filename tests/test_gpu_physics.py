@@ -216,10 +216,13 @@ def test_hfield_prism_contacts_match_oracle(task, height, gpu):
 @pytest.mark.parametrize("task", ["rough_terrain", "rough_terrain_backlash"])
 def test_hfield_kernel_matches_brute_force_prisms(task, gpu):
     """The kernel's height-field contacts against the brute-force prism reference (every axis of
-    every prism, fp64; tools/hfield_deviation.py --gpu) at oracle rollout states of rough + DR: the
-    feet's contact flags agree, the deepest depth to fp32 (1e-6 m at p99), and its normal -- the
-    declared tie-band blend of the two smallest overlaps' axes -- the oracle's to 0.1 deg at p99
-    (fp32 ties of equal-depth prisms aside)."""
+    every prism, fp64; tools/hfield_deviation.py --gpu) and the oracle at oracle rollout states of
+    rough + DR: the feet's contact flags agree, the deepest depth to fp32 (1e-6 m at p99), its normal
+    the oracle's to 0.1 deg at p99 (fp32 ties of equal-depth prisms aside), and the contact points --
+    the declared penetration-weighted centroid, what round 4's point band changed -- the oracle's:
+    the deepest slot's point to 0.2 mm at p99 and every active slot's to 0.2 mm at p99, with at most
+    1 % of either further than 1 mm (onset prisms, whose centroid of ~1e-7 m weights fp32 cannot
+    place: DESIGN.md §5 item 6)."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
@@ -229,3 +232,5 @@ def test_hfield_kernel_matches_brute_force_prisms(task, gpu):
     assert r["contact_kernel"] > 200
     assert r["flag_agreement"] >= 0.999, r
     assert r["depth_abs_diff_m"]["p99"] < 1e-6 and r["normal_angle_deg"]["p99"] < 0.1, r
+    for k in ("deepest_point_m", "slot_point_m"):
+        assert r[k]["p99"] < 2e-4 and r[k]["frac_over_1mm"] <= 0.01, (k, r[k])

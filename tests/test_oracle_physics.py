@@ -232,9 +232,9 @@ def test_hfield_contacts_match_brute_force_prisms():
     penetration over the Minkowski-face axes, 4 slots by _manifold_points from the deepest) against
     the brute-force reference over every separating axis of every prism (oracle_hfield_prisms), on
     rough-terrain + DR env-steps: contact flags agree everywhere, the deepest contact's depth and
-    normal agree to fp64 rounding (tools/hfield_deviation.py), with the declared point band
-    (HF_POINT_BAND) and with round 3's plain weighted centroid (oracle_set_hf_band_scale(0)): the
-    point rule moves no depth or normal."""
+    normal agree to fp64 rounding (tools/hfield_deviation.py), with the declared plain weighted
+    centroid and with round 4's point band (oracle_set_hf_band_scale(1), now a test aid): the point
+    rule moves no depth or normal."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
     from hfield_deviation import measure

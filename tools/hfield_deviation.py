@@ -38,7 +38,7 @@ def prisms(om, d, g_hf, g_foot, max_n=64):
     return dep[:n], nrm[:3 * n].reshape(n, 3)
 
 
-def measure(task: str, n_envs: int, n_steps: int, seed: int = 0, blend: bool = True):
+def measure(task: str, n_envs: int, n_steps: int, seed: int = 0, blend: bool = False):
     m = Model.load(constants.task_to_xml(task))
     base = OracleModel(m)
     cfg = env_config_struct(m, default_config(), False, domain_randomize=True)
@@ -52,13 +52,13 @@ def measure(task: str, n_envs: int, n_steps: int, seed: int = 0, blend: bool = T
     rows = []
     wins = (C.c_longlong * 14)()
     lib().oracle_hfield_axis_wins(wins, 1)
-    # blend=False: round 3's plain penetration-weighted centroid (oracle_set_hf_band_scale(0)) in
-    # place of the point band
+    # blend=True: round 4's point band (oracle_set_hf_band_scale(1)) in place of the declared plain
+    # penetration-weighted centroid
     lib().oracle_set_hf_band_scale(1.0 if blend else 0.0)
     try:
         rows = _rollout(m, base, cfg, pairs, floor, n_envs, n_steps, seed, rng)
     finally:
-        lib().oracle_set_hf_band_scale(1.0)
+        lib().oracle_set_hf_band_scale(0.0)
     lib().oracle_hfield_axis_wins(wins, 1)
     return _summary(task, rows, wins, blend)
 
@@ -108,11 +108,14 @@ def _summary(task, rows, wins, blend):
 
 def measure_gpu(task: str, n_envs: int, n_steps: int, seed: int = 0, device="cuda:0"):
     """The HIP kernel's contacts (TPhys::collide_hfield, through duck_physics_step's forward) against
-    the brute-force prisms at the same states: oracle rollouts (rough + DR, U(-1,1) actions) give
-    the states; per foot the contact flag and the deepest depth are compared with the brute force,
-    the deepest slot's normal with the oracle's (the declared tie-band blend of the SAT axes, which
-    the brute force's single minimum axis does not make; normal_angle_vs_brute_deg reports that
-    difference too)."""
+    the brute-force prisms and the oracle at the same states: oracle rollouts (rough + DR, U(-1,1)
+    actions) give the states; per foot the contact flag and the deepest depth are compared with the
+    brute force, the deepest slot's normal with the oracle's (normal_angle_vs_brute_deg: against the
+    brute force's single minimum axis), and the contact points with the oracle's declared rule (the
+    penetration-weighted centroid): the deepest slot's point against the oracle
+    slot of the same depth (within HF_DEPTH_TIE) nearest to it, and every active kernel slot against
+    the nearest active oracle slot. band_point_shift_m: how far round 4's point band (the oracle with
+    oracle_set_hf_band_scale(1)) moves the oracle's own deepest point at the same states."""
     import torch
     from open_duck_playground_amd.joystick import Joystick, domain_randomize
     from tests.helpers import parse_aux
@@ -133,7 +136,7 @@ def measure_gpu(task: str, n_envs: int, n_steps: int, seed: int = 0, device="cud
     rng = np.random.default_rng(seed)
     L = envs[0].L
     o = L.off
-    rows = []
+    rows, pts, slot_pts, band = [], [], [], []
     for t in range(n_steps):
         X = np.zeros((n_envs, m.nq + 2 * m.nv + m.nu))
         for e in range(n_envs):
@@ -150,35 +153,56 @@ def measure_gpu(task: str, n_envs: int, n_steps: int, seed: int = 0, device="cud
         torch.cuda.synchronize()
         g = parse_aux(m, aux.cpu().numpy().astype(np.float64))
         for e in range(n_envs):
-            d = models[e].new_data(qpos=X[e, :m.nq], qvel=X[e, m.nq:m.nq + m.nv], ctrl=X[e, sl[3]:],
-                                   warm=X[e, sl[2]:sl[3]])
-            models[e].forward(d)
+            def fwd(scale):
+                lib().oracle_set_hf_band_scale(scale)
+                try:
+                    d = models[e].new_data(qpos=X[e, :m.nq], qvel=X[e, m.nq:m.nq + m.nv], ctrl=X[e, sl[3]:],
+                                           warm=X[e, sl[2]:sl[3]])
+                    models[e].forward(d)
+                finally:
+                    lib().oracle_set_hf_band_scale(0.0)
+                return d
+            d, db = fwd(0.0), fwd(1.0)
             for gid, p in pairs.items():
                 gd = g["con_dist"][e, 4 * p:4 * p + 4]
                 gn = g["con_normal"][e].reshape(-1, 3)[4 * p:4 * p + 4]
+                gp = g["con_pos"][e].reshape(-1, 3)[4 * p:4 * p + 4]
                 dep, nrm = prisms(models[e], d, floor, gid)
                 od = d.arr("con_dist", 4 * m.npair)[4 * p:4 * p + 4]
                 on = np.ctypeslib.as_array(d.con_frame)[4 * p:4 * p + 4, :3]
+                op = np.ctypeslib.as_array(d.con_pos)[4 * p:4 * p + 4]
                 ours = -gd.min()
                 ref = dep.max() if len(dep) else -1.0
                 ang = angb = np.nan
                 if ours > 0 and ref > 0:
-                    n1 = gn[int(np.argmin(gd))] / np.linalg.norm(gn[int(np.argmin(gd))])
+                    k = int(np.argmin(gd))
+                    n1 = gn[k] / np.linalg.norm(gn[k])
                     angb = float(np.degrees(np.arccos(np.clip(n1 @ nrm[int(np.argmax(dep))], -1, 1))))
                     if od.min() < 0:
                         ang = float(np.degrees(np.arccos(np.clip(n1 @ on[int(np.argmin(od))], -1, 1))))
+                        tie = (od < 0) & (np.abs(od - gd[k]) <= 1e-6)
+                        cand = op[tie] if tie.any() else op[[int(np.argmin(od))]]
+                        pts.append(float(np.min(np.linalg.norm(cand - gp[k], axis=1))))
+                        act = op[od < 0]
+                        slot_pts += [float(np.min(np.linalg.norm(act - gp[j], axis=1))) for j in range(4) if gd[j] < 0]
+                        odb = db.arr("con_dist", 4 * m.npair)[4 * p:4 * p + 4]
+                        if odb.min() < 0:
+                            opb = np.ctypeslib.as_array(db.con_pos)[4 * p:4 * p + 4]
+                            band.append(float(np.linalg.norm(opb[int(np.argmin(odb))] - op[int(np.argmin(od))])))
                 rows.append((ours > 0, ref > 0, max(ours, 0.0), max(ref, 0.0), ang, angb))
     a = np.array(rows, dtype=float)
     flag_o, flag_r, dep_o, dep_r, ang, angb = a.T
     both = (flag_o > 0) & (flag_r > 0)
     dd = np.abs(dep_o - dep_r)[both]
-    q = lambda x: {"median": float(np.median(x)), "p99": float(np.quantile(x, 0.99)), "max": float(np.max(x))}  # noqa: E731
-    return {"scene": task, "side": "HIP kernel (fp32) vs brute-force prisms (fp64)", "foot_samples": len(a),
+    q = lambda x: {"median": float(np.median(x)), "p99": float(np.quantile(x, 0.99)), "max": float(np.max(x)),  # noqa: E731
+                   "frac_over_1mm": float(np.mean(np.asarray(x) > 1e-3))}
+    return {"scene": task, "side": "HIP kernel (fp32) vs brute-force prisms / the oracle (fp64)", "foot_samples": len(a),
             "contact_kernel": int(flag_o.sum()), "contact_prism": int(flag_r.sum()),
             "flag_agreement": float((flag_o == flag_r).mean()),
             "flag_disagree_max_depth_m": float(np.max(np.maximum(dep_o, dep_r)[flag_o != flag_r], initial=0.0)),
             "depth_abs_diff_m": q(dd), "normal_angle_deg": q(ang[both & np.isfinite(ang)]),
-            "normal_angle_vs_brute_deg": q(angb[both & np.isfinite(angb)])}
+            "normal_angle_vs_brute_deg": q(angb[both & np.isfinite(angb)]),
+            "deepest_point_m": q(pts), "slot_point_m": q(slot_pts), "band_point_shift_m": q(band)}
 
 
 def main():

@@ -21,8 +21,10 @@ def main():
                 rules.update(rule_of(x))
                 if x["kind"] != "sensitive":
                     bad.append((t, int(e), round(max(x["substep_err"]), 4)))
-        print(f"{case} seed {seed}: good_frac {rep.summary()['good_frac']:.5f} rules {dict(sorted(rules.items()))} "
-              f"unexplained {bad}", flush=True)
+        sm = rep.summary()
+        p99 = {k: f"{sm['err_median_p99_max'][k][1]:.2e}" for k in ("qpos", "qvel", "qacc_warmstart")}
+        print(f"{case} seed {seed}: good_frac {sm['good_frac']:.5f} outliers {sm['outliers']} p99 {p99} "
+              f"rules {dict(sorted(rules.items()))} unexplained {bad}", flush=True)
 
 
 if __name__ == "__main__":
