@@ -166,8 +166,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline sampling (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this job may use")
     ap.add_argument("--strong", action="store_true", help="4096 envs in total over the ranks (strong scaling)")
-    ap.add_argument("--step-mode", default="auto", choices=["auto", "throughput", "latency"],
-                    help="duck_set_step_mode: auto = the latency kernel at <= 4 envs per CU (strong scaling)")
+    ap.add_argument("--step-mode", default="auto", choices=["auto", "throughput", "latency", "paired"],
+                    help="duck_set_step_mode: auto = the latency kernel at <= 4 envs per CU, the paired latency "
+                         "kernel at <= 8 (strong scaling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -286,7 +287,8 @@ def main():
                        "parallelism": f"env-shard x{world}", "step_kernel": env.step_kernel},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "step_kernel" if env.step_kernel == "throughput" else "step_kernel_lat",
+                         "kernel": {"throughput": "step_kernel", "latency": "step_kernel_lat<1>",
+                                    "paired": "step_kernel_lat<2>"}[env.step_kernel],
                          "kernel_ms": kern_ms, "bytes_per_env_step": B},
             "issue_roofline": issue_rf,
             "cpu_baseline": cpu,

@@ -73,14 +73,19 @@ void duck_destroy(duck_sim* sim);
 int duck_reset(duck_sim* sim, int n_envs, float* fstate, int32_t* istate, const uint8_t* mask, uint64_t seed,
                int64_t env_offset, const float* dr, float* obs, float* priv, void* stream);
 
-/* Step kernel selection for duck_step (the same results bit for bit, a different work split):
+/* Step kernel selection for duck_step (the same stage code, a different work split):
  * THROUGHPUT runs 16 envs per workgroup, each env's substeps on one 16-lane team (the batch
  * rate at >= 4 envs per SIMD); LATENCY runs 4 envs per workgroup with each substep's stages
- * split over its waves (a shorter env-step for small batches: strong scaling over GPUs);
- * AUTO (the default) picks LATENCY while n_envs <= 4 x the device's CU count. */
-enum { DUCK_STEP_AUTO = 0, DUCK_STEP_THROUGHPUT = 1, DUCK_STEP_LATENCY = 2 };
+ * split over its 4 waves (the shortest env-step: strong scaling over GPUs, <= 4 envs per CU);
+ * PAIRED runs 8 envs per workgroup, each set of 4 on a pair of waves that split the stages
+ * (the shortest env-step at 4-8 envs per CU: 4,096 envs over 2 GPUs). AUTO (the default) picks
+ * LATENCY while n_envs <= 4 x the device's CU count, PAIRED while n_envs <= 8 x, else THROUGHPUT.
+ * Height-field scenes give the same results bit for bit in every mode; flat scenes agree to fp32
+ * rounding (the compiler contracts some expressions differently in the kernels), so a run's
+ * trajectories depend on the kernel: bench.py and the PPO runner record which one ran. */
+enum { DUCK_STEP_AUTO = 0, DUCK_STEP_THROUGHPUT = 1, DUCK_STEP_LATENCY = 2, DUCK_STEP_PAIRED = 3 };
 int duck_set_step_mode(duck_sim* sim, int mode);
-/* the kernel duck_step would launch for n_envs envs: DUCK_STEP_THROUGHPUT or DUCK_STEP_LATENCY */
+/* the kernel duck_step would launch for n_envs envs: DUCK_STEP_THROUGHPUT, _LATENCY or _PAIRED */
 int duck_step_kernel_for(const duck_sim* sim, int n_envs);
 /* debug: latency-mode event waits that gave up (a broken cross-wave schedule; must stay 0) */
 int duck_debug_lat_timeouts(const duck_sim* sim, unsigned* out, int reset);

@@ -145,7 +145,8 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
   if (cfg->use_imitation && !ref) return duck_fail(DUCK_EINVAL, "use_imitation requires a reference-motion table");
   if (cfg->n_substeps < 1 || cfg->action_max_delay < 1 || cfg->action_max_delay > 3)
     return duck_fail(DUCK_EINVAL, "bad config (n_substeps >= 1, 1 <= action_max_delay <= 3)");
-  if (kVariants[v]->lds_bytes() > 160 * 1024 || kVariants[v]->lds_bytes_lat() > 160 * 1024)
+  if (kVariants[v]->lds_bytes() > 160 * 1024 || kVariants[v]->lds_bytes_lat() > 160 * 1024 ||
+      kVariants[v]->lds_bytes_lat2() > 160 * 1024)
     return duck_fail(DUCK_EUNSUPPORTED, "per-workgroup LDS over 160 KiB");
   // the elevation is uploaded here, not baked (the fingerprint covers nrow / ncol / size only)
   if (kVariants[v]->floor_type == 1 && (!model->hfield_data || model->hfield_nrow < 2 || model->hfield_ncol < 2))
@@ -261,15 +262,14 @@ int duck_physics_step(duck_sim* s, int n, float* qpos, float* qvel, float* warm,
 
 int duck_set_step_mode(duck_sim* s, int mode) {
   g_err.clear();
-  if (!s || mode < DUCK_STEP_AUTO || mode > DUCK_STEP_LATENCY) return duck_fail(DUCK_EINVAL, "bad argument");
+  if (!s || mode < DUCK_STEP_AUTO || mode > DUCK_STEP_PAIRED) return duck_fail(DUCK_EINVAL, "bad argument");
   s->step_mode = mode;
   return DUCK_OK;
 }
 
 int duck_step_kernel_for(const duck_sim* s, int n) {
   if (!s || n < 0) return duck_fail(DUCK_EINVAL, "bad argument");
-  const bool lat = s->step_mode == DUCK_STEP_LATENCY || (s->step_mode == DUCK_STEP_AUTO && n <= LAT_WG_HOST * s->n_cu);
-  return lat ? DUCK_STEP_LATENCY : DUCK_STEP_THROUGHPUT;
+  return step_kernel_choice(s, n);
 }
 
 int duck_device_error(duck_sim* s, unsigned* out, int clear) {

@@ -62,4 +62,15 @@ struct VariantOps {
   int (*stage_cycles)(unsigned long long* out, int reset);
   int (*lat_timeouts)(unsigned* out, int reset);
   size_t (*lds_bytes_lat)();
+  size_t (*lds_bytes_lat2)();
 };
+
+// the step kernel duck_step launches for n envs (DUCK_STEP_THROUGHPUT / _LATENCY / _PAIRED): the mode
+// asked for, or under AUTO the latency kernel while n <= 4 envs per CU, the paired latency kernel
+// while n <= 8 per CU, else the throughput kernel
+inline int step_kernel_choice(const duck_sim* s, int n) {
+  if (s->step_mode != DUCK_STEP_AUTO) return s->step_mode;
+  if (n <= LAT_WG_HOST * s->n_cu) return DUCK_STEP_LATENCY;
+  if (n <= 2 * LAT_WG_HOST * s->n_cu) return DUCK_STEP_PAIRED;
+  return DUCK_STEP_THROUGHPUT;
+}

@@ -60,7 +60,7 @@ DK int local_env(int& lane) {
   return threadIdx.x / TEAM;
 }
 
-template <class Md, bool LAT = false>
+template <class Md, int LAT = 0>
 DK Slice<SW> env_slice(float* lds, int t) {
   return Slice<SW>{(lds_float*)(lds + t * TLay<Md, LAT>::STRIDE)};
 }
@@ -165,7 +165,7 @@ DK void load_dyn(const KArgs& A, int e, Slice<WG> L) {
 }
 
 // load_dyn with the team's lanes: nominal block from the LDS model blob, then the env's DR record
-template <class Md, bool LAT = false>
+template <class Md, int LAT = 0>
 DK void load_dyn_team(const KArgs& A, int e, Slice<SW> L, int lane) {
   using Ly = Lay<Md>;
   using TP = TPhys<Md, LAT>;
@@ -474,7 +474,7 @@ DK StepPre step_prefetch(const KArgs& A, int e, int lane) {
 
 // Joystick.step body for env e (joystick.py:323-481 + wrappers); F = the env's hot state
 // (LDS-staged or the global row), G = the global row (auto-reset snapshot)
-template <class Md, class FA, bool STAGE_OBS, class RT, bool LAT = false>
+template <class Md, class FA, bool STAGE_OBS, class RT, int LAT = 0>
 DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, const Col<0>& G, const RT& r,
                  const StepPre& P) {
   using Ly = Lay<Md>;
@@ -549,12 +549,15 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   float* scr = A.scratch ? A.scratch + e : nullptr;
   STAGE_MARK(29);
   if constexpr (LAT) {
-    // wave 0's share of each substep; waves 1 and 2 run theirs in step_kernel_lat. The env code
-    // below reads the last substep's state and sensors: wait for wave 1's Euler
-    using TPL = TPhys<Md, true>;
+    // wave 0's share of each substep (the paired kernel: wave A's); the other waves run theirs in
+    // step_kernel_lat. The env code below reads the last substep's state and sensors: wait for Euler
+    using TPL = TPhys<Md, LAT>;
     (void)scr;
     LAT_T(43, 5);
-    for (int s = 0; s < c.n_substeps; s++) TPL::lat_r0(L.p, lane, s);
+    for (int s = 0; s < c.n_substeps; s++) {
+      if constexpr (LAT == 2) TPL::lat2_a(L.p, lane, s, A.hfield);
+      else TPL::lat_r0(L.p, lane, s);
+    }
     TPL::ev_wait(TPL::EV_EULER, c.n_substeps);
     LAT_T(44, 5);
   } else {
@@ -884,20 +887,22 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
 // the smooth acceleration (M's factorization and solve). Same stage code and arithmetic as step_kernel, so the
 // results are the same bit for bit (test_gpu_env.py::test_latency_mode_matches_throughput_mode);
 // one env-step of a small batch takes the critical path through the waves instead of the sum.
-template <class Md>
+template <class Md, int LAT>
 __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
-  using TL = TLay<Md, true>;
-  using TPL = TPhys<Md, true>;
-  constexpr int WGL = LAT_WG;
+  using TL = TLay<Md, LAT>;
+  using TPL = TPhys<Md, LAT>;
+  constexpr int WGL = TL::NWG;
   static_assert(TL::TAB_LDS && TL::ES_LDS, "latency mode: the model blob and the hot state in LDS");
-  static_assert(TPB == 4 * 64 && WGL * TEAM == 64, "latency mode: 4 waves, one set of 4 teams per wave");
+  static_assert(TPB == 4 * 64 && WGL * TEAM == 64 * (LAT == 2 ? 2 : 1),
+                "latency modes: 4 waves, one set of 4 teams per wave (paired: per pair of waves)");
   extern __shared__ float lds[];
   LAT_T(40, 5);
   TPL::ev_init((int)threadIdx.x);
-  load_model_tables<Md, true>(lds);  // (ends with a workgroup barrier: the event counters are 0 before any wait)
+  load_model_tables<Md, LAT>(lds);  // (ends with a workgroup barrier: the event counters are 0 before any wait)
   LAT_T(41, 5);
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int t = ((int)threadIdx.x & 63) / TEAM, lane = (int)threadIdx.x % TEAM;
+  // the paired kernel: waves 2w and 2w + 1 work env set w (envs 4w .. 4w + 3 of the workgroup)
+  const int t = (LAT == 2 ? 4 * (wave >> 1) : 0) + ((int)threadIdx.x & 63) / TEAM, lane = (int)threadIdx.x % TEAM;
   const int e = blockIdx.x * WGL + t;
   const int n = A.n;
   const int j = threadIdx.x % WGL, ej = blockIdx.x * WGL + j;
@@ -921,9 +926,10 @@ __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
   __syncthreads();
   LAT_T(42, 5);
   if (e < n) {
-    const Slice<SW> L = env_slice<Md, true>(lds, t);
+    const Slice<SW> L = env_slice<Md, LAT>(lds, t);
     const int ns = A.cfg.n_substeps;
-    if (wave == 0) {
+    float* scr = A.scratch ? A.scratch + e : nullptr;
+    auto env_code = [&]() {
       const Col<0> G{A.fs + e, n};
       lds_float* esp = (lds_float*)(lds + TL::ES + t * TL::ESTRIDE);
       RngTab rt;
@@ -933,15 +939,26 @@ __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
       rt.tab = esp + TL::HOT;
       rt.fill(esp + TL::HOT, lane);
       TSYNC();
-      step_env<Md, LCol, true, RngTab, true>(A, e, lane, L, LCol{esp}, G, rt, P);
+      step_env<Md, LCol, true, RngTab, LAT>(A, e, lane, L, LCol{esp}, G, rt, P);
       LAT_T(45, 5);
-    } else if (wave == 1) {
-      float* scr = A.scratch ? A.scratch + e : nullptr;
-      for (int s = 0; s < ns; s++) TPL::lat_r1(L.p, lane, s, true, s == ns - 1, scr, n);
-    } else if (wave == 2) {
-      for (int s = 0; s < ns; s++) TPL::lat_r2(L.p, lane, s, A.hfield);
+    };
+    if constexpr (LAT == 2) {
+      // the paired kernel: waves 2w (A: the env code and its share of each substep) and 2w + 1 (B)
+      if ((wave & 1) == 0) {
+        env_code();
+      } else {
+        for (int s = 0; s < ns; s++) TPL::lat2_b(L.p, lane, s, true, s == ns - 1, scr, n);
+      }
     } else {
-      for (int s = 0; s < ns; s++) TPL::lat_r3(L.p, lane, s);
+      if (wave == 0) {
+        env_code();
+      } else if (wave == 1) {
+        for (int s = 0; s < ns; s++) TPL::lat_r1(L.p, lane, s, true, s == ns - 1, scr, n);
+      } else if (wave == 2) {
+        for (int s = 0; s < ns; s++) TPL::lat_r2(L.p, lane, s, A.hfield);
+      } else {
+        for (int s = 0; s < ns; s++) TPL::lat_r3(L.p, lane, s);
+      }
     }
   }
   __syncthreads();
@@ -949,8 +966,8 @@ __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
   // a cross-wave wait that gave up: this workgroup's results are not valid. Raise the sticky error
   // word (the next duck_* call on the handle returns DUCK_EDEVICE) and store NaN qpos, which the
   // termination check turns into done, as the reference does for NaN physics (joystick.py:483-485)
-  const bool timed_out = TPL::ev_timed_out();
-  if (timed_out && threadIdx.x == 0 && A.err)
+  const bool timed_out = TPL::ev_timed_out(LAT == 2 ? j / LAT_WG : 0);  // env ej's set
+  if (threadIdx.x == 0 && A.err && (TPL::ev_timed_out(0) || (LAT == 2 && TPL::ev_timed_out(1))))
     __hip_atomic_fetch_or(A.err, (unsigned)DUCK_DEVERR_LAT_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   {
     float hv[NK];
@@ -1043,7 +1060,11 @@ static size_t lds_bytes() {
 }
 template <class Md>
 static size_t lds_bytes_lat() {
-  return (size_t)TLay<Md, true>::LDS_FLOATS * sizeof(float);
+  return (size_t)TLay<Md, 1>::LDS_FLOATS * sizeof(float);
+}
+template <class Md>
+static size_t lds_bytes_lat2() {
+  return (size_t)TLay<Md, 2>::LDS_FLOATS * sizeof(float);
 }
 
 template <class Md>
@@ -1084,13 +1105,18 @@ static int launch_step(duck_sim* s, int n, float* fs, int32_t* is, const float* 
   A.fs = fs; A.is = is; A.dr = dr; A.action = action; A.obs = obs; A.priv = priv;
   A.reward = reward; A.done = done; A.scratch = scratch;
   if (s->lay.first_qpos != TLay<Md>::HOT) return duck_fail(DUCK_EINVAL, "state layout does not match the kernel's hot-state size");
-  // latency mode while the batch leaves at least a CU per 4 envs (each latency workgroup takes a
-  // whole CU: one wave of 512 registers per SIMD), or when asked for
+  // the kernel for this batch (step_kernel_choice: AUTO takes the latency kernel while the batch
+  // leaves a CU per 4 envs, the paired one while it leaves a CU per 8 -- each latency workgroup takes a
+  // whole CU, one wave of 512 registers per SIMD)
   static_assert(LAT_WG == LAT_WG_HOST, "latency workgroup size");
-  const bool lat = s->step_mode == DUCK_STEP_LATENCY || (s->step_mode == DUCK_STEP_AUTO && n <= LAT_WG * s->n_cu);
-  if (lat) {
-    const dim3 grid((A.n + LAT_WG - 1) / LAT_WG), block(TPB);
-    hipLaunchKernelGGL((step_kernel_lat<Md>), grid, block, lds_bytes_lat<Md>(), st, A);
+  const int k = step_kernel_choice(s, n);
+  if (k == DUCK_STEP_LATENCY || k == DUCK_STEP_PAIRED) {
+    const int wgl = k == DUCK_STEP_PAIRED ? 2 * LAT_WG : LAT_WG;
+    const dim3 grid((A.n + wgl - 1) / wgl), block(TPB);
+    if (k == DUCK_STEP_PAIRED)
+      hipLaunchKernelGGL((step_kernel_lat<Md, 2>), grid, block, lds_bytes_lat2<Md>(), st, A);
+    else
+      hipLaunchKernelGGL((step_kernel_lat<Md, 1>), grid, block, lds_bytes_lat<Md>(), st, A);
     HIPCHECK(hipGetLastError());
     return DUCK_OK;
   }
@@ -1155,6 +1181,7 @@ static int stage_cycles_of(unsigned long long* out, int reset) {
     static const VariantOps ops = {#NAME,               matches<MODEL>,         aux_size_of<MODEL>, \
                                    lds_bytes<MODEL>,    MODEL::FLOOR_TYPE,      launch_reset<MODEL>, \
                                    launch_step<MODEL>,  launch_randomize<MODEL>, launch_physics<MODEL>, \
-                                   stage_cycles_of,     lat_timeouts_of,        lds_bytes_lat<MODEL>}; \
+                                   stage_cycles_of,     lat_timeouts_of,        lds_bytes_lat<MODEL>, \
+                                   lds_bytes_lat2<MODEL>};                                              \
     return &ops;                                                                                \
   }

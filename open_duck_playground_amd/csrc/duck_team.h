@@ -165,13 +165,23 @@ static __device__ unsigned int g_lat_timeouts;
   do {                                                                                                      \
     if (blockIdx.x == 0 && ((int)threadIdx.x & 63) == 0 && (s) == 5) g_stage_cycles[DUCK_NSTAGE + (k)] = clock64(); \
   } while (0)
+#define LAT2_T(k, s)               \
+  do {                             \
+    if (threadIdx.x < 128) LAT_T(k, s); \
+  } while (0)
 #else
 #define LAT_T(k, s) \
   do {              \
   } while (0)
+#define LAT2_T(k, s) \
+  do {               \
+  } while (0)
 #endif
 
-template <class Md, bool LAT = false>
+// LAT: 0 = the throughput kernel (one team per env, 16 envs per workgroup); 1 = the latency kernel
+// (4 envs per workgroup, each substep's stages over 4 waves); 2 = the paired latency kernel (8 envs per
+// workgroup, each set of 4 envs on a pair of waves: the stages split over 2 waves)
+template <class Md, int LAT = 0>
 struct TLay {
   using Ly = Lay<Md>;
   // per-lane dump slots (SINK, 2 x TEAM words; debug line-search dumps use 136 words from here)
@@ -197,7 +207,7 @@ struct TLay {
   static constexpr int XDIR = LAT ? ((XSIL + (Md::FLOOR_TYPE == 1 ? 2 * HF_SLSZ : 0) + 3) & ~3) : 0;
   static constexpr int USED = LAT ? XDIR + Md::NV + 4 : USED0;
   static constexpr int STRIDE = ((USED + 15) / 32) * 32 + 16;  // = 16 (mod 32), >= USED
-  static constexpr int NWG = LAT ? LAT_WG : TEAM_WG;          // envs per workgroup
+  static constexpr int NWG = LAT == 2 ? 2 * LAT_WG : (LAT ? LAT_WG : TEAM_WG);  // envs per workgroup
   static_assert(STRIDE >= USED && STRIDE % 32 == 16, "stride");
   // per-lane dump slots for branchless conditional stores (L[ok ? addr : SINK + lane] = v): a
   // lane-divergent `if` leaves a join block whose exec restore the register allocator may put
@@ -217,9 +227,10 @@ struct TLay {
   static constexpr int HOT = Md::NQ + 2 * Md::NV + 8 * Md::NU + 77;
   static constexpr int ESTRIDE = (HOT + 64) | 1;  // + the step's 64 random draws; odd: distinct banks
   static constexpr int ES_FLOATS = ESTRIDE * NWG;
-  // latency mode: the cross-wave event counters, one 16-B word group each, in front of the slices'
-  // end of LDS (LDS_FLOATS counts them)
-  static constexpr int NEV = LAT ? 10 : 0;
+  // latency modes: the cross-wave event counters, one 16-B word group each, in front of the slices'
+  // end of LDS (LDS_FLOATS counts them); NEV_G per set of 4 envs (the paired kernel has two sets)
+  static constexpr int NEV_G = LAT ? 10 : 0;
+  static constexpr int NEV = LAT == 2 ? 2 * NEV_G : NEV_G;
   static constexpr size_t LDS_MAX = 160 * 1024 / 4 - 4 * NEV;
   // LDS priority: model blob (read every substep), then the hot state (read once per env-step)
   static constexpr bool TAB_LDS = (size_t)(TAB + Md::NBLOB) <= LDS_MAX;
@@ -239,7 +250,7 @@ struct TLay {
 };
 
 // copy the model blob into the workgroup's LDS (before any thread of the block exits)
-template <class Md, bool LAT = false>
+template <class Md, int LAT = 0>
 DK void load_model_tables(float* lds) {
   using TLy = TLay<Md, LAT>;
   if constexpr (TLy::TAB_LDS) {
@@ -301,7 +312,7 @@ struct HullFaceOrder {
   }
 };
 
-template <class Md, bool LAT = false>
+template <class Md, int LAT = 0>
 struct TPhys {
   using Ly = Lay<Md>;
   using TL = TLay<Md, LAT>;
@@ -1369,7 +1380,11 @@ struct TPhys {
 
   // plane floor vs hull for both feet at once (mjx collision_convex.plane_convex): lanes 0-7 take
   // the first floor pair, 8-15 the second
+#ifdef DUCK_PLANE_NOINLINE
+  static __device__ __noinline__ void collide_planes(LP L, int lane) {
+#else
   static DK void collide_planes(LP L, int lane) {
+#endif
 #ifdef DUCK_PLANE_NO_CONTRACT
 #pragma clang fp contract(off)
 #endif
@@ -3327,13 +3342,16 @@ struct TPhys {
   // handle's sticky device error word and writes NaN qpos for the workgroup's envs (duck_device_error)
   enum { EV_KIN = 0, EV_VEL = 1, EV_FSM = 2, EV_ROWS = 3, EV_EULER = 4, EV_M = 5, EV_QSM = 6, EV_WA = 7, EV_DIR = 8,
          EV_TIMEOUT = 9 };
-  static_assert(EV_TIMEOUT < TL::NEV || !LAT, "event slots");
+  static_assert(EV_TIMEOUT < TL::NEV_G || !LAT, "event slots");
+  // the paired kernel (LAT 2): waves 2w and 2w + 1 work env set w, whose events are its own group
   static DK lds_int* ev_ptr(int k) {
     extern __shared__ float lds_dyn[];
-    return (lds_int*)(lds_dyn + TL::EV) + 4 * k;
+    const int g = LAT == 2 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 7) : 0;
+    return (lds_int*)(lds_dyn + TL::EV) + 4 * (k + TL::NEV_G * g);
   }
   static DK void ev_init(int tid) {
-    if (tid < TL::NEV) ev_ptr(tid)[0] = 0;
+    extern __shared__ float lds_dyn[];
+    if (tid < TL::NEV) ((lds_int*)(lds_dyn + TL::EV))[4 * tid] = 0;
   }
   static DK void ev_signal(int k, int v) {
     __hip_atomic_store(ev_ptr(k), v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3357,8 +3375,10 @@ struct TPhys {
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  static DK bool ev_timed_out() {
-    return __hip_atomic_load(ev_ptr(EV_TIMEOUT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+  // did a wait of env set g give up (after the final barrier: every wave's waits are over)
+  static DK bool ev_timed_out(int g) {
+    extern __shared__ float lds_dyn[];
+    return ((lds_int*)(lds_dyn + TL::EV))[4 * (EV_TIMEOUT + TL::NEV_G * g)] != 0;
   }
   // wave 0, substep s: kinematics and com_pos (everything else waits for them), rne's velocities
   // (the contact rows need the feet's), then the rest of rne and the actuation (qfrc_smooth)
@@ -3459,5 +3479,98 @@ struct TPhys {
     TSYNC();
     ev_signal(EV_DIR, s + 1);
     LAT_T(35, s);
+  }
+
+  // ---------------- paired latency mode: one substep over two waves (step_kernel_lat<Md, 2>) ----------------
+  // The same stages, events and scratch regions as the four-wave split (lat_r0 .. lat_r3), folded
+  // onto two waves so that 8 envs per workgroup fill the chip at 2,048 envs (one wave per SIMD):
+  // wave A (the env code's wave) takes kinematics, com_pos, rne and the actuation, then collision and
+  // the constraint rows, then the speculative Newton direction at qacc_warmstart; wave B takes the
+  // composite inertias, crb, M's register columns, the warm start's qacc_warmstart products, M's
+  // factorization, the smooth solve, the rest of the warm start, the Newton step and line search,
+  // sensors and Euler. Each wave's stages run in the order of their inputs, so B's chain is the
+  // critical path: kinematics (A) -> crb -> ... -> the rows (A) -> warm start -> line search -> Euler.
+  static DK void lat2_a(LP L, int lane, int s, const float* hf) {
+    ev_wait(EV_EULER, s);
+    LAT2_T(0, s);
+    kinematics(L, lane);
+    com_pos(L, lane);
+    ev_signal(EV_KIN, s + 1);
+    LAT2_T(1, s);
+    rne_vel(L, lane);
+    LAT2_T(2, s);
+    rne_rest<1>(L, lane);
+    smooth(L, lane);
+    ev_signal(EV_FSM, s + 1);
+    LAT2_T(3, s);
+    collision(L, lane, hf);
+    LAT2_T(4, s);
+    make_rows(L, lane);
+    ev_signal(EV_ROWS, s + 1);
+    LAT2_T(5, s);
+    // the Newton direction at qacc_warmstart, speculatively (B takes it when every team of the wave
+    // starts there): M's columns from B's crb, the rows' values there and M qacc_warmstart from B's
+    // warm start
+    ev_wait(EV_M, s + 1);
+    LAT2_T(6, s);
+    float Mc[NC][NV];
+    load_cols(L, lane, Mc, false);
+    ev_wait(EV_WA, s + 1);
+    LAT2_T(7, s);
+    const bool ok = newton_fused<false, TL::XDIR>(L, lane, Mc);
+    if (lane == 0) L[TL::XDIR + NV] = ok ? 1.0f : 0.0f;
+    TSYNC();
+    ev_signal(EV_DIR, s + 1);
+    LAT2_T(8, s);
+  }
+  static DK void lat2_b(LP L, int lane, int s, bool integrate, bool want_out, float* scratch, int sstride) {
+    ev_wait(EV_KIN, s + 1);
+    LAT2_T(10, s);
+    subtree_sums<2>(L, lane);
+    crb(L, lane);
+    ev_signal(EV_M, s + 1);
+    LAT2_T(11, s);
+    {
+      float Mc[NC][NV];
+      load_cols(L, lane, Mc, false);
+      LAT2_T(12, s);
+      float SL[6], SR[6], cwp;
+      warm_start_a0(L, lane, Mc, SL, SR);
+      LAT2_T(13, s);
+      {
+        Fac F;
+        smooth_factor(F, lane, Mc);
+        LAT2_T(14, s);
+        ev_wait(EV_FSM, s + 1);
+        LAT2_T(15, s);
+        smooth_solve(L, lane, F);
+        LAT2_T(16, s);
+      }
+      ev_wait(EV_ROWS, s + 1);
+      LAT2_T(17, s);
+      warm_start_a1(L, lane, SL, SR, cwp);
+      ev_signal(EV_WA, s + 1);
+      LAT2_T(18, s);
+      bool warm;
+      const float g0 = warm_start_b(L, lane, cwp, warm);
+      LAT2_T(19, s);
+      bool pre = false;
+      if (__ballot(!warm) == 0ull) {
+        ev_wait(EV_DIR, s + 1);
+        pre = L[TL::XDIR + NV] != 0.0f;
+      }
+      LAT2_T(20, s);
+      newton(L, lane, scratch, sstride, Mc, g0, pre);
+      LAT2_T(21, s);
+    }
+    if (want_out) sensors(L, lane);
+    if (integrate) {
+      euler(L, lane);
+    } else {
+      for (int i = lane; i < NV; i += TEAM) L[Ly::WARM + i] = L[Ly::QACC + i];
+      TSYNC();
+    }
+    LAT2_T(22, s);
+    ev_signal(EV_EULER, s + 1);
   }
 };

@@ -43,8 +43,13 @@ class BaseRunner:
 
     def progress_callback(self, num_steps: int, metrics: dict) -> None:
         os.makedirs(self.output_dir, exist_ok=True)
+        # which step kernel ran (include/duck.h DUCK_STEP_*): flat-scene trajectories depend on it at fp32
+        # rounding, so a run is reproduced on the same kernel
+        kernels = {"train": getattr(self.env, "step_kernel", None)}
+        if self.eval_env is not None:
+            kernels["eval"] = getattr(self.eval_env, "step_kernel", None)
         with open(self.output_dir / "metrics.jsonl", "a") as f:
-            f.write(json.dumps({"step": num_steps, **metrics}) + "\n")
+            f.write(json.dumps({"step": num_steps, **metrics, "step_kernel": kernels}) + "\n")
         if "eval/episode_reward" in metrics:
             print("-----------")
             print(f'STEP: {num_steps} reward: {metrics["eval/episode_reward"]} '

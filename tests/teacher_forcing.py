@@ -256,6 +256,11 @@ CASES = {
                                    step_mode="throughput"),
     "rough_backlash_dr_throughput_kernel": dict(task="rough_terrain_backlash", imitation=False, dr=True,
                                                 force_push=True, step_mode="throughput"),
+    # the paired latency kernel (each substep's stages over a pair of waves per 4 envs)
+    "flat_paired_kernel": dict(task="flat_terrain", imitation=True, force_push=True, force_resample=True,
+                               step_mode="paired"),
+    "rough_backlash_dr_paired_kernel": dict(task="rough_terrain_backlash", imitation=False, dr=True,
+                                            force_push=True, step_mode="paired"),
 }
 
 

@@ -184,10 +184,14 @@ def test_full_size_runs_are_deterministic(cfg, gpu):
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("cfg,n", [("C2", 512), ("C3", 1021), ("C4", 1024), ("C5", 510)])
-def test_latency_mode_matches_throughput_mode(cfg, n, gpu):
+@pytest.mark.parametrize("cfg,n,mode", [("C2", 512, "latency"), ("C3", 1021, "latency"), ("C4", 1024, "latency"),
+                                        ("C5", 510, "latency"), ("C2", 2048, "paired"), ("C3", 1021, "paired"),
+                                        ("C4", 2044, "paired"), ("C5", 2048, "paired")])
+def test_latency_mode_matches_throughput_mode(cfg, n, mode, gpu):
     """The latency kernel (each substep's stages split over four waves per 4 envs, DUCK_STEP_LATENCY)
-    runs the same stage code on the same data as the throughput kernel (one team per env). Every
+    and the paired latency kernel (the stages over a pair of waves per 4 envs, 8 envs per workgroup,
+    DUCK_STEP_PAIRED) run the same stage code on the same data as the throughput kernel (one team per
+    env). Every
     env-step is taken by both kernels from the same state (the throughput kernel's), over auto-resets
     (5-step episodes), DR, and a batch with a partial workgroup (n % 4 != 0). Height-field scenes: bit
     for bit. Flat scenes: the compiler contracts a few fp32 expressions of the inlined plane collision
@@ -202,13 +206,13 @@ def test_latency_mode_matches_throughput_mode(cfg, n, gpu):
     g = torch.Generator(device=gpu)
     g.manual_seed(11)
     envs = {}
-    for mode in ("throughput", "latency"):
+    for m in ("throughput", mode):
         env = wrap_for_brax_training(Joystick(c["task"], num_envs=n, device=gpu, use_imitation=c["imitation"]),
                                      episode_length=5, randomization_fn=domain_randomize if c["dr"] else None)
-        env.set_step_mode(mode)
-        assert env.step_kernel == mode
+        env.set_step_mode(m)
+        assert env.step_kernel == m
         env.lat_timeouts(reset=True)
-        envs[mode] = env
+        envs["latency" if m == mode else m] = env
     st = envs["throughput"].reset(rng=4)
     L = envs["throughput"]._layout
     nq = envs["throughput"].mj_model.nq
@@ -237,20 +241,22 @@ def test_latency_mode_matches_throughput_mode(cfg, n, gpu):
     assert envs["latency"].lat_timeouts() == 0
 
 
-def test_latency_timeout_surfaces(gpu, monkeypatch):
+@pytest.mark.parametrize("mode,wg_envs", [("latency", 4), ("paired", 8)])
+def test_latency_timeout_surfaces(mode, wg_envs, gpu, monkeypatch):
     """A latency-kernel launch whose cross-wave wait gives up is not silent: the test build
-    (native.debug_library "force_timeout", -DDUCK_LAT_FORCE_TIMEOUT: wave 3 of workgroup 1 never sees
-    its M event and gives up after a few polls) sets the handle's sticky device error word, writes NaN
-    qpos for workgroup 1's envs (4..7) and only those, and the next step raises DuckError (DUCK_EDEVICE)
-    until the word is cleared. The shipped library's word stays 0 over the same steps."""
+    (native.debug_library "force_timeout", -DDUCK_LAT_FORCE_TIMEOUT: in workgroup 1 the waits for the
+    M event never see it and give up after a few polls) sets the handle's sticky device error word,
+    writes NaN qpos for workgroup 1's envs (4..7 in the latency kernel, 8..15 in the paired one) and
+    only those, and the next step raises DuckError (DUCK_EDEVICE) until the word is cleared. The
+    shipped library's word stays 0 over the same steps."""
     import os
     from open_duck_playground_amd import joystick as jmod
     from open_duck_playground_amd.native import BUILD, DuckError
     path = os.path.join(BUILD, "libduck_force_timeout.so")
     assert os.path.exists(path), "built by __graft_entry__.build()"
-    n = 16
+    n = 4 * wg_envs
     ok = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
-    ok.set_step_mode("latency")
+    ok.set_step_mode(mode)
     st = ok.reset(rng=1)
     for _ in range(2):
         st = ok.step(st, torch.zeros(n, 14, device=gpu))
@@ -258,7 +264,7 @@ def test_latency_timeout_surfaces(gpu, monkeypatch):
     assert ok.device_error() == 0
     monkeypatch.setattr(jmod, "model_library", lambda m: path)
     env = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
-    env.set_step_mode("latency")
+    env.set_step_mode(mode)
     st = env.reset(rng=1)
     st = env.step(st, torch.zeros(n, 14, device=gpu))
     torch.cuda.synchronize()
@@ -266,7 +272,8 @@ def test_latency_timeout_surfaces(gpu, monkeypatch):
     L = env._layout
     q = st.fstate.view(L.nfloat, n)[L.off["qpos"]:L.off["qpos"] + env.mj_model.nq]
     bad = torch.isnan(q).any(dim=0).cpu().numpy()
-    assert bad[4:8].all() and not bad[:4].any() and not bad[8:].any(), bad
+    w = wg_envs
+    assert bad[w:2 * w].all() and not bad[:w].any() and not bad[2 * w:].any(), bad
     with pytest.raises(DuckError, match="device error word"):
         env.step(st, torch.zeros(n, 14, device=gpu))
     assert env.device_error(clear=True) == 1 and env.device_error() == 0
@@ -274,9 +281,10 @@ def test_latency_timeout_surfaces(gpu, monkeypatch):
 
 
 def test_step_mode_auto_selects_by_batch(gpu):
-    """AUTO: the latency kernel while the batch leaves a CU per 4 envs, the throughput kernel above."""
+    """AUTO: the latency kernel while the batch leaves a CU per 4 envs, the paired latency kernel while
+    it leaves a CU per 8, the throughput kernel above."""
     ncu = torch.cuda.get_device_properties(gpu).multi_processor_count
-    for n, want in ((4 * ncu, "latency"), (4 * ncu + 1, "throughput")):
+    for n, want in ((4 * ncu, "latency"), (4 * ncu + 1, "paired"), (8 * ncu, "paired"), (8 * ncu + 1, "throughput")):
         env = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
         assert env.step_kernel == want, (n, ncu)
 

@@ -24,6 +24,14 @@ NAMES = {0: "w0 start (Euler of s-1 seen)", 1: "w0 kinematics+com_pos done", 2: 
          20: "w2 com_pos seen", 21: "w2 collision done", 22: "w2 rne velocities seen", 23: "w2 rows done",
          30: "w3 crb seen", 31: "w3 M factored", 32: "w3 qfrc_smooth seen", 33: "w3 qacc_smooth done",
          34: "w3 warm start's rows seen", 35: "w3 speculative Newton direction done", 19: "w1 direction seen"}
+# the paired kernel (step_kernel_lat<Md, 2>: waves A and B of env set 0 in workgroup 0)
+NAMES2 = {0: "A start (Euler of s-1 seen)", 1: "A kinematics+com_pos done", 2: "A rne velocities done",
+          3: "A rne + actuation done (qfrc_smooth)", 4: "A collision done", 5: "A rows done", 6: "A crb seen",
+          7: "A warm start's rows seen", 8: "A speculative Newton direction done",
+          10: "B com_pos seen", 11: "B composite inertias + crb done", 12: "B M columns loaded",
+          13: "B warm start (qacc_warmstart products) done", 14: "B M factored", 15: "B qfrc_smooth seen",
+          16: "B qacc_smooth done", 17: "B rows seen", 18: "B warm start's rows done", 19: "B warm start done",
+          20: "B direction seen / own", 21: "B Newton + line search done", 22: "B Euler done"}
 LAUNCH = {40: "kernel start", 41: "model blob in LDS", 42: "hot state staged", 43: "w0 env code before the substeps done",
           44: "w0 last Euler seen", 45: "w0 env code after the substeps done", 46: "final barrier"}
 NSTAGE = 56
@@ -34,12 +42,13 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--envs", type=int, default=512)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--mode", default="latency", choices=["latency", "paired"])
     a = ap.parse_args()
     c = CONFIGS[a.config]
     dev = torch.device("cuda:0")
     env = wrap_for_brax_training(Joystick(c["task"], num_envs=a.envs, device=dev, use_imitation=c["imitation"]),
                                  episode_length=1000, randomization_fn=domain_randomize if c["dr"] else None)
-    env.set_step_mode("latency")
+    env.set_step_mode(a.mode)
     st = env.reset(rng=0)
     g = torch.Generator(device=dev)
     g.manual_seed(1)
@@ -64,9 +73,10 @@ def main():
     for k in sorted(LAUNCH):
         print(f"{r[k]:9.0f}  {LAUNCH[k]}")
     print("substep 5:")
-    for k in sorted(NAMES, key=lambda k: r[k]):
-        print(f"{r[k]:9.0f}  {NAMES[k]}")
-    print(f"substep (w0 start -> w1 Euler): {r[18]:.0f} cycles")
+    names, last = (NAMES, 18) if a.mode == "latency" else (NAMES2, 22)
+    for k in sorted(names, key=lambda k: r[k]):
+        print(f"{r[k]:9.0f}  {names[k]}")
+    print(f"substep (start -> Euler): {r[last]:.0f} cycles")
     # per-stage cycles (STAGE_MARK sums, workgroup 0), per substep
     from stage_prof import ENV, SUB, TOP  # noqa: E402
     names = {**TOP, **SUB, **ENV}
