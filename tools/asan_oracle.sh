@@ -5,5 +5,5 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 make -s -C oracle ASAN=1
-LD_PRELOAD=$(gcc -print-file-name=libasan.so) ORACLE_LIB=$PWD/oracle/liboracle_asan.so ASAN_OPTIONS=detect_leaks=0 \
+LD_PRELOAD=$(gcc -print-file-name=libasan.so)${LD_PRELOAD:+:$LD_PRELOAD} ORACLE_LIB=$PWD/oracle/liboracle_asan.so ASAN_OPTIONS=detect_leaks=0 \
   python -m pytest tests -m "not gpu" -q -p no:cacheprovider "$@"

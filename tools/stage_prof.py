@@ -93,6 +93,10 @@ def main():
         print(f"{'hfield pass-2 iterations':28s} {buf[48] / (nwg * steps * 10):10.2f} per substep (wave 0: the most crossing pairs of a lane)")
         print(f"{'hfield crossing pairs':28s} {buf[49] / (nwg * steps * 10):10.2f} per substep (wave 0: all survivors)")
         print(f"{'hfield crossing edges':28s} {buf[50] / (nwg * steps * 10):10.2f} per substep (wave 0: hull edges crossing in any survivor)")
+        hist = [buf[k] for k in range(51, 56)]
+        if sum(hist):
+            print(f"{'hfield survivors per wave':28s} " + ", ".join(
+                f"{lab}: {100 * v / sum(hist):.1f} %" for lab, v in zip(("<=21", "22-32", "33-42", "43-64", ">64"), hist)))
     outside = per(14) + sum(per(k) for k in ENV)
     kern = outside + tot / (nwg * steps)
     if per(14) == 0:
