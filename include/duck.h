@@ -80,9 +80,9 @@ int duck_reset(duck_sim* sim, int n_envs, float* fstate, int32_t* istate, const 
  * PAIRED runs 8 envs per workgroup, each set of 4 on a pair of waves that split the stages
  * (the shortest env-step at 4-8 envs per CU: 4,096 envs over 2 GPUs). AUTO (the default) picks
  * LATENCY while n_envs <= 4 x the device's CU count, PAIRED while n_envs <= 8 x, else THROUGHPUT.
- * Height-field scenes give the same results bit for bit in every mode; flat scenes agree to fp32
- * rounding (the compiler contracts some expressions differently in the kernels), so a run's
- * trajectories depend on the kernel: bench.py and the PPO runner record which one ran. */
+ * Every mode gives the same results bit for bit (every scene; tests/test_gpu_env.py), so a run's
+ * trajectories do not depend on the batch size or the GPU count that picked the kernel; bench.py
+ * and the PPO runner still record which kernel ran. */
 enum { DUCK_STEP_AUTO = 0, DUCK_STEP_THROUGHPUT = 1, DUCK_STEP_LATENCY = 2, DUCK_STEP_PAIRED = 3 };
 int duck_set_step_mode(duck_sim* sim, int mode);
 /* the kernel duck_step would launch for n_envs envs: DUCK_STEP_THROUGHPUT, _LATENCY or _PAIRED */

@@ -1380,14 +1380,7 @@ struct TPhys {
 
   // plane floor vs hull for both feet at once (mjx collision_convex.plane_convex): lanes 0-7 take
   // the first floor pair, 8-15 the second
-#ifdef DUCK_PLANE_NOINLINE
-  static __device__ __noinline__ void collide_planes(LP L, int lane) {
-#else
   static DK void collide_planes(LP L, int lane) {
-#endif
-#ifdef DUCK_PLANE_NO_CONTRACT
-#pragma clang fp contract(off)
-#endif
     constexpr int NH = Md::NHV;
     const int h = lane >> 3, sub = lane & 7;
     const int p = Md::PLANE_PAIR[0] * (1 - h) + Md::PLANE_PAIR[1] * h;
@@ -1843,223 +1836,6 @@ struct TPhys {
 #endif
   }
 
-  // hf_exec with three lanes per queue entry (collide_hfield takes this form when the wave's survivors fit
-  // 21 entries, three lanes each): lanes 3g .. 3g + 2 work entry g, lane kq with the prism's top edge kq in
-  // the top-edge pairs (pass 1 and pass 2: a third of the pairs per lane) and its top vertex kq inside the
-  // hull, every third entry of the silhouette list; the overlaps are combined by the lexicographic minimum
-  // over (overlap, axis priority), the prism vertices' weights summed in hf_exec's order, so the results
-  // are hf_exec's bit for bit (the three lanes share the hull-face axes and the hull vertices' weights).
-  static DK void hf_exec3(lds_float* E, LP L, int tw, int kq) {
-    STAGE_T0();
-    constexpr int NH = Md::NHV, NF = Md::NHF, NE = Md::NHE;
-    static_assert(NE <= 64, "one 64-bit pair mask per prism edge");
-    constexpr float DXC = 2.0f * Md::HF_SIZE[0] / (Md::HF_NCOL - 1), DYC = 2.0f * Md::HF_SIZE[1] / (Md::HF_NROW - 1);
-    const float GN = 1.0f / sqrtf(DXC * DXC + DYC * DYC);
-    const float GX = DYC * GN, GY = DXC * GN;
-    lds_f4* E4 = (lds_f4*)E;
-    const f4v d0 = E4[0], d1 = E4[1], d2 = E4[2], d3 = E4[3], d4 = E4[4], d5 = E4[5], d6 = E4[6];
-    const float Tm[3][3] = {{d0.x, d0.y, d0.z}, {d1.x, d1.y, d1.z}, {d2.x, d2.y, d2.z}};
-    const float base = d0.w;
-    float mo = d1.w;
-    int mp = __float_as_int(d2.w);
-    const int tag = __float_as_int(d3.w), tri = tag & 1, foot = tag >> 1;
-    const float ntm[3] = {d3.x, d3.y, d3.z}, zc[3] = {d4.x, d4.y, d4.z};
-    const float xc[3] = {d5.x, d5.y, d5.z}, yc[3] = {d6.x, d6.y, d6.z};
-    float sm[3][3];
-    {
-      const float sx0 = tri ? -GX : -1.0f, sx1 = tri ? 1.0f : GX;
-      const float sy0 = tri ? -GY : 0.0f, sy1 = tri ? 0.0f : GY, sy2 = tri ? 1.0f : -1.0f;
-      for (int a = 0; a < 3; a++) {
-        sm[0][a] = sx0 * xc[a] + sy0 * yc[a];
-        sm[1][a] = sx1 * xc[a] + sy1 * yc[a];
-        sm[2][a] = 0.0f * xc[a] + sy2 * yc[a];
-      }
-    }
-    auto side = [&](int k, float* o) {  // side normal k (opaque selects, as hf_exec)
-      const unsigned long long m0 = __ballot(k == 0), m1 = __ballot(k == 1);
-      for (int a = 0; a < 3; a++) o[a] = vsel(m0, sm[0][a], vsel(m1, sm[1][a], sm[2][a]));
-    };
-    // this lane's prism edge: side normal, top vertex kq and the edge to vertex kq + 1
-    float sk[3], tmk[3], emk[3];
-    {
-      const unsigned long long m0 = __ballot(kq == 0), m1 = __ballot(kq == 1);
-      for (int a = 0; a < 3; a++) {
-        sk[a] = vsel(m0, sm[0][a], vsel(m1, sm[1][a], sm[2][a]));
-        tmk[a] = vsel(m0, Tm[0][a], vsel(m1, Tm[1][a], Tm[2][a]));
-        emk[a] = vsel(m0, Tm[1][a], vsel(m1, Tm[2][a], Tm[0][a])) - tmk[a];
-      }
-    }
-    // the hull's faces (every lane of the three: hf_exec's loop)
-    {
-      const float hk[3] = {d4.w - base, d5.w - base, d6.w - base};
-      static_for<0, NF>([&](auto fI) {
-        constexpr int f = fI.value;
-        const float nz = fmaxf(nf_dot<f>(zc), 0.0f);
-        float pf = nf_dot<f>(Tm[0]) - hk[0] * nz;
-        pf = fminf(pf, nf_dot<f>(Tm[1]) - hk[1] * nz);
-        pf = fminf(pf, nf_dot<f>(Tm[2]) - hk[2] * nz);
-        const float ov = nf_off_minus<f>(pf);
-        const bool b = (ov < mo) | ((ov == mo) & (5 + f < mp));
-        mo = b ? ov : mo;
-        mp = b ? 5 + f : mp;
-      });
-    }
-    float mu[3] = {0.0f, 0.0f, 0.0f};
-    auto take = [&](float ov, int pr, const float* u) {
-      const bool b = (ov < mo) | ((ov == mo) & (pr < mp));
-      mo = b ? ov : mo;
-      mp = b ? pr : mp;
-      for (int a = 0; a < 3; a++) mu[a] = b ? u[a] : mu[a];
-    };
-    // vertical-edge pairs: every third entry of the foot's silhouette list
-    {
-      const lds_float* SL = L + ((foot >> 1) - tw) * TL::STRIDE + HF_CINQ + (foot & 1) * HF_SLSZ;
-      const int n = ((const lds_int*)SL)[0];
-      for (int i = kq; i < n; i += 3) {
-        const int e = ((const lds_int*)SL)[1 + i];
-        const f4v w = ((const lds_f4*)(SL + HF_SLF))[i];
-        const float wv[3] = {w.x, w.y, w.z};
-        const float q0 = dot3(wv, Tm[0]), q1 = dot3(wv, Tm[1]), q2 = dot3(wv, Tm[2]);
-        const int kk = q0 >= q1 ? (q0 >= q2 ? 0 : 2) : (q1 >= q2 ? 1 : 2);
-        take(fmaxf(q0, fmaxf(q1, q2)) - w.w, HF_PRIO_V + 3 * e + kk, wv);
-      }
-    }
-    STAGE_MARK(44);
-    // pass 1 for prism edge kq: bit e of pm when hull edge e's arc crosses (hf_exec's products)
-    unsigned long long pm = 0ull;
-    {
-      float hxk[3];
-      cross3(hxk, sk, ntm);
-      float phi[NF];
-      static_for<0, NF>([&](auto fI) { phi[fI.value] = nf_dot<fI.value>(hxk); });
-      static_for<0, NE>([&](auto eI) {
-        constexpr int e = eI.value, fa = Md::hull_edge_face[e][0], fb = Md::hull_edge_face[e][1];
-        const float ADC = dxc_dot<e>(ntm);
-        const float BDC = dxc_dot<e>(sk);
-        const float mx = fmaxf(fmaxf(phi[fa] * phi[fb], ADC * BDC), phi[fa] * BDC);
-        pm |= (unsigned long long)(__float_as_uint(mx) >> 31) << e;
-      });
-    }
-    STAGE_MARK(45);
-    // pass 2: each crossing pair's overlap along ev x em
-    while (pm) {
-      const int e = __builtin_ctzll(pm);
-      pm &= pm - 1ull;
-      const int o = Md::B_HEDGE + 20 * e;
-      const f4v ev4 = ht4(o + 12), v04 = ht4(o + 16);
-      const float ev[3] = {ev4.x, ev4.y, ev4.z}, v0[3] = {v04.x, v04.y, v04.z};
-      float u[3];
-      cross3(u, ev, emk);
-      const float u2 = dot3(u, u);
-      const float sg = (dot3(u, ntm) + dot3(u, sk) < 0.0f ? -1.0f : 1.0f) * __builtin_amdgcn_rsqf(u2);
-      const float un[3] = {sg * u[0], sg * u[1], sg * u[2]};
-      const float ov = u2 >= 1e-12f * ev4.w * dot3(emk, emk) ? sg * (dot3(u, tmk) - dot3(u, v0)) : 1e30f;
-      take(ov, HF_PRIO_T + 3 * e + kq, un);
-    }
-    STAGE_MARK(47);
-    // the three lanes' minima combined: the lexicographic minimum over (overlap, priority)
-    const int b0 = ((int)threadIdx.x & 63) - kq;
-    {
-      float cm = 1e30f, cu[3] = {0.0f, 0.0f, 0.0f};
-      int cp = 1 << 30;
-#pragma unroll
-      for (int j = 0; j < 3; j++) {
-        const int src = b0 + j;
-        const float oj = __shfl(mo, src, 64);
-        const int pj = __shfl(mp, src, 64);
-        const float uj[3] = {__shfl(mu[0], src, 64), __shfl(mu[1], src, 64), __shfl(mu[2], src, 64)};
-        const bool b = (oj < cm) | ((oj == cm) & (pj < cp));
-        cm = b ? oj : cm;
-        cp = b ? pj : cp;
-        for (int a = 0; a < 3; a++) cu[a] = b ? uj[a] : cu[a];
-      }
-      mo = cm;
-      mp = cp;
-      for (int a = 0; a < 3; a++) mu[a] = cu[a];
-    }
-    if (!(mo > 0.0f)) {
-      if (kq == 0) E4[0] = f4v{-1.0f, 0.0f, 0.0f, 0.0f};
-      return;
-    }
-    // the screen's axes: the prism's top, sides, bottom or a hull face
-    if (mp < HF_PRIO_T) {
-      const int f = mp - 5;
-      const f4v n4 = ht4(Md::B_HFACE + 4 * (f > 0 ? f : 0));
-      const float nf[3] = {-n4.x, -n4.y, -n4.z};
-      float sv[3];
-      side(mp - 1, sv);
-      for (int a = 0; a < 3; a++) mu[a] = mp == 0 ? ntm[a] : (mp < 4 ? sv[a] : (mp == 4 ? -zc[a] : nf[a]));
-    }
-    // the contact point: the hull's vertices inside the prism (every lane of the three), then this
-    // lane's prism top vertex inside the hull, the three weights summed in hf_exec's order
-    const float ptop = dot3(ntm, Tm[0]);
-    const float smt[3] = {dot3(sm[0], Tm[0]), dot3(sm[1], Tm[1]), dot3(sm[2], Tm[2])};
-    float W = 0.0f, Cx[3] = {0.0f, 0.0f, 0.0f};
-    static_for<0, NH>([&](auto kI) {
-      constexpr int k = kI.value;
-      const float atop = ptop - hv_dot<k>(ntm);
-      float pen = fminf(atop, hv_dot<k>(zc) - base);
-      for (int j = 0; j < 3; j++) pen = fminf(pen, smt[j] - hv_dot<k>(sm[j]));
-      const float w = fmaxf(pen, 0.0f);
-      W += w;
-      Cx[0] = cfma<fbits(Md::hull_vert[k][0])>(w, Cx[0]);
-      Cx[1] = cfma<fbits(Md::hull_vert[k][1])>(w, Cx[1]);
-      Cx[2] = cfma<fbits(Md::hull_vert[k][2])>(w, Cx[2]);
-    });
-    {
-      // (the wave-uniform early-outs of hf_exec: the same vertices, one per lane instead of three)
-      float pk = 1e30f;
-      bool live = true;
-      static_for<0, NF>([&](auto pI) {
-        constexpr int pos = pI.value;
-        constexpr int f = HullFaceOrder<Md>{}.f[pos];
-        if (pos == 6 || pos == 14) live = live && __ballot(pk > 0.0f) != 0ull;
-        if (!live) return;
-        pk = fminf(pk, nf_off_minus<f>(nf_dot<f>(tmk)));
-      });
-      const float wk = fmaxf(pk, 0.0f);
-      const float wj[3] = {__shfl(wk, b0, 64), __shfl(wk, b0 + 1, 64), __shfl(wk, b0 + 2, 64)};
-#pragma unroll
-      for (int j = 0; j < 3; j++) {
-        W += wj[j];
-        for (int a = 0; a < 3; a++) Cx[a] += wj[j] * Tm[j][a];
-      }
-    }
-    float pos[3];
-    if (W > 0.0f) {
-      const float iw = 1.0f / W;
-      for (int a = 0; a < 3; a++) pos[a] = Cx[a] * iw;
-    } else {
-      float hmu = 1e30f;
-      float hv[NH];
-      static_for<0, NH>([&](auto kI) { hv[kI.value] = hv_dot<kI.value>(mu); });
-#pragma unroll
-      for (int k = 0; k < NH; k++) hmu = fminf(hmu, hv[k]);
-      float wh_ = 0.0f, ch[3] = {0.0f, 0.0f, 0.0f};
-      static_for<0, NH>([&](auto kI) {
-        constexpr int k = kI.value;
-        const float w = fmaxf(0.0f, 1.0f - (hv[k] - hmu) * (1.0f / HF_WITNESS_BAND));
-        wh_ += w;
-        ch[0] = cfma<fbits(Md::hull_vert[k][0])>(w, ch[0]);
-        ch[1] = cfma<fbits(Md::hull_vert[k][1])>(w, ch[1]);
-        ch[2] = cfma<fbits(Md::hull_vert[k][2])>(w, ch[2]);
-      });
-      const float q[3] = {dot3(mu, Tm[0]), dot3(mu, Tm[1]), dot3(mu, Tm[2])};
-      const float pmx = fmaxf(q[0], fmaxf(q[1], q[2]));
-      float wp_ = 0.0f, cq[3] = {0.0f, 0.0f, 0.0f};
-      for (int k = 0; k < 3; k++) {
-        const float w = fmaxf(0.0f, 1.0f - (pmx - q[k]) * (1.0f / HF_WITNESS_BAND));
-        wp_ += w;
-        for (int a = 0; a < 3; a++) cq[a] += w * Tm[k][a];
-      }
-      for (int a = 0; a < 3; a++) pos[a] = 0.5f * (ch[a] / wh_ + cq[a] / wp_);
-    }
-    if (kq == 0) {
-      E4[0] = f4v{mo, mu[0], mu[1], mu[2]};
-      E4[1] = f4v{pos[0], pos[1], pos[2], 0.0f};
-    }
-  }
-
   static DK void collide_hfield(LP L, int lane, const float* hf) {
     STAGE_T0();
     constexpr int NH = Md::NHV, NF = Md::NHF, NE = Md::NHE;
@@ -2285,15 +2061,7 @@ struct TPhys {
         S += c;
       }
     }
-    const int nact = __popcll(act), QR1 = nact < HF_QR ? nact : HF_QR;
-    // three lanes per entry (hf_exec3) when the wave is whole and its survivors fit 21 entries: a third
-    // of the top-edge pairs per lane, the same results bit for bit
-#ifdef DUCK_HF_NO_SPLIT
-    const bool m3 = false;
-#else
-    const bool m3 = act == ~0ull && S <= 21;
-#endif
-    const int QRa = m3 ? 21 : QR1;
+    const int nact = __popcll(act), QRa = nact < HF_QR ? nact : HF_QR;
 #ifdef DUCK_STAGE_PROF
     if (threadIdx.x == 0) STAGE_ADD(40, (unsigned long long)S);
     // the survivors' distribution over wave-substeps (wave 0): <= 21, 22-32, 33-42, 43-64, > 64
@@ -2339,11 +2107,7 @@ struct TPhys {
 #ifdef DUCK_ASM_MARKS
       asm volatile("; HF_EXEC_BEGIN" ::: "memory");
 #endif
-      if (m3) {
-        if (gi < 3 * S) hf_exec3(qent(gi / 3), L, tw, gi - 3 * (gi / 3));
-      } else if (gi < QRa && r0 + gi < S) {
-        hf_exec(qent(gi), L, tw);
-      }
+      if (gi < QRa && r0 + gi < S) hf_exec(qent(gi), L, tw);
 #ifdef DUCK_ASM_MARKS
       asm volatile("; HF_EXEC_END" ::: "memory");
 #endif
@@ -2911,6 +2675,11 @@ struct TPhys {
 
   // J.x of one contact slot (4 pyramid edges) for body spatial motions SL/SR (runtime pair)
   static DK void contact_jx(LP L, int p, int slot, const float* SL, const float* SR, float* out4) {
+    // contractions within expressions only: this function's statements are inlined into the fused warm
+    // start of step_kernel and into the split halves of the latency kernels, where the backend formed
+    // different FMAs across them (the flat scenes' kernels then agreed only to fp32 rounding;
+    // tools/fpc_bisect.py located it, profiles/r05_lat_bitcmp.txt). With it the kernels agree bit for bit.
+#pragma clang fp contract(on)
     const int o = Md::B_PAIR + PAIRW * p;
     const int s1 = ti(o), s2 = ti(o + 1);
     const float mu = tf(o + 2);

@@ -223,8 +223,7 @@ class Joystick(OpenDuckMiniV2Env):
         splits each substep's stages over four waves per 4 envs (a shorter env-step for small batches,
         e.g. a 4096-env job strong-scaled over 4 or 8 GPUs); "paired" splits them over a pair of waves
         per 4 envs, 8 envs per workgroup (4096 envs over 2 GPUs); "auto" takes latency at <= 4 envs
-        per CU and paired at <= 8. Height-field scenes: bit-identical results in every mode; flat
-        scenes: equal to fp32 rounding (include/duck.h), so `step_kernel` is part of a run's record."""
+        per CU and paired at <= 8. Every mode gives bit-identical results (include/duck.h)."""
         if mode not in STEP_MODES:
             raise DuckError(f"step mode {mode!r} not in {sorted(STEP_MODES)}")
         if not hasattr(self._lib, "duck_set_step_mode") and mode in ("auto", "throughput"):

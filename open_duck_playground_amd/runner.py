@@ -43,8 +43,8 @@ class BaseRunner:
 
     def progress_callback(self, num_steps: int, metrics: dict) -> None:
         os.makedirs(self.output_dir, exist_ok=True)
-        # which step kernel ran (include/duck.h DUCK_STEP_*): flat-scene trajectories depend on it at fp32
-        # rounding, so a run is reproduced on the same kernel
+        # which step kernel ran (include/duck.h DUCK_STEP_*; the kernels agree bit for bit, recorded for
+        # the run's provenance)
         kernels = {"train": getattr(self.env, "step_kernel", None)}
         if self.eval_env is not None:
             kernels["eval"] = getattr(self.eval_env, "step_kernel", None)
