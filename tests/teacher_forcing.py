@@ -307,7 +307,7 @@ def _one_kp_small(m: Model) -> Model:        # the left knee servo's kp x 1.001
 # the defect induces IS a defect and explain() must say so (test_explain_has_teeth). The knob defects
 # change only contact generation on the height field -- where sat_tie, onset, onset_selection and
 # dup_selection fire: round 4's point band switched back on, the support features' witness band x 1.5,
-# the deepest-prism tie x 30 (3e-5 m; at x 10 = 1e-5 m the defect sits at the reach of flip_level's 1e-5
+# the deepest-prism tie x 100 (1e-4 m; at x 10 = 1e-5 m the defect sits at the reach of flip_level's 1e-5
 # input perturbation, and 4 of 23 differing substeps were flips, none a contact rule: DESIGN.md §5), and the
 # 4-slot manifold started from the second-deepest prism contact
 DEFECTS = {
@@ -319,7 +319,7 @@ DEFECTS = {
     "foot_hull_x1.0005_hfield": ("rough_dr", _foot_hull, None),
     "hf_point_band_on": ("rough_dr", None, (0, 1.0)),
     "hf_witness_band_x1.5": ("rough_dr", None, (1, 1.5)),
-    "hf_depth_tie_x30": ("rough_dr", None, (2, 30.0)),
+    "hf_depth_tie_x100": ("rough_dr", None, (2, 100.0)),
     "hf_manifold_second_deepest": ("rough_dr", None, (3, 1.0)),
 }
 

@@ -115,13 +115,13 @@ def _classify(m, om, cases, seed: int = 0):
 @pytest.mark.parametrize("defect", [d for d in DEFECTS if DEFECTS[d][2] is not None])
 def test_contact_rules_reject_contact_generation_defects(defect):
     """The CPU half of test_explain_has_teeth for the contact-generation-only defects (DEFECTS' oracle
-    knobs: round 4's point band, the witness band x 1.5, the deepest-prism tie x 30, the manifold from
+    knobs: round 4's point band, the witness band x 1.5, the deepest-prism tie x 100, the manifold from
     the second-deepest prism): the stand-in GPU is the oracle WITH the defect (its substep and its
     contacts), the classifier runs the nominal oracle. The rules that fire on contact generation --
     onset, sat_tie, onset_selection, dup_selection -- and backward_error and flip_level must call
     >= 90 % of the differing substeps a defect (per-rule counts printed)."""
     knob = DEFECTS[defect][2]
-    # (the deepest-prism tie x 30 changes the result rarely: a larger rollout for enough cases)
+    # (the deepest-prism tie x 100 changes the result rarely: a larger rollout for enough cases)
     m, xs = _states("rough_terrain", n=64 if knob[0] == 2 else 16, steps=12, substeps=True)
     om = OracleModel(m)
 

@@ -99,7 +99,7 @@ def test_explain_has_teeth(defect, gpu):
     x 1.02, one servo's kp x 1.005 and x 1.001, hinge damping x 1.01, contact solref x 1.02, the foot hull
     scaled by 1.0005 on the height field) or a wrong contact generation (teacher_forcing.DEFECTS' oracle
     knobs, which change only the height field's contacts: round 4's point band, the witness band x 1.5,
-    the deepest-prism tie x 30, the manifold from the second-deepest prism) while the GPU runs the
+    the deepest-prism tie x 100, the manifold from the second-deepest prism) while the GPU runs the
     nominal one. A model defect makes every outlier a real model difference; a contact knob counts
     only the outliers it induced -- those where the oracle without the knob, from the same pre-state,
     lands inside the bars on the GPU (nominal_agrees). Such outliers must appear (>= 20 for round 4's
