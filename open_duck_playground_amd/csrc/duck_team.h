@@ -1836,6 +1836,12 @@ struct TPhys {
 #endif
   }
 
+  // the grid offsets (column, row) of top vertex k of a cell's triangle: A (tri 0) = (0, 0), (0, 1), (1, 0);
+  // B (tri 1) = (0, 1), (1, 0), (1, 1). Arithmetic on tri: written as a table indexed by tri the compiler
+  // made it a lookup in global memory, two dependent loads per prism slot in the survivor descriptors
+  static DK int tri_dc(int k, int tri) { return k == 0 ? 0 : (k == 1 ? tri : 1); }
+  static DK int tri_dr(int k, int tri) { return k == 0 ? tri : (k == 1 ? 1 - tri : tri); }
+
   static DK void collide_hfield(LP L, int lane, const float* hf) {
     STAGE_T0();
     constexpr int NH = Md::NHV, NF = Md::NHF, NE = Md::NHE;
@@ -1919,9 +1925,9 @@ struct TPhys {
     auto prism_top = [&](int q, float (*T)[3], int& tri) {
       const int rr = q / (2 * ncx), rem = q - rr * 2 * ncx, cc = rem >> 1;
       tri = rem & 1;
-      const int dcs[2][3] = {{0, 0, 1}, {0, 1, 1}}, drs[2][3] = {{0, 1, 0}, {1, 0, 1}};
+#pragma unroll
       for (int k = 0; k < 3; k++) {
-        const int ci = cc + (tri ? dcs[1][k] : dcs[0][k]), ri = rr + (tri ? drs[1][k] : drs[0][k]);
+        const int ci = cc + tri_dc(k, tri), ri = rr + tri_dr(k, tri);
         T[k][0] = X0 + (float)ci * DXC;
         T[k][1] = Y0 + (float)ri * DYC;
         T[k][2] = zat(ci, ri);
@@ -2082,11 +2088,11 @@ struct TPhys {
         if (mine) {
           // the prism's top (local) as the screen had it, then the mesh frame
           const int rr = q / (2 * ncx), rem = q - rr * 2 * ncx, cc = rem >> 1, tri = rem & 1;
-          const int dcs[2][3] = {{0, 0, 1}, {0, 1, 1}}, drs[2][3] = {{0, 1, 0}, {1, 0, 1}};
           float T[3][3], nt[3], ntm[3], Tm[3][3];
+#pragma unroll
           for (int k = 0; k < 3; k++) {
-            T[k][0] = X0 + (float)(cc + (tri ? dcs[1][k] : dcs[0][k])) * DXC;
-            T[k][1] = Y0 + (float)(rr + (tri ? drs[1][k] : drs[0][k])) * DYC;
+            T[k][0] = X0 + (float)(cc + tri_dc(k, tri)) * DXC;
+            T[k][1] = Y0 + (float)(rr + tri_dr(k, tri)) * DYC;
             T[k][2] = szt[j][k];
           }
           top_normal(T, nt);
