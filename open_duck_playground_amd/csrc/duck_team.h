@@ -2014,7 +2014,15 @@ struct TPhys {
     // order into the env slice's composite-inertia storage (dead after crb()): the direction w in
     // which the negated arc crosses the equator and the hull's support along it
     lds_float* const SLo = L + HF_CINQ + h * HF_SLSZ;
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 17
+    for (int rep_ = 0; rep_ < 2; rep_++)
+#endif
     {
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 17
+      float zc_l[3] = {zc[0], zc[1], zc[2]};
+      launder<3>(zc_l);
+      const auto& zc = zc_l;
+#endif
       unsigned long long M = 0;
       float wv[EPL][3], wh[EPL];
       bool sl[EPL];
@@ -2079,6 +2087,10 @@ struct TPhys {
 #ifdef DUCK_STAGE_PROF
       if (threadIdx.x == 0) STAGE_ADD(46, 1ull);
 #endif
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 18
+      for (int rep_ = 0; rep_ < 2; rep_++) {
+      launder<9>(R);
+#endif
 #pragma unroll
       for (int j = 0; j < PPL; j++) {
         const int q = sub + 8 * j;
@@ -2108,6 +2120,9 @@ struct TPhys {
           E4[6] = f4v{R[3], R[4], R[5], szt[j][2]};
         }
       }
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 18
+      }
+#endif
       TSYNC();
       STAGE_MARK(41);
 #ifdef DUCK_ASM_MARKS
@@ -2141,6 +2156,12 @@ struct TPhys {
     // 4 slots by mjx's _manifold_points over the prism contacts, from the deepest (the first prism
     // within HF_DEPTH_TIE of it: prisms sharing a grid vertex or edge often tie exactly); index
     // q = sub + 8 s is the prism's strip position
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 19
+    for (int rep_ = 0; rep_ < 2; rep_++) {
+    launder<PPL>(cd);
+    launder<3 * PPL>(&cx[0][0]);
+    launder<3 * PPL>(&cn[0][0]);
+#endif
     constexpr int QN = 8 * PPL;
     float dmax = -1e30f;
 #pragma unroll
@@ -2263,6 +2284,9 @@ struct TPhys {
         P1::store_contact(Ls, 4 * p + sub, 1.0f, zero, nofr);
       }
     }
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 19
+    }
+#endif
     STAGE_MARK(39);
   }
 
@@ -3283,19 +3307,31 @@ struct TPhys {
                       int sstride, const float* hf) {
     STAGE_T0();
     kinematics(L, lane);
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 6
+    kinematics(L, lane);
+#endif
     STAGE_MARK(0);
     com_pos(L, lane);
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 7
+    com_pos(L, lane);
+#endif
     STAGE_MARK(1);
     rne(L, lane);
     STAGE_MARK(2);
     crb(L, lane);
-    // DUCK_DOUBLE (measurement builds, tools/gpu_stage_double.sh): one idempotent stage runs twice,
-    // and the launch-time difference to the normal build is that stage's cost, unperturbed by markers
+    // DUCK_DOUBLE (measurement builds, tools/gpu_stage_double.sh, tools/gpu_stage_pmc.sh): one
+    // idempotent stage runs twice, and the launch-time (and counter) difference to the normal build
+    // is that stage's cost, unperturbed by markers: 1 crb, 2 collision, 3 make_rows, 4 smooth_acc,
+    // 5 solve, 6 kinematics, 7 com_pos, 8 rne + smooth
 #if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 1
     crb(L, lane);
 #endif
     STAGE_MARK(3);
     smooth(L, lane);
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 8
+    rne(L, lane);  // (smooth adds to rne's qfrc_smooth: the pair is idempotent, smooth alone is not)
+    smooth(L, lane);
+#endif
     STAGE_MARK(28);
     // collision and the constraint rows depend on the kinematics only: they run before the
     // smooth acceleration so that M is loaded into registers once for both solves
@@ -3319,6 +3355,9 @@ struct TPhys {
 #endif
       STAGE_MARK(4);
       solve(L, lane, scratch, sstride, Mc);
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 5
+      solve(L, lane, scratch, sstride, Mc);  // (reads qacc_warmstart / qacc_smooth, not qacc)
+#endif
     }
     STAGE_MARK(7);
     if (want_out) {
