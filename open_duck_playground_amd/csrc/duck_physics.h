@@ -63,6 +63,16 @@ static __device__ unsigned long long g_stage_wg[DUCK_NSTAGE * 256];
     if (blockIdx.x == 0 && ((int)threadIdx.x & 63) == 0) g_stage_cycles[DUCK_NSTAGE + 64 + (k)] += _c1 - _c0; \
     _c0 = _c1;                                                                         \
   } while (0)
+#elif defined(DUCK_ASM_MARKS)
+// static instruction counts per stage (tools/isa_stage_hist.py on hipcc -S output): a comment
+// at each stage boundary, no code
+#define STAGE_T0() \
+  do {             \
+  } while (0)
+#define STAGE_MARK(k) asm volatile("; STAGE_MARK " #k ::: "memory")
+#define STAGE_RESET() \
+  do {                \
+  } while (0)
 #else
 #define STAGE_T0() \
   do {             \

@@ -132,6 +132,52 @@ DK float cdot(const float* x) {
   asm("v_fmac_f32_e32 %0, %1, %2" : "+v"(r) : "i"(C2), "v"(x[2]));
   return r;
 }
+// c . x, c . y, c . z (and c . u, c . w): the same products as cdot, interleaved in one statement.
+// The scheduler prices an asm statement at no latency, so separate per-instruction statements were
+// left as dependent mul -> fmac -> fmac chains, each link stalled (8 cycles for one wave, against 4-5
+// independent) and padded with an s_nop that the hazard recognizer puts after inline asm
+template <int C0, int C1, int C2>
+DK void cdot3v(const float* x, const float* y, const float* z, float* r) {
+  asm("v_mul_f32_e32 %0, %3, %6\n\tv_mul_f32_e32 %1, %3, %9\n\tv_mul_f32_e32 %2, %3, %12\n\t"
+      "v_fmac_f32_e32 %0, %4, %7\n\tv_fmac_f32_e32 %1, %4, %10\n\tv_fmac_f32_e32 %2, %4, %13\n\t"
+      "v_fmac_f32_e32 %0, %5, %8\n\tv_fmac_f32_e32 %1, %5, %11\n\tv_fmac_f32_e32 %2, %5, %14"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2])
+      : "i"(C0), "i"(C1), "i"(C2), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(y[0]), "v"(y[1]), "v"(y[2]),
+        "v"(z[0]), "v"(z[1]), "v"(z[2]));
+}
+template <int C0, int C1, int C2>
+DK void cdot4v(const float* x, const float* y, const float* z, const float* u, float* r) {
+  asm("v_mul_f32_e32 %0, %4, %7\n\tv_mul_f32_e32 %1, %4, %10\n\tv_mul_f32_e32 %2, %4, %13\n\t"
+      "v_mul_f32_e32 %3, %4, %16\n\t"
+      "v_fmac_f32_e32 %0, %5, %8\n\tv_fmac_f32_e32 %1, %5, %11\n\tv_fmac_f32_e32 %2, %5, %14\n\t"
+      "v_fmac_f32_e32 %3, %5, %17\n\t"
+      "v_fmac_f32_e32 %0, %6, %9\n\tv_fmac_f32_e32 %1, %6, %12\n\tv_fmac_f32_e32 %2, %6, %15\n\t"
+      "v_fmac_f32_e32 %3, %6, %18"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+      : "i"(C0), "i"(C1), "i"(C2), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(y[0]), "v"(y[1]), "v"(y[2]),
+        "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(u[0]), "v"(u[1]), "v"(u[2]));
+}
+template <int C0, int C1, int C2>
+DK void cdot5v(const float* x, const float* y, const float* z, const float* u, const float* w, float* r) {
+  asm("v_mul_f32_e32 %0, %5, %8\n\tv_mul_f32_e32 %1, %5, %11\n\tv_mul_f32_e32 %2, %5, %14\n\t"
+      "v_mul_f32_e32 %3, %5, %17\n\tv_mul_f32_e32 %4, %5, %20\n\t"
+      "v_fmac_f32_e32 %0, %6, %9\n\tv_fmac_f32_e32 %1, %6, %12\n\tv_fmac_f32_e32 %2, %6, %15\n\t"
+      "v_fmac_f32_e32 %3, %6, %18\n\tv_fmac_f32_e32 %4, %6, %21\n\t"
+      "v_fmac_f32_e32 %0, %7, %10\n\tv_fmac_f32_e32 %1, %7, %13\n\tv_fmac_f32_e32 %2, %7, %16\n\t"
+      "v_fmac_f32_e32 %3, %7, %19\n\tv_fmac_f32_e32 %4, %7, %22"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4])
+      : "i"(C0), "i"(C1), "i"(C2), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(y[0]), "v"(y[1]), "v"(y[2]),
+        "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(u[0]), "v"(u[1]), "v"(u[2]), "v"(w[0]), "v"(w[1]), "v"(w[2]));
+}
+// a . x and b . x for two compile-time vectors a = (A0, A1, A2), b = (B0, B1, B2), interleaved
+template <int A0, int A1, int A2, int B0, int B1, int B2>
+DK void cdot2c(const float* x, float& ra, float& rb) {
+  asm("v_mul_f32_e32 %0, %2, %8\n\tv_mul_f32_e32 %1, %5, %8\n\t"
+      "v_fmac_f32_e32 %0, %3, %9\n\tv_fmac_f32_e32 %1, %6, %9\n\t"
+      "v_fmac_f32_e32 %0, %4, %10\n\tv_fmac_f32_e32 %1, %7, %10"
+      : "=&v"(ra), "=&v"(rb)
+      : "i"(A0), "i"(A1), "i"(A2), "i"(B0), "i"(B1), "i"(B2), "v"(x[0]), "v"(x[1]), "v"(x[2]));
+}
 // a + c * x (fma with a literal c)
 template <int C>
 DK float cfma(float x, float a) {
@@ -1524,6 +1570,33 @@ struct TPhys {
   static DK float dxc_dot(const float* x) {
     return cdot<fbits(Md::hull_edge_dxc[E][0]), fbits(Md::hull_edge_dxc[E][1]), fbits(Md::hull_edge_dxc[E][2])>(x);
   }
+  // the same products for several vectors at once (cdot3v / cdot4v / cdot5v / cdot2c)
+#define DUCK_C3(A) fbits(A[0]), fbits(A[1]), fbits(A[2])
+  template <int F>
+  static DK void nf_dot3(const float* x, const float* y, const float* z, float* r) {
+    cdot3v<DUCK_C3(Md::hull_face_normal[F])>(x, y, z, r);
+  }
+  template <int F>
+  static DK void nf_dot4(const float* x, const float* y, const float* z, const float* u, float* r) {
+    cdot4v<DUCK_C3(Md::hull_face_normal[F])>(x, y, z, u, r);
+  }
+  template <int K>
+  static DK void hv_dot5(const float* x, const float* y, const float* z, const float* u, const float* w, float* r) {
+    cdot5v<DUCK_C3(Md::hull_vert[K])>(x, y, z, u, w, r);
+  }
+  template <int K>
+  static DK void hv_dot2(const float* x, float& ra, float& rb) {  // vertices K and K + 1
+    cdot2c<DUCK_C3(Md::hull_vert[K]), DUCK_C3(Md::hull_vert[K + 1])>(x, ra, rb);
+  }
+  template <int F>
+  static DK void nf_dot2(const float* x, float& ra, float& rb) {  // faces F and F + 1
+    cdot2c<DUCK_C3(Md::hull_face_normal[F]), DUCK_C3(Md::hull_face_normal[F + 1])>(x, ra, rb);
+  }
+  template <int E>
+  static DK void dxc_dot2(const float* x, float& ra, float& rb) {  // edges E and E + 1
+    cdot2c<DUCK_C3(Md::hull_edge_dxc[E]), DUCK_C3(Md::hull_edge_dxc[E + 1])>(x, ra, rb);
+  }
+#undef DUCK_C3
   template <int F>
   static DK float nf_off_minus(float x) {  // offset_F - x
     float r;
@@ -1605,10 +1678,12 @@ struct TPhys {
       const float hk[3] = {d4.w - base, d5.w - base, d6.w - base};
       static_for<0, NF>([&](auto fI) {
         constexpr int f = fI.value;
-        const float nz = fmaxf(nf_dot<f>(zc), 0.0f);
-        float pf = nf_dot<f>(Tm[0]) - hk[0] * nz;
-        pf = fminf(pf, nf_dot<f>(Tm[1]) - hk[1] * nz);
-        pf = fminf(pf, nf_dot<f>(Tm[2]) - hk[2] * nz);
+        float d[4];
+        nf_dot4<f>(zc, Tm[0], Tm[1], Tm[2], d);
+        const float nz = fmaxf(d[0], 0.0f);
+        float pf = d[1] - hk[0] * nz;
+        pf = fminf(pf, d[2] - hk[1] * nz);
+        pf = fminf(pf, d[3] - hk[2] * nz);
         const float ov = nf_off_minus<f>(pf);
         const bool b = (ov < mo) | ((ov == mo) & (5 + f < mp));
         mo = b ? ov : mo;
@@ -1660,20 +1735,30 @@ struct TPhys {
       for (int k = 0; k < 3; k++) cross3(hx[k], sm[k], ntm);
       // (one prism edge at a time: 30 face products live, not 90)
       float ADC[NE];
-      static_for<0, NE>([&](auto eI) { ADC[eI.value] = dxc_dot<eI.value>(ntm); });
+      // (pairs of products per statement: cdot2c)
+      static_for<0, NE / 2>([&](auto eI) { dxc_dot2<2 * eI.value>(ntm, ADC[2 * eI.value], ADC[2 * eI.value + 1]); });
+      if constexpr (NE % 2) ADC[NE - 1] = dxc_dot<NE - 1>(ntm);
       // (k a compile-time constant too, so that every pm index is one: a runtime index kept pm in
       // scratch memory, and pass 2's word selects became indexed scratch loads)
       static_for<0, 3>([&](auto kI) {
         constexpr int k = kI.value;
         float phi[NF];
-        static_for<0, NF>([&](auto fI) { phi[fI.value] = nf_dot<fI.value>(hx[k]); });
-        static_for<0, NE>([&](auto eI) {
-          constexpr int e = eI.value, fa = Md::hull_edge_face[e][0], fb = Md::hull_edge_face[e][1];
-          const float BDC = dxc_dot<e>(sm[k]);
+        static_for<0, NF / 2>([&](auto fI) { nf_dot2<2 * fI.value>(hx[k], phi[2 * fI.value], phi[2 * fI.value + 1]); });
+        if constexpr (NF % 2) phi[NF - 1] = nf_dot<NF - 1>(hx[k]);
+        auto arc = [&](auto eI, float BDC) {
+          constexpr int e = decltype(eI)::value, fa = Md::hull_edge_face[e][0], fb = Md::hull_edge_face[e][1];
           const float mx = fmaxf(fmaxf(phi[fa] * phi[fb], ADC[e] * BDC), phi[fa] * BDC);
           constexpr int p = 3 * e + k;
           pm[p >> 6] |= (unsigned long long)(__float_as_uint(mx) >> 31) << (p & 63);
+        };
+        static_for<0, NE / 2>([&](auto eI) {
+          constexpr int e = 2 * eI.value;
+          float b0, b1;
+          dxc_dot2<e>(sm[k], b0, b1);
+          arc(std::integral_constant<int, e>{}, b0);
+          arc(std::integral_constant<int, e + 1>{}, b1);
         });
+        if constexpr (NE % 2) arc(std::integral_constant<int, NE - 1>{}, dxc_dot<NE - 1>(sm[k]));
       });
     }
     STAGE_MARK(45);
@@ -1767,9 +1852,11 @@ struct TPhys {
     // branches cost more than the distances they skipped, C4 -0.8 %; the weights are the same)
     static_for<0, NH>([&](auto kI) {
       constexpr int k = kI.value;
-      const float atop = ptop - hv_dot<k>(ntm);
-      float pen = fminf(atop, hv_dot<k>(zc) - base);
-      for (int j = 0; j < 3; j++) pen = fminf(pen, smt[j] - hv_dot<k>(sm[j]));
+      float d[5];
+      hv_dot5<k>(ntm, zc, sm[0], sm[1], sm[2], d);
+      const float atop = ptop - d[0];
+      float pen = fminf(atop, d[1] - base);
+      for (int j = 0; j < 3; j++) pen = fminf(pen, smt[j] - d[2 + j]);
       const float w = fmaxf(pen, 0.0f);
       W += w;
       Cx[0] = cfma<fbits(Md::hull_vert[k][0])>(w, Cx[0]);
@@ -1787,8 +1874,10 @@ struct TPhys {
         constexpr int f = HullFaceOrder<Md>{}.f[pos];
         if (pos == 6 || pos == 14) live = live && __ballot(fmaxf(pk[0], fmaxf(pk[1], pk[2])) > 0.0f) != 0ull;
         if (!live) return;
+        float d[3];
+        nf_dot3<f>(Tm[0], Tm[1], Tm[2], d);
 #pragma unroll
-        for (int j = 0; j < 3; j++) pk[j] = fminf(pk[j], nf_off_minus<f>(nf_dot<f>(Tm[j])));
+        for (int j = 0; j < 3; j++) pk[j] = fminf(pk[j], nf_off_minus<f>(d[j]));
       });
 #pragma unroll
       for (int j = 0; j < 3; j++) {
@@ -1985,7 +2074,13 @@ struct TPhys {
       float ntm[3];
       mulmtv3(ntm, R, nt);
       float hm = 1e30f;
-      static_for<0, NH>([&](auto kI) { hm = fminf(hm, hv_dot<kI.value>(ntm)); });
+      // (vertex pairs: two interleaved products per statement; the minimum is order-independent)
+      static_for<0, NH / 2>([&](auto kI) {
+        float ha, hb;
+        hv_dot2<2 * kI.value>(ntm, ha, hb);
+        hm = fminf(hm, fminf(ha, hb));
+      });
+      if constexpr (NH % 2) hm = fminf(hm, hv_dot<NH - 1>(ntm));
       // priority order (equal overlaps: the first): top 0, sides 1-3, bottom 4, hull faces 5 + f
       float mo = dot3(nt, T[0]) - hm;
       int mp = 0;

@@ -55,9 +55,24 @@ __global__ void __launch_bounds__(256) probe(float* out, long long* cyc, int ite
     } else if constexpr (K == 10) {  // v_add_f32 with a DPP operand
 #define I10(j) asm volatile("v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(s[j]) : "v"(sc));
       REP16(I10(0) I10(1) I10(2) I10(3) I10(4) I10(5) I10(6) I10(7))
-    } else if constexpr (K == 11) {  // v_dot2_f32_f32? (not on gfx950): v_fmac_f32 (VOP2) instead
+    } else if constexpr (K == 11) {  // v_fmac_f32 (VOP2)
 #define I11(j) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(s[j]) : "v"(sb), "v"(sc));
       REP16(I11(0) I11(1) I11(2) I11(3) I11(4) I11(5) I11(6) I11(7))
+    } else if constexpr (K == 12) {  // v_fmac_f32 with a 32-bit literal operand (the SAT's hull constants)
+#define I12(j) asm volatile("v_fmac_f32 %0, 0x3f8ccccd, %1" : "+v"(s[j]) : "v"(sc));
+      REP16(I12(0) I12(1) I12(2) I12(3) I12(4) I12(5) I12(6) I12(7))
+    } else if constexpr (K == 13) {  // s_mov_b32 literal + v_pk_fma_f32 with that SGPR splat (per pair, 2 instr)
+#define I13(j) asm volatile("s_mov_b32 s90, 0x3f8ccccd\n v_pk_fma_f32 %0, %0, s[90:91], %1 op_sel_hi:[1,0,1]" : "+v"(a[j]) : "v"(c) : "s90", "s91");
+      REP16(I13(0) I13(1) I13(2) I13(3) I13(4) I13(5) I13(6) I13(7))
+    } else if constexpr (K == 14) {  // v_pk_fma_f32 with an inline-constant splat
+#define I14(j) asm volatile("v_pk_fma_f32 %0, %0, 0.5, %1 op_sel_hi:[1,0,1]" : "+v"(a[j]) : "v"(c));
+      REP16(I14(0) I14(1) I14(2) I14(3) I14(4) I14(5) I14(6) I14(7))
+    } else if constexpr (K == 15) {  // v_cndmask_b32 (the SAT's selects)
+#define I15(j) asm volatile("v_cmp_gt_f32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(s[j]) : "v"(sc) : "vcc");
+      REP16(I15(0) I15(1) I15(2) I15(3) I15(4) I15(5) I15(6) I15(7))
+    } else if constexpr (K == 16) {  // v_max3_f32 / v_min3_f32
+#define I16(j) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(s[j]) : "v"(sb), "v"(sc));
+      REP16(I16(0) I16(1) I16(2) I16(3) I16(4) I16(5) I16(6) I16(7))
     }
   }
   const long long t1 = clock64();
@@ -85,10 +100,12 @@ int main() {
   hipMalloc(&out, sizeof(float) * nb * 256);
   hipMalloc(&cyc_d, sizeof(long long) * nb * 4);
   const char* names[] = {"v_fma_f32 x8 chains", "v_pk_fma_f32 x8 chains", "v_pk_mul_f32 x8", "v_pk_add_f32 x8",
-                         "v_add_f32 x8", "v_rcp_f32 x8", "v_fma_f32 + v_pk_fma_f32 alternating (per instr)",
+                         "v_add_f32 x8", "v_rcp_f32 x8", "v_fma_f32 + v_pk_fma_f32 alternating (per pair)",
                          "v_fma_f32 dependent chain", "v_pk_fma_f32 dependent chain", "v_mov_b32_dpp row_shr x8",
-                         "v_add_f32_dpp row_shr x8", "v_fmac_f32 x8"};
-  double r[12];
+                         "v_add_f32_dpp row_shr x8", "v_fmac_f32 x8", "v_fmac_f32 literal x8",
+                         "s_mov_b32 literal + v_pk_fma_f32 sgpr splat (per pair)", "v_pk_fma_f32 inline-constant splat",
+                         "v_cmp + v_cndmask (per pair)", "v_max3_f32"};
+  double r[17];
   r[0] = run<0>(out, cyc_d, cyc_h, nb, iters);
   r[1] = run<1>(out, cyc_d, cyc_h, nb, iters);
   r[2] = run<2>(out, cyc_d, cyc_h, nb, iters);
@@ -101,8 +118,13 @@ int main() {
   r[9] = run<9>(out, cyc_d, cyc_h, nb, iters);
   r[10] = run<10>(out, cyc_d, cyc_h, nb, iters);
   r[11] = run<11>(out, cyc_d, cyc_h, nb, iters);
+  r[12] = run<12>(out, cyc_d, cyc_h, nb, iters);
+  r[13] = run<13>(out, cyc_d, cyc_h, nb, iters);
+  r[14] = run<14>(out, cyc_d, cyc_h, nb, iters);
+  r[15] = run<15>(out, cyc_d, cyc_h, nb, iters);
+  r[16] = run<16>(out, cyc_d, cyc_h, nb, iters);
   printf("one wave per SIMD, %d workgroups x 256 threads, s_memtime cycles per wave-instruction:\n", nb);
-  for (int k = 0; k < 12; k++) printf("  %-52s %.2f\n", names[k], r[k]);
+  for (int k = 0; k < 17; k++) printf("  %-52s %.2f\n", names[k], r[k]);
   hipError_t e = hipGetLastError();
   printf("status: %s\n", hipGetErrorString(e));
   return e == hipSuccess ? 0 : 1;
