@@ -132,17 +132,19 @@ DK float cdot(const float* x) {
   asm("v_fmac_f32_e32 %0, %1, %2" : "+v"(r) : "i"(C2), "v"(x[2]));
   return r;
 }
-// c . x, c . y, c . z (and c . u, c . w): the same products as cdot, interleaved in one statement.
+// c . x, c . y, c . z, c . u (and c . w): the same products as cdot, interleaved in one statement.
 // The scheduler prices an asm statement at no latency, so separate per-instruction statements were
 // left as dependent mul -> fmac -> fmac chains, each link stalled (8 cycles for one wave, against 4-5
 // independent) and padded with an s_nop that the hazard recognizer puts after inline asm
-template <int C0, int C1, int C2>
-DK void cdot3v(const float* x, const float* y, const float* z, float* r) {
-  asm("v_mul_f32_e32 %0, %3, %6\n\tv_mul_f32_e32 %1, %3, %9\n\tv_mul_f32_e32 %2, %3, %12\n\t"
-      "v_fmac_f32_e32 %0, %4, %7\n\tv_fmac_f32_e32 %1, %4, %10\n\tv_fmac_f32_e32 %2, %4, %13\n\t"
-      "v_fmac_f32_e32 %0, %5, %8\n\tv_fmac_f32_e32 %1, %5, %11\n\tv_fmac_f32_e32 %2, %5, %14"
+// OFF - c . x, OFF - c . y, OFF - c . z: three products and the subtraction in one statement
+template <int C0, int C1, int C2, int OFF>
+DK void cdot3v_off(const float* x, const float* y, const float* z, float* r) {
+  asm("v_mul_f32_e32 %0, %3, %7\n\tv_mul_f32_e32 %1, %3, %10\n\tv_mul_f32_e32 %2, %3, %13\n\t"
+      "v_fmac_f32_e32 %0, %4, %8\n\tv_fmac_f32_e32 %1, %4, %11\n\tv_fmac_f32_e32 %2, %4, %14\n\t"
+      "v_fmac_f32_e32 %0, %5, %9\n\tv_fmac_f32_e32 %1, %5, %12\n\tv_fmac_f32_e32 %2, %5, %15\n\t"
+      "v_sub_f32_e32 %0, %6, %0\n\tv_sub_f32_e32 %1, %6, %1\n\tv_sub_f32_e32 %2, %6, %2"
       : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2])
-      : "i"(C0), "i"(C1), "i"(C2), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(y[0]), "v"(y[1]), "v"(y[2]),
+      : "i"(C0), "i"(C1), "i"(C2), "i"(OFF), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(y[0]), "v"(y[1]), "v"(y[2]),
         "v"(z[0]), "v"(z[1]), "v"(z[2]));
 }
 template <int C0, int C1, int C2>
@@ -1570,11 +1572,11 @@ struct TPhys {
   static DK float dxc_dot(const float* x) {
     return cdot<fbits(Md::hull_edge_dxc[E][0]), fbits(Md::hull_edge_dxc[E][1]), fbits(Md::hull_edge_dxc[E][2])>(x);
   }
-  // the same products for several vectors at once (cdot3v / cdot4v / cdot5v / cdot2c)
+  // the same products for several vectors at once (cdot3v_off / cdot4v / cdot5v / cdot2c)
 #define DUCK_C3(A) fbits(A[0]), fbits(A[1]), fbits(A[2])
   template <int F>
-  static DK void nf_dot3(const float* x, const float* y, const float* z, float* r) {
-    cdot3v<DUCK_C3(Md::hull_face_normal[F])>(x, y, z, r);
+  static DK void nf_off_dot3(const float* x, const float* y, const float* z, float* r) {  // offset_F - n_F . (x, y, z)
+    cdot3v_off<DUCK_C3(Md::hull_face_normal[F]), fbits(Md::hull_face_offset[F])>(x, y, z, r);
   }
   template <int F>
   static DK void nf_dot4(const float* x, const float* y, const float* z, const float* u, float* r) {
@@ -1875,9 +1877,9 @@ struct TPhys {
         if (pos == 6 || pos == 14) live = live && __ballot(fmaxf(pk[0], fmaxf(pk[1], pk[2])) > 0.0f) != 0ull;
         if (!live) return;
         float d[3];
-        nf_dot3<f>(Tm[0], Tm[1], Tm[2], d);
+        nf_off_dot3<f>(Tm[0], Tm[1], Tm[2], d);
 #pragma unroll
-        for (int j = 0; j < 3; j++) pk[j] = fminf(pk[j], nf_off_minus<f>(d[j]));
+        for (int j = 0; j < 3; j++) pk[j] = fminf(pk[j], d[j]);
       });
 #pragma unroll
       for (int j = 0; j < 3; j++) {
@@ -2266,7 +2268,7 @@ struct TPhys {
     int a_ = 1 << 20;
 #pragma unroll
     for (int s = PPL - 1; s >= 0; s--)
-      if (cd[s] > 0.0f && cd[s] >= dmax - HF_DEPTH_TIE) a_ = sub + 8 * s;
+      a_ = (cd[s] > 0.0f) & (cd[s] >= dmax - HF_DEPTH_TIE) ? sub + 8 * s : a_;  // (& : selects, not branches)
     a_ = hmin8i(a_);
     a_ = a_ < QN ? a_ : 0;
     // a contact's fields, fetched from its owner lane (q uniform over the half-team)
@@ -2292,7 +2294,7 @@ struct TPhys {
       int best = 1 << 20;
 #pragma unroll
       for (int s = PPL - 1; s >= 0; s--)
-        if (cd[s] > 0.0f && v[s] >= mx - tol) best = sub + 8 * s;
+        best = (cd[s] > 0.0f) & (v[s] >= mx - tol) ? sub + 8 * s : best;
       best = hmin8i(best);
       return best < QN ? best : a_;
     };
@@ -2341,11 +2343,11 @@ struct TPhys {
       int best = 1 << 20;
 #pragma unroll
       for (int s = PPL - 1; s >= 0; s--) {
-        if (cd[s] > 0.0f && s2[s] >= mx - MANIFOLD_TOL) best = QN + sub + 8 * s;
+        best = (cd[s] > 0.0f) & (s2[s] >= mx - MANIFOLD_TOL) ? QN + sub + 8 * s : best;
       }
 #pragma unroll
       for (int s = PPL - 1; s >= 0; s--) {
-        if (cd[s] > 0.0f && s1[s] >= mx - MANIFOLD_TOL) best = sub + 8 * s;
+        best = (cd[s] > 0.0f) & (s1[s] >= mx - MANIFOLD_TOL) ? sub + 8 * s : best;
       }
       d_ = hmin8i(best);
       d_ = d_ < 2 * QN ? (d_ >= QN ? d_ - QN : d_) : a_;
