@@ -1676,7 +1676,19 @@ struct TPhys {
     };
     // the hull's faces (compile-time normals): the prism's lowest point along n_f, a bottom vertex
     // where n_f leans up the field's z (priority 5 + f; mu is formed after the SAT for these)
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 20
+    for (int rep_ = 0; rep_ < 2; rep_++)
+#endif
     {
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 20
+      float Tm_l[3][3], zc_l[3] = {zc[0], zc[1], zc[2]};
+      for (int k = 0; k < 3; k++)
+        for (int a = 0; a < 3; a++) Tm_l[k][a] = Tm[k][a];
+      launder<9>(&Tm_l[0][0]);
+      launder<3>(zc_l);
+      const auto& Tm = Tm_l;
+      const auto& zc = zc_l;
+#endif
       const float hk[3] = {d4.w - base, d5.w - base, d6.w - base};
       static_for<0, NF>([&](auto fI) {
         constexpr int f = fI.value;
@@ -1993,13 +2005,17 @@ struct TPhys {
     const float X0 = ((float)cmin - CC0) * DXC - t[0], Y0 = ((float)rmin - RC0) * DYC - t[1];
     const float base = -SB - t[2];  // the prisms' bottom (local z)
     // the sub-grid's elevations (local z), one global load per lane: vertex v = iy (ncx + 1) + ix
-    // on lane v & 7, register v >> 3; prisms read them by shuffles
-    float zg[GPL];
+    // on lane v & 7, register v >> 3; prisms read them by shuffles. The loads are unconditional (an
+    // in-range index on every lane) and issue here, back to back; the side minima and the silhouette
+    // lists run before their first use (as conditional loads each waited for itself at once: two
+    // exposed L2 round trips per substep)
+    float zg[GPL], hraw[GPL];
+    bool zok[GPL];
 #pragma unroll
     for (int i = 0; i < GPL; i++) {
       const int v = sub + 8 * i, iy = v / (ncx + 1), ix = v - iy * (ncx + 1);
-      const bool ok = np > 0 && iy <= ncy;
-      zg[i] = ok ? SZ * hf[(rmin + iy) * NCc + cmin + ix] - t[2] : 0.0f;
+      zok[i] = np > 0 && iy <= ncy;
+      hraw[i] = hf[zok[i] ? (rmin + iy) * NCc + cmin + ix : 0];
     }
     auto zat = [&](int ix, int iy) -> float {  // any lane pattern: every lane supplies both registers
       const int v = iy * (ncx + 1) + ix, src = 8 * h + (v & 7);
@@ -2031,8 +2047,6 @@ struct TPhys {
       const float sg = (nt[2] < 0.0f ? -1.0f : 1.0f) / sqrtf(dot3(nt, nt));
       for (int a = 0; a < 3; a++) nt[a] *= sg;
     };
-    // the hull's lowest point along each side normal (the six directions of the two triangle
-    // kinds: A (-x, +g, -y), B (-g, +x, +y))
     // the hull's lowest point along each side normal (the six directions of the two triangle kinds:
     // A (-x, +g, -y), B (-g, +x, +y))
     const float sx_[2][3] = {{-1.0f, GX, 0.0f}, {-GX, 1.0f, 0.0f}}, sy_[2][3] = {{0.0f, GY, -1.0f}, {-GY, 0.0f, 1.0f}};
@@ -2048,6 +2062,51 @@ struct TPhys {
         smin[ty][k] = hmin8f(mv);
       }
     const float obot = hi[2] - base;
+    // this foot's silhouette edges (the hull's edges whose faces straddle the field's horizontal
+    // plane: the only ones whose Gauss arc crosses a prism's vertical-edge arc), compacted in edge
+    // order into the env slice's composite-inertia storage (dead after crb()): the direction w in
+    // which the negated arc crosses the equator and the hull's support along it
+    lds_float* const SLo = L + HF_CINQ + h * HF_SLSZ;
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 17
+    for (int rep_ = 0; rep_ < 2; rep_++)
+#endif
+    {
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 17
+      float zc_l[3] = {zc[0], zc[1], zc[2]};
+      launder<3>(zc_l);
+      const auto& zc = zc_l;
+#endif
+      unsigned long long M = 0;
+      float wv[EPL][3], wh[EPL];
+      bool sl[EPL];
+#pragma unroll
+      for (int j = 0; j < EPL; j++) {
+        const int e = sub + 8 * j, ee = e < NE ? e : 0, o = Md::B_HEDGE + 20 * ee;
+        const f4v C4 = ht4(o), D4 = ht4(o + 4), v04 = ht4(o + 16);
+        const float C[3] = {C4.x, C4.y, C4.z}, D[3] = {D4.x, D4.y, D4.z}, v0[3] = {v04.x, v04.y, v04.z};
+        const float sa = dot3(C, zc), sb = dot3(D, zc);
+        const float w[3] = {fabsf(sb) * C[0] + fabsf(sa) * D[0], fabsf(sb) * C[1] + fabsf(sa) * D[1],
+                            fabsf(sb) * C[2] + fabsf(sa) * D[2]};
+        const float wn = sqrtf(dot3(w, w));
+        sl[j] = e < NE && sa * sb < 0.0f && wn > 0.0f;
+        const float inv = sl[j] ? 1.0f / wn : 0.0f;
+        for (int a = 0; a < 3; a++) wv[j][a] = w[a] * inv;
+        wh[j] = dot3(wv[j], v0);
+        M |= (unsigned long long)half_bits(__ballot(sl[j]), lane) << (8 * j);
+      }
+#pragma unroll
+      for (int j = 0; j < EPL; j++) {
+        const int e = sub + 8 * j;
+        const int r = __popcll(M & ((1ull << e) - 1ull));
+        if (sl[j] && r < Md::HF_SILCAP) {
+          ((lds_int*)SLo)[1 + r] = e;
+          ((lds_f4*)(SLo + HF_SLF))[r] = f4v{wv[j][0], wv[j][1], wv[j][2], wh[j]};
+        }
+      }
+      if (sub == 0) ((lds_int*)SLo)[0] = min(__popcll(M), Md::HF_SILCAP);
+    }
+#pragma unroll
+    for (int i = 0; i < GPL; i++) zg[i] = zok[i] ? SZ * hraw[i] - t[2] : 0.0f;
     // 1. lane-parallel screen: prism q = sub + 8 j passes the height test and the axes of its own
     // faces, the bottom and the hull's faces (the hull's support along its top normal from the
     // compile-time vertices). The running minimum and its axis priority are kept: the survivors'
@@ -2106,49 +2165,6 @@ struct TPhys {
 #if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 14
     }
 #endif
-    // this foot's silhouette edges (the hull's edges whose faces straddle the field's horizontal
-    // plane: the only ones whose Gauss arc crosses a prism's vertical-edge arc), compacted in edge
-    // order into the env slice's composite-inertia storage (dead after crb()): the direction w in
-    // which the negated arc crosses the equator and the hull's support along it
-    lds_float* const SLo = L + HF_CINQ + h * HF_SLSZ;
-#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 17
-    for (int rep_ = 0; rep_ < 2; rep_++)
-#endif
-    {
-#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 17
-      float zc_l[3] = {zc[0], zc[1], zc[2]};
-      launder<3>(zc_l);
-      const auto& zc = zc_l;
-#endif
-      unsigned long long M = 0;
-      float wv[EPL][3], wh[EPL];
-      bool sl[EPL];
-#pragma unroll
-      for (int j = 0; j < EPL; j++) {
-        const int e = sub + 8 * j, ee = e < NE ? e : 0, o = Md::B_HEDGE + 20 * ee;
-        const f4v C4 = ht4(o), D4 = ht4(o + 4), v04 = ht4(o + 16);
-        const float C[3] = {C4.x, C4.y, C4.z}, D[3] = {D4.x, D4.y, D4.z}, v0[3] = {v04.x, v04.y, v04.z};
-        const float sa = dot3(C, zc), sb = dot3(D, zc);
-        const float w[3] = {fabsf(sb) * C[0] + fabsf(sa) * D[0], fabsf(sb) * C[1] + fabsf(sa) * D[1],
-                            fabsf(sb) * C[2] + fabsf(sa) * D[2]};
-        const float wn = sqrtf(dot3(w, w));
-        sl[j] = e < NE && sa * sb < 0.0f && wn > 0.0f;
-        const float inv = sl[j] ? 1.0f / wn : 0.0f;
-        for (int a = 0; a < 3; a++) wv[j][a] = w[a] * inv;
-        wh[j] = dot3(wv[j], v0);
-        M |= (unsigned long long)half_bits(__ballot(sl[j]), lane) << (8 * j);
-      }
-#pragma unroll
-      for (int j = 0; j < EPL; j++) {
-        const int e = sub + 8 * j;
-        const int r = __popcll(M & ((1ull << e) - 1ull));
-        if (sl[j] && r < Md::HF_SILCAP) {
-          ((lds_int*)SLo)[1 + r] = e;
-          ((lds_f4*)(SLo + HF_SLF))[r] = f4v{wv[j][0], wv[j][1], wv[j][2], wh[j]};
-        }
-      }
-      if (sub == 0) ((lds_int*)SLo)[0] = min(__popcll(M), Md::HF_SILCAP);
-    }
     float cd[PPL], cn[PPL][3], cx[PPL][3];  // this lane's prism contacts: depth, normal, point (local)
 #pragma unroll
     for (int s = 0; s < PPL; s++) {
@@ -2268,7 +2284,7 @@ struct TPhys {
     int a_ = 1 << 20;
 #pragma unroll
     for (int s = PPL - 1; s >= 0; s--)
-      a_ = (cd[s] > 0.0f) & (cd[s] >= dmax - HF_DEPTH_TIE) ? sub + 8 * s : a_;  // (& : selects, not branches)
+      a_ = ((cd[s] > 0.0f) & (cd[s] >= dmax - HF_DEPTH_TIE)) ? sub + 8 * s : a_;  // (& : selects, not branches)
     a_ = hmin8i(a_);
     a_ = a_ < QN ? a_ : 0;
     // a contact's fields, fetched from its owner lane (q uniform over the half-team)
@@ -2294,7 +2310,7 @@ struct TPhys {
       int best = 1 << 20;
 #pragma unroll
       for (int s = PPL - 1; s >= 0; s--)
-        best = (cd[s] > 0.0f) & (v[s] >= mx - tol) ? sub + 8 * s : best;
+        best = ((cd[s] > 0.0f) & (v[s] >= mx - tol)) ? sub + 8 * s : best;
       best = hmin8i(best);
       return best < QN ? best : a_;
     };
@@ -2343,11 +2359,11 @@ struct TPhys {
       int best = 1 << 20;
 #pragma unroll
       for (int s = PPL - 1; s >= 0; s--) {
-        best = (cd[s] > 0.0f) & (s2[s] >= mx - MANIFOLD_TOL) ? QN + sub + 8 * s : best;
+        best = ((cd[s] > 0.0f) & (s2[s] >= mx - MANIFOLD_TOL)) ? QN + sub + 8 * s : best;
       }
 #pragma unroll
       for (int s = PPL - 1; s >= 0; s--) {
-        best = (cd[s] > 0.0f) & (s1[s] >= mx - MANIFOLD_TOL) ? sub + 8 * s : best;
+        best = ((cd[s] > 0.0f) & (s1[s] >= mx - MANIFOLD_TOL)) ? sub + 8 * s : best;
       }
       d_ = hmin8i(best);
       d_ = d_ < 2 * QN ? (d_ >= QN ? d_ - QN : d_) : a_;
@@ -3419,7 +3435,7 @@ struct TPhys {
     // DUCK_DOUBLE (measurement builds, tools/gpu_stage_double.sh, tools/gpu_stage_pmc.sh): one
     // idempotent stage runs twice, and the launch-time (and counter) difference to the normal build
     // is that stage's cost, unperturbed by markers: 1 crb, 2 collision, 3 make_rows, 4 smooth_acc,
-    // 5 solve, 6 kinematics, 7 com_pos, 8 rne + smooth
+    // 5 solve, 6 kinematics, 7 com_pos, 8 rne + smooth (height field: 11-20, tools/stage_pmc_summary.py)
 #if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 1
     crb(L, lane);
 #endif
