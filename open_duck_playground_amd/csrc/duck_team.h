@@ -752,6 +752,22 @@ struct TPhys {
     }
     TSYNC();
   }
+  static constexpr bool bodies_distinct() {
+    for (int m = 0; m < Md::T_NBR; m++)
+      for (int d = 0; d < Md::T_BRLEN; d++) {
+        const int b = Md::T_BRB[m][d];
+        if (b < 0) continue;
+        for (int m2 = 0; m2 < Md::T_NBR; m2++)
+          for (int d2 = 0; d2 < Md::T_BRLEN; d2++)
+            if ((m2 != m || d2 != d) && Md::T_BRB[m2][d2] == b) return false;
+        for (int r = 0; r < Md::T_NROOT; r++)
+          if (Md::T_ROOT[r] == b) return false;
+      }
+    for (int r = 0; r < Md::T_NROOT; r++)
+      for (int r2 = r + 1; r2 < Md::T_NROOT; r2++)
+        if (Md::T_ROOT[r] == Md::T_ROOT[r2]) return false;
+    return true;
+  }
   // phase C of rne: PART 0 both sums, PART 1 the forces (inertia lanes into XDUM0), PART 2 the
   // composite inertias (force lanes read CIN and write XDUM1: no read of rne's forces in flight)
   template <int PART>
@@ -769,6 +785,20 @@ struct TPhys {
       const int idst = PART == 1 ? TL::XDUM0 + (lk - 6) : TL::XCIN + (lk - 6);
       const int src = fk ? fsrc : Ly::CIN + (lk - 6), dst = fk ? fdst : idst;
       const int st = fk ? 6 : 10;
+      // every body's word first, in one batch: the bodies are distinct (bodies_distinct), so no store
+      // below (in place for the inertias in throughput mode) feeds a later read. Interleaved, the
+      // loads could not pass the stores (same region) and each body cost an LDS round trip
+      static_assert(bodies_distinct(), "limb and root bodies must be distinct");
+      float xb[Md::T_NBR][BL], xr[NR];
+#pragma unroll
+      for (int m = 0; m < Md::T_NBR; m++)
+#pragma unroll
+        for (int d = 0; d < BL; d++) {
+          const int b = Md::T_BRB[m][d];
+          xb[m][d] = b >= 0 ? L[src + st * (b >= 0 ? b : 0)] : 0.0f;
+        }
+#pragma unroll
+      for (int r = 0; r < NR; r++) xr[r] = L[src + st * Md::T_ROOT[r]];
       float tot = 0.0f;
 #pragma unroll
       for (int m = 0; m < Md::T_NBR; m++) {
@@ -777,7 +807,7 @@ struct TPhys {
         for (int d = BL - 1; d >= 0; d--) {
           const int b = Md::T_BRB[m][d];
           if (b < 0) continue;
-          acc += L[src + st * b];
+          acc += xb[m][d];
           L[dst + st * b] = acc;
         }
         tot = m == 0 ? acc : tot + acc;
@@ -786,7 +816,7 @@ struct TPhys {
 #pragma unroll
       for (int r = NR - 1; r >= 0; r--) {
         const int b = Md::T_ROOT[r];
-        tot += L[src + st * b];
+        tot += xr[r];
         L[dst + st * b] = tot;
       }
     }
@@ -1103,14 +1133,26 @@ struct TPhys {
       // lane opaque: the table words are per-lane constants, which the compiler would otherwise
       // hoist out of the substep loop and keep in registers (+39 AGPRs)
       asm volatile("" : "+v"(lane));
+      // in groups of G entries: G table words, then G M words. Written entry by entry, the
+      // scheduler (short of registers here) alternated one table load and one M load with a wait
+      // for each: 2 NV dependent LDS round trips per substep (C5 +2.3 %; with a scheduling barrier
+      // between the groups C2 lost 0.9 %, without one it gains 0.6 %)
+      constexpr int G = 10;
 #pragma unroll
       for (int s = 0; s < NC; s++) {
 #pragma unroll
-        for (int r = 0; r < NV; r++) {
-          if (lower_only && r < TEAM * s) { col[s][r] = 0.0f; continue; }  // above the diagonal
-          // (with lower_only the entries right of the diagonal may stay: the factorization's lower
-          // triangle never reads them, and factor_solve drops them afterwards)
-          col[s][r] = L[Ly::M + ti(Md::B_MCOLZ + TEAM * (NV * s + r) + lane)];
+        for (int r0 = 0; r0 < NV; r0 += G) {
+          int a[G];
+#pragma unroll
+          for (int r = r0; r < r0 + G && r < NV; r++)
+            if (!(lower_only && r < TEAM * s)) a[r - r0] = ti(Md::B_MCOLZ + TEAM * (NV * s + r) + lane);
+#pragma unroll
+          for (int r = r0; r < r0 + G && r < NV; r++) {
+            if (lower_only && r < TEAM * s) { col[s][r] = 0.0f; continue; }  // above the diagonal
+            // (with lower_only the entries right of the diagonal may stay: the factorization's lower
+            // triangle never reads them, and factor_solve drops them afterwards)
+            col[s][r] = L[Ly::M + a[r - r0]];
+          }
         }
       }
     } else {
