@@ -2996,6 +2996,9 @@ struct TPhys {
   static DK void solve(LP L, int lane, float* scratch, int stride, const float (*Mc)[NV]) {
     STAGE_T0();
     const float g0 = warm_start(L, lane, Mc);
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 21
+    (void)warm_start(L, lane, Mc);
+#endif
     newton(L, lane, scratch, stride, Mc, g0);
   }
   // latency mode: the warm start's products that need only qacc_warmstart (its feet motions, M and J
@@ -3177,6 +3180,9 @@ struct TPhys {
       sparse_ok = true;
     } else {
       sparse_ok = newton_fused<false>(L, lane, Mc);
+#if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 22
+      sparse_ok = newton_fused<false>(L, lane, Mc);
+#endif
     }
     STAGE_MARK(10);
     if (sparse_ok) {

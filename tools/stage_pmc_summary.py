@@ -21,7 +21,7 @@ STAGES = {1: "crb", 2: "collision", 3: "make_rows", 4: "smooth_acc (qacc_smooth 
           5: "solve (warm start + Newton + line search)", 6: "kinematics", 7: "com_pos", 8: "rne + smooth",
           11: "hf SAT pass 2", 12: "hf SAT pass 1", 13: "hf contact point", 14: "hf screen",
           15: "hf vertical-edge pairs", 16: "hf setup (frames, hull vertices, box, sub-grid, side minima)",
-          17: "hf silhouette lists", 18: "hf survivor descriptors", 19: "hf manifold slots + contact stores", 20: "hf hull-face axes"}
+          17: "hf silhouette lists", 18: "hf survivor descriptors", 19: "hf manifold slots + contact stores", 20: "hf hull-face axes", 21: "warm start", 22: "Newton direction (gradient, J'DJ, factor + solves)"}
 
 
 def build(variant, stages):
