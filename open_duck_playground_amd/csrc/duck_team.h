@@ -3282,7 +3282,9 @@ struct TPhys {
     }
     Pt lo;
     {
-      const float a1 = p0.alpha - p0.d0 / p0.d1;
+      // (as the loop's steps: alpha - d0 v_rcp(d1); written as a division this one, at alpha = 0, compiled
+      // to the correctly rounded sequence with two MODE register writes)
+      const float a1 = p0.alpha - p0.d0 * frcp(p0.d1);
       float q0 = 0, q1 = 0, q2 = 0;
       quad2(R, a1, q0, q1, q2);
       lo = mk(a1, q0, q1, q2);
