@@ -1972,7 +1972,8 @@ struct TPhys {
         wp_ += w;
         for (int a = 0; a < 3; a++) cq[a] += w * Tm[k][a];
       }
-      for (int a = 0; a < 3; a++) pos[a] = 0.5f * (ch[a] / wh_ + cq[a] / wp_);
+      const float iwh = frcp(wh_), iwp = frcp(wp_);
+      for (int a = 0; a < 3; a++) pos[a] = 0.5f * (ch[a] * iwh + cq[a] * iwp);
     }
     E4[0] = f4v{mo, mu[0], mu[1], mu[2]};
     E4[1] = f4v{pos[0], pos[1], pos[2], 0.0f};
@@ -2131,7 +2132,7 @@ struct TPhys {
                             fabsf(sb) * C[2] + fabsf(sa) * D[2]};
         const float wn = sqrtf(dot3(w, w));
         sl[j] = e < NE && sa * sb < 0.0f && wn > 0.0f;
-        const float inv = sl[j] ? 1.0f / wn : 0.0f;
+        const float inv = sl[j] ? frcp(wn) : 0.0f;  // (1.0f / wn compiled to the correctly rounded division)
         for (int a = 0; a < 3; a++) wv[j][a] = w[a] * inv;
         wh[j] = dot3(wv[j], v0);
         M |= (unsigned long long)half_bits(__ballot(sl[j]), lane) << (8 * j);
