@@ -3427,8 +3427,11 @@ struct TPhys {
       if (typ == 7 && site == Md::RFOOT_SITE) L[Ly::FOOTZ + 1] = sp[2];
     }
     if (lane < 2) {
-      const int p = Md::PLANE_PAIR[lane];
-      const int s2 = cgeom_slot<Md>(Md::pair_geom2[p]);
+      // (compile-time table entries selected by lane: indexed by lane, the tables were read from
+      // global memory with an exposed load)
+      constexpr int p0 = Md::PLANE_PAIR[0], p1 = Md::PLANE_PAIR[1];
+      constexpr int s20 = cgeom_slot<Md>(Md::pair_geom2[p0]), s21 = cgeom_slot<Md>(Md::pair_geom2[p1]);
+      const int p = lane == 0 ? p0 : p1, s2 = lane == 0 ? s20 : s21;
       float mn = 1e4f;
       for (int c = 0; c < 4; c++) mn = fminf(mn, L[Ly::CDIST + 4 * p + c]);
       L[Ly::OCON + s2 - 1] = mn < 0.0f ? 1.0f : 0.0f;
