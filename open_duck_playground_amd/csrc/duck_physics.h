@@ -28,7 +28,7 @@ typedef __attribute__((address_space(3))) float lds_float;
 #define DUCK_ANY_PROF 1
 #endif
 #ifdef DUCK_ANY_PROF
-#define DUCK_NSTAGE 56
+#define DUCK_NSTAGE 60
 static __device__ unsigned long long g_stage_cycles[DUCK_NSTAGE + 3 * 1024];
 // the stage counters themselves are kept per workgroup slot (summed by the host): one shared
 // counter per stage made every workgroup's atomics contend at one L2 channel, which slowed whole

@@ -3306,11 +3306,18 @@ struct TPhys {
       done = done || ((hi.d0 > 0.0f) && (hi.d0 < gtol_ls));
       stop = done;
 #else
+#ifdef DUCK_STAGE_PROF
+    int its = 0;
+#endif
     for (int it = 0; it < Md::ls_iterations; it++) {
       bool done = !swap;
       done = done || ((lo.d0 < 0.0f) && (lo.d0 > -gtol_ls));
       done = done || ((hi.d0 > 0.0f) && (hi.d0 < gtol_ls));
       if (done) break;
+#ifdef DUCK_STAGE_PROF
+      its = it + 1;
+      if (threadIdx.x < 64 && (int)threadIdx.x == __ffsll((long long)__ballot(1)) - 1) STAGE_ADD(56, 1ull);
+#endif
 #endif
       const float al = lo.alpha - lo.d0 / lo.d1, ah = hi.alpha - hi.d0 / hi.d1, am = 0.5f * (lo.alpha + hi.alpha);
       float a0 = 0, a1 = 0, a2 = 0, b0 = 0, b1 = 0, b2 = 0, c0 = 0, c1 = 0, c2 = 0;
@@ -3340,6 +3347,9 @@ struct TPhys {
       swap = s1 || s2 || s3 || s4;
 #endif
     }
+#if defined(DUCK_STAGE_PROF) && !defined(DUCK_LS_NOBREAK)
+    if (threadIdx.x < 64 && (lane & 15) == 0) { STAGE_ADD(57, (unsigned long long)its); STAGE_ADD(58, 1ull); }
+#endif
     const float lo_cost = cost(lo), hi_cost = cost(hi), p0_cost = cost(p0);
     const bool improved = (lo_cost < p0_cost) || (hi_cost < p0_cost);
     const float alpha = lo_cost < hi_cost ? lo.alpha : hi.alpha;

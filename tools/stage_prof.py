@@ -25,7 +25,7 @@ SUB = {24: "kinematics:local", 21: "rne:A vel/acc", 22: "rne:A+B forces", 35: "r
        13: "solve:linesearch", 37: "hfield: setup+screen+silhouettes", 38: "hfield: survivor queue", 39: "hfield: slots",
        41: "  queue: descriptors", 42: "  queue: per-lane SAT", 43: "  queue: gather",
        44: "    sat: vertical pairs", 45: "    sat: pass 1 (arc tests)", 47: "    sat: pass 2 (crossing pairs)"}
-NSTAGE = 56  # DUCK_NSTAGE
+NSTAGE = 60  # DUCK_NSTAGE
 ENV = {32: "env: hot state load", 33: "env: rng draws", 29: "env: pre-physics (per env-step)", 30: "env: contacts+obs",
        31: "env: termination+rewards+state", 34: "env: obs/priv stores", 15: "env: hot state store"}
 
@@ -101,6 +101,10 @@ def main():
     kern = outside + tot / (nwg * steps)
     if per(14) == 0:
         return
+    if buf[58] > 0:
+        # line search (wave 0 of each workgroup): iterations the wave ran vs its teams needed
+        print(f"{'line search iterations':28s} per team {buf[57] / buf[58]:.2f}, per wave {4 * buf[56] / buf[58]:.2f} "
+              f"({buf[58] / (nwg * steps * 10) / 4:.2f} searches per team and substep)")
     print(f"{'kernel (per env-step)':28s} {kern:10.0f} cycles/env-step/wave (sum of the marked sections)")
     print(f"{'  model-table copy':28s} {per(14):10.0f}  {100 * per(14) / kern:5.1f}%")
     print(f"{'  10 substeps':28s} {tot / (nwg * steps):10.0f}  {100 * tot / (nwg * steps) / kern:5.1f}%")
