@@ -2415,17 +2415,21 @@ struct TPhys {
     // half-team: a lane's shuffle source selects its slot with the requester's index)
     float pdd[3], ndd[3], ddd;
     fetch(d_, pdd, ndd, ddd);
-    const int myq = sub == 0 ? a_ : (sub == 1 ? b_ : (sub == 2 ? c_ : d_));
+    // slot sub's contact by v_cndmask on the lanes' sub masks: written as nested ?: on sub, the compiler
+    // made each of the seven values a tree of exec-masked branches
+    const unsigned long long m0 = __ballot(sub == 0), m1 = __ballot(sub == 1), m2 = __ballot(sub == 2);
+    auto pick = [&](float v0, float v1, float v2, float v3) { return vsel(m0, v0, vsel(m1, v1, vsel(m2, v2, v3))); };
+    const int myq = (sub == 0) * a_ + (sub == 1) * b_ + (sub == 2) * c_ + (sub >= 3) * d_;
     float px[3], pn[3], pd;
     for (int a = 0; a < 3; a++) {
-      px[a] = sub == 0 ? pa[a] : (sub == 1 ? pb[a] : (sub == 2 ? pc[a] : pdd[a]));
-      pn[a] = sub == 0 ? na[a] : (sub == 1 ? nb[a] : (sub == 2 ? nc_[a] : ndd[a]));
+      px[a] = pick(pa[a], pb[a], pc[a], pdd[a]);
+      pn[a] = pick(na[a], nb[a], nc_[a], ndd[a]);
     }
-    pd = sub == 0 ? da : (sub == 1 ? db : (sub == 2 ? dcc : ddd));
+    pd = pick(da, db, dcc, ddd);
     if (sub < 4) {
       const int idx[4] = {a_, b_, c_, d_};
       bool unique = true;
-      for (int e = 0; e < 4; e++) unique = unique && !(e < sub && idx[e] == myq);
+      for (int e = 0; e < 4; e++) unique = unique & !((e < sub) & (idx[e] == myq));
       float fr[9], pw[3], nw[3];
       if (any) {
         const float pl[3] = {px[0] + t[0], px[1] + t[1], px[2] + t[2]};
