@@ -76,6 +76,16 @@ DK float tsum(float v) {
   v += dppf<0x140>(v);  // row_mirror
   return v;
 }
+// for (i = lane; i < N; i += TEAM) f(i), the trip count unrolled at compile time: straight-line code
+// instead of a loop whose trip count depends on the lane (exec-masked loop control per iteration)
+template <int N, class F>
+DK void team_for(int lane, F&& f) {
+#pragma unroll
+  for (int s = 0; s < (N + TEAM - 1) / TEAM; s++) {
+    const int i = lane + TEAM * s;
+    if (TEAM * (s + 1) <= N || i < N) f(i);
+  }
+}
 DK float tmaxf(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));
@@ -744,12 +754,12 @@ struct TPhys {
     // tip (the limb bodies are compile-time, Md::T_BRB), then the limb totals, then the root path.
     // Each component's additions run in the same order as a limb-per-lane pass.
     subtree_sums<PART>(L, lane);
-    for (int i = lane; i < NV; i += TEAM) {
+    team_for<NV>(lane, [&](int i) {
       const int b = dof_body(i);
       float s = 0.0f;
       for (int k = 0; k < 6; k++) s += L[Ly::CDOF + 6 * i + k] * L[TL::CFRC + 6 * b + k];
       L[Ly::FSM + i] = -s;
-    }
+    });
     TSYNC();
   }
   static constexpr bool bodies_distinct() {
@@ -921,7 +931,7 @@ struct TPhys {
 #ifdef DUCK_ASM_MARKS
     asm volatile("; SMOOTH_BEGIN" ::: "memory");
 #endif
-    for (int i = lane; i < NV; i += TEAM) L[Ly::FSM + i] += -tf(Md::B_DAMP + i) * L[Ly::QVEL + i];
+    team_for<NV>(lane, [&](int i) { L[Ly::FSM + i] += -tf(Md::B_DAMP + i) * L[Ly::QVEL + i]; });
     TSYNC();
     if (lane < NU) {
       const int a = lane, o = Md::B_ACT + 12 * a;
@@ -3082,18 +3092,17 @@ struct TPhys {
         L[Ly::JV + row] = js;
       }
     }
-    for (int i = lane; i < NV; i += TEAM)
-      gwp += 0.5f * (L[Ly::MA + i] - L[Ly::FSM + i]) * (L[Ly::WARM + i] - L[Ly::QSM + i]);
+    team_for<NV>(lane, [&](int i) { gwp += 0.5f * (L[Ly::MA + i] - L[Ly::FSM + i]) * (L[Ly::WARM + i] - L[Ly::QSM + i]); });
     const float gw = tsum(gwp);
     const float cw = gw + tsum(cwp), cs = tsum(csp);
     float g0;
     warm = cw < cs;
     if (warm) {
-      for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] = L[Ly::WARM + i];
+      team_for<NV>(lane, [&](int i) { L[Ly::QACC + i] = L[Ly::WARM + i]; });
       g0 = gw;
     } else {
-      for (int i = lane; i < NV; i += TEAM) { L[Ly::QACC + i] = L[Ly::QSM + i]; L[Ly::MA + i] = L[Ly::FSM + i]; }
-      for (int r = lane; r < NROW; r += TEAM) L[Ly::JA + r] = L[Ly::JV + r];
+      team_for<NV>(lane, [&](int i) { L[Ly::QACC + i] = L[Ly::QSM + i]; L[Ly::MA + i] = L[Ly::FSM + i]; });
+      team_for<NROW>(lane, [&](int r) { L[Ly::JA + r] = L[Ly::JV + r]; });
       g0 = 0.0f;
     }
     TSYNC();
@@ -3152,17 +3161,16 @@ struct TPhys {
         L[Ly::JV + row] = js;
       }
     }
-    for (int i = lane; i < NV; i += TEAM)
-      gwp += 0.5f * (L[Ly::MA + i] - L[Ly::FSM + i]) * (L[Ly::WARM + i] - L[Ly::QSM + i]);
+    team_for<NV>(lane, [&](int i) { gwp += 0.5f * (L[Ly::MA + i] - L[Ly::FSM + i]) * (L[Ly::WARM + i] - L[Ly::QSM + i]); });
     const float gw = tsum(gwp);
     const float cw = gw + tsum(cwp), cs = tsum(csp);
     float g0;
     if (cw < cs) {
-      for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] = L[Ly::WARM + i];
+      team_for<NV>(lane, [&](int i) { L[Ly::QACC + i] = L[Ly::WARM + i]; });
       g0 = gw;
     } else {
-      for (int i = lane; i < NV; i += TEAM) { L[Ly::QACC + i] = L[Ly::QSM + i]; L[Ly::MA + i] = L[Ly::FSM + i]; }
-      for (int r = lane; r < NROW; r += TEAM) L[Ly::JA + r] = L[Ly::JV + r];
+      team_for<NV>(lane, [&](int i) { L[Ly::QACC + i] = L[Ly::QSM + i]; L[Ly::MA + i] = L[Ly::FSM + i]; });
+      team_for<NROW>(lane, [&](int r) { L[Ly::JA + r] = L[Ly::JV + r]; });
       g0 = 0.0f;  // gauss(qacc_smooth) = 0.5 (M qs - f).(qs - qs) = 0
     }
     TSYNC();
@@ -3180,7 +3188,7 @@ struct TPhys {
     for (int newton_it = 0;;) {
     bool sparse_ok;
     if (LAT && newton_it == 0 && __ballot(!pre_dir) == 0ull) {
-      for (int i = lane; i < NV; i += TEAM) L[Ly::SRCH + i] = L[TL::XDIR + i];
+      team_for<NV>(lane, [&](int i) { L[Ly::SRCH + i] = L[TL::XDIR + i]; });
       TSYNC();
       sparse_ok = true;
     } else {
@@ -3247,13 +3255,13 @@ struct TPhys {
       L[TL::KC + 120 + lane] = L[Ly::SRCH + lane];
     }
 #endif
-    for (int i = lane; i < NV; i += TEAM) {
+    team_for<NV>(lane, [&](int i) {
       const float sv = L[Ly::SRCH + i];
       sn += sv * sv;
       sMa += sv * L[Ly::MA + i];
       sf += sv * L[Ly::FSM + i];
       sMv += sv * L[Ly::GRAD + i];
-    }
+    });
 #ifdef DUCK_LS_DUMP
     L[TL::KC + 56 + lane] = (float)lane;
     L[TL::KC + 72 + lane] = sn;
@@ -3358,7 +3366,7 @@ struct TPhys {
     const bool improved = (lo_cost < p0_cost) || (hi_cost < p0_cost);
     const float alpha = lo_cost < hi_cost ? lo.alpha : hi.alpha;
     if (improved)
-      for (int i = lane; i < NV; i += TEAM) L[Ly::QACC + i] += L[Ly::SRCH + i] * alpha;
+      team_for<NV>(lane, [&](int i) { L[Ly::QACC + i] += L[Ly::SRCH + i] * alpha; });
     TSYNC();
     STAGE_MARK(13);
     if constexpr (Md::iterations <= 1) {
@@ -3372,7 +3380,7 @@ struct TPhys {
       const float a = improved ? alpha : 0.0f;
       const float cnew = improved ? (lo_cost < hi_cost ? lo_cost : hi_cost) : p0_cost;
       g0 = G0 + a * G1 + a * a * G2;  // gauss at the new point
-      for (int i = lane; i < NV; i += TEAM) L[Ly::MA + i] += a * L[Ly::GRAD + i];  // GRAD = M.search
+      team_for<NV>(lane, [&](int i) { L[Ly::MA + i] += a * L[Ly::GRAD + i]; });  // GRAD = M.search
       if (lane < NFRIC) L[Ly::JA + lane] = R.fja + a * R.fv;
 #pragma unroll
       for (int m = 0; m < NLR; m++) {
@@ -3456,10 +3464,10 @@ struct TPhys {
   // ---------------- semi-implicit Euler ----------------
   static DK void euler(LP L, int lane) {
     const float dt = Md::timestep;
-    for (int i = lane; i < NV; i += TEAM) {
+    team_for<NV>(lane, [&](int i) {
       L[Ly::WARM + i] = L[Ly::QACC + i];
       L[Ly::QVEL + i] += dt * L[Ly::QACC + i];
-    }
+    });
     TSYNC();
     if (lane == 0) {
       for (int k = 0; k < 3; k++) L[Ly::QPOS + k] += dt * L[Ly::QVEL + k];
@@ -3551,7 +3559,7 @@ struct TPhys {
     if (integrate) {
       euler(L, lane);
     } else {
-      for (int i = lane; i < NV; i += TEAM) L[Ly::WARM + i] = L[Ly::QACC + i];
+      team_for<NV>(lane, [&](int i) { L[Ly::WARM + i] = L[Ly::QACC + i]; });
       TSYNC();
     }
     STAGE_MARK(8);
@@ -3664,7 +3672,7 @@ struct TPhys {
     if (integrate) {
       euler(L, lane);
     } else {
-      for (int i = lane; i < NV; i += TEAM) L[Ly::WARM + i] = L[Ly::QACC + i];
+      team_for<NV>(lane, [&](int i) { L[Ly::WARM + i] = L[Ly::QACC + i]; });
       TSYNC();
     }
     ev_signal(EV_EULER, s + 1);
@@ -3793,7 +3801,7 @@ struct TPhys {
     if (integrate) {
       euler(L, lane);
     } else {
-      for (int i = lane; i < NV; i += TEAM) L[Ly::WARM + i] = L[Ly::QACC + i];
+      team_for<NV>(lane, [&](int i) { L[Ly::WARM + i] = L[Ly::QACC + i]; });
       TSYNC();
     }
     LAT2_T(22, s);
