@@ -78,12 +78,12 @@ DK float tsum(float v) {
 }
 // for (i = lane; i < N; i += TEAM) f(i), the trip count unrolled at compile time: straight-line code
 // instead of a loop whose trip count depends on the lane (exec-masked loop control per iteration)
-template <int N, class F>
+template <int N, int B0 = 0, class F>
 DK void team_for(int lane, F&& f) {
 #pragma unroll
-  for (int s = 0; s < (N + TEAM - 1) / TEAM; s++) {
-    const int i = lane + TEAM * s;
-    if (TEAM * (s + 1) <= N || i < N) f(i);
+  for (int s = 0; s < (N - B0 + TEAM - 1) / TEAM; s++) {
+    const int i = B0 + lane + TEAM * s;
+    if (B0 + TEAM * (s + 1) <= N || i < N) f(i);
   }
 }
 DK float tmaxf(float v) {
@@ -496,8 +496,8 @@ struct TPhys {
     STAGE_T0();
     // K1: local transform (body quat x joint rotations, body pos) of every moving body, a
     // body per lane, off the serial chain
-    for (int b = 2 + lane; b < NB; b += TEAM) {
-      if (!moving(b)) continue;
+    team_for<NB, 2>(lane, [&](int b) {
+      if (!moving(b)) return;
       const int o = Md::B_BKIN + 17 * b;
       float q[4] = {tf(o), tf(o + 1), tf(o + 2), tf(o + 3)};
       const int nj = ti(o + 7);
@@ -513,7 +513,7 @@ struct TPhys {
       }
       for (int k = 0; k < 4; k++) L[TL::KLOC + 7 * b + k] = q[k];
       for (int k = 0; k < 3; k++) L[TL::KLOC + 7 * b + 4 + k] = tf(o + 4 + k);
-    }
+    });
     TSYNC();
     STAGE_MARK(24);
     // K2: compose down the root path (every lane) and the limbs (a limb per lane)
@@ -609,7 +609,7 @@ struct TPhys {
       L[o + 6] = m * d[0]; L[o + 7] = m * d[1]; L[o + 8] = m * d[2];
       L[o + 9] = m;
     }
-    for (int j = lane; j < NJ; j += TEAM) {
+    team_for<NJ>(lane, [&](int j) {
       const int oj = Md::B_JREC + 9 * j;
       // affine joint maps (codegen B_JAFF): hinge j >= B_JN0 sits on body j + B_JBD with dof j + B_JDD
       const bool jh = Md::B_JAFF && j >= Md::B_JN0;
@@ -634,7 +634,7 @@ struct TPhys {
         const int o = Ly::CDOF + 6 * da;
         L[o] = ax[0]; L[o + 1] = ax[1]; L[o + 2] = ax[2]; L[o + 3] = t[0]; L[o + 4] = t[1]; L[o + 5] = t[2];
       }
-    }
+    });
     TSYNC();
   }
 
@@ -736,8 +736,8 @@ struct TPhys {
 #pragma clang fp reassociate(on)
     STAGE_T0();
     // (B) body forces, a body per lane
-    for (int b = 1 + lane; b < NB; b += TEAM) {
-      if (!moving(b)) continue;
+    team_for<NB, 1>(lane, [&](int b) {
+      if (!moving(b)) return;
       float I[10], v6[6], a6[6], f[6], t1[6], t2[6];
       for (int k = 0; k < 10; k++) I[k] = L[Ly::CIN + 10 * b + k];
       for (int k = 0; k < 6; k++) { v6[k] = L[Ly::CVEL + 6 * b + k]; a6[k] = L[RCA + 6 * b + k]; }
@@ -745,7 +745,7 @@ struct TPhys {
       mul_inert_vec(t1, I, v6);
       cross_force(t2, v6, t1);
       for (int k = 0; k < 6; k++) L[RFB + 6 * b + k] = f[k] + t2[k];
-    }
+    });
     TSYNC();
     STAGE_MARK(22);
     // (C) subtree sums of the body forces (rne) and of the body inertias (mj_crb's composite
@@ -2836,7 +2836,7 @@ struct TPhys {
       L[Ly::RD + r] = tf(Md::B_FRIC + 3 * r + 1);
       L[Ly::AREF + r] = -tf(Md::B_FRIC + 3 * r + 2) * L[Ly::QVEL + i];
     }
-    for (int r = lane; r < NLIM; r += TEAM) {
+    team_for<NLIM>(lane, [&](int r) {
       const int o = Md::B_LIM + LIMW * r;
       const int i = lim_dof(r), qa = lim_qadr(r);
       const float q = L[Ly::QPOS + qa];
@@ -2851,7 +2851,7 @@ struct TPhys {
       L[Ly::RD + R_LIM + r] = active ? frcp(R) : 0.0f;
       L[Ly::AREF + R_LIM + r] = active ? (-b * sgn * L[Ly::QVEL + i] - k * imp * pos) : 0.0f;
       L[Ly::LSGN + r] = sgn;
-    }
+    });
     if (lane < NCON) {
       const int slot = lane, p = slot >> 2, o = Md::B_PAIR + PAIRW * p;
       float SL[6], SR[6];
@@ -3040,13 +3040,13 @@ struct TPhys {
       cwp += fr ? fric_cost(D, jw, f) : 0.0f;
       L[fr ? Ly::JA + r : TL::SINK + lane] = jw;
     }
-    for (int r = lane; r < NLIM; r += TEAM) {
+    team_for<NLIM>(lane, [&](int r) {
       const int i = lim_dof(r), row = R_LIM + r;
       const float D = L[Ly::RD + row], sg = L[Ly::LSGN + r], ar = L[Ly::AREF + row];
       const float jw = sg * L[Ly::WARM + i] - ar;
       cwp += jw < 0.0f ? 0.5f * D * jw * jw : 0.0f;
       L[Ly::JA + row] = jw;
-    }
+    });
     if (lane < NCON) {
       float vw[4];
       contact_jx(L, lane >> 2, lane, SL, SR, vw);
@@ -3074,13 +3074,13 @@ struct TPhys {
       csp += fr ? fric_cost(D, js, f) : 0.0f;
       L[fr ? Ly::JV + r : TL::SINK + TEAM + lane] = js;
     }
-    for (int r = lane; r < NLIM; r += TEAM) {
+    team_for<NLIM>(lane, [&](int r) {
       const int i = lim_dof(r), row = R_LIM + r;
       const float D = L[Ly::RD + row], sg = L[Ly::LSGN + r], ar = L[Ly::AREF + row];
       const float js = sg * L[Ly::QSM + i] - ar;
       csp += js < 0.0f ? 0.5f * D * js * js : 0.0f;
       L[Ly::JV + row] = js;
-    }
+    });
     if (lane < NCON) {
       float vs[4];
       contact_jx(L, lane >> 2, lane, SL2, SR2, vs);
@@ -3138,7 +3138,7 @@ struct TPhys {
       L[fr ? Ly::JA + r : TL::SINK + lane] = jw;
       L[fr ? Ly::JV + r : TL::SINK + TEAM + lane] = js;
     }
-    for (int r = lane; r < NLIM; r += TEAM) {
+    team_for<NLIM>(lane, [&](int r) {
       const int i = lim_dof(r), row = R_LIM + r;
       const float D = L[Ly::RD + row], sg = L[Ly::LSGN + r], ar = L[Ly::AREF + row];
       const float jw = sg * L[Ly::WARM + i] - ar, js = sg * L[Ly::QSM + i] - ar;
@@ -3146,7 +3146,7 @@ struct TPhys {
       csp += js < 0.0f ? 0.5f * D * js * js : 0.0f;
       L[Ly::JA + row] = jw;
       L[Ly::JV + row] = js;
-    }
+    });
     if (lane < NCON) {
       float vw[4], vs[4];
       contact_jx(L, lane >> 2, lane, SL, SR, vw);
@@ -3483,12 +3483,12 @@ struct TPhys {
       qnormalize(q);
       for (int k = 0; k < 4; k++) L[Ly::QPOS + 3 + k] = q[k];
     }
-    for (int j = 1 + lane; j < NJ; j += TEAM) {
+    team_for<NJ, 1>(lane, [&](int j) {
       const int oj = Md::B_JREC + 9 * j;
       const bool jh = Md::B_JAFF && j >= Md::B_JN0;
       const int qa = jh ? j + Md::B_JQD : ti(oj + 2), da = jh ? j + Md::B_JDD : ti(oj + 1);
       L[Ly::QPOS + qa] += dt * L[Ly::QVEL + da];
-    }
+    });
     TSYNC();
   }
 
