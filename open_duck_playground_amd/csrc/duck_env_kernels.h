@@ -472,6 +472,17 @@ DK StepPre step_prefetch(const KArgs& A, int e, int lane) {
   return P;
 }
 
+// for (i = l0; i < N; i += TS) f(i) with the trip count unrolled at compile time (l0 < TS): straight-line
+// code instead of a loop whose trip count depends on the lane (team mode: l0 = lane, TS = TEAM)
+template <int N, int TS, class Fn>
+DK void strided_for(int l0, Fn&& f) {
+#pragma unroll
+  for (int s = 0; s < (N + TS - 1) / TS; s++) {
+    const int i = l0 + TS * s;
+    if (TS * (s + 1) <= N || i < N) f(i);
+  }
+}
+
 // Joystick.step body for env e (joystick.py:323-481 + wrappers); F = the env's hot state
 // (LDS-staged or the global row), G = the global row (auto-reset snapshot)
 template <class Md, class FA, bool STAGE_OBS, class RT, int LAT = 0>
@@ -531,11 +542,11 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   const float push[2] = {cosf(theta) * gate * (float)c.push_enable, sinf(theta) * gate * (float)c.push_enable};
   if constexpr (STAGE_OBS) {  // team: lane-split copies, sums by DPP
     arate = tsum(arate);
-    for (int i = lane; i < NQ; i += TEAM) L[Ly::QPOS + i] = F[Lo.qpos + i];
-    for (int i = lane; i < NV; i += TEAM) {
+    strided_for<NQ, TEAM>(lane, [&](int i) { L[Ly::QPOS + i] = F[Lo.qpos + i]; });
+    strided_for<NV, TEAM>(lane, [&](int i) {
       L[Ly::QVEL + i] = F[Lo.qvel + i] + (i == 0 ? push[0] * mag : (i == 1 ? push[1] * mag : 0.0f));
       L[Ly::WARM + i] = F[Lo.qacc_warmstart + i];
-    }
+    });
     load_dyn_team<Md, LAT>(A, e, L, lane);
     TSYNC();
   } else {
@@ -595,8 +606,8 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   };
   // termination (joystick.py:483-485)
   float nanp = 0.0f;
-  for (int i = l0; i < NQ; i += TS) nanp += isnan(L[Ly::QPOS + i]) ? 1.0f : 0.0f;
-  for (int i = l0; i < NV; i += TS) nanp += isnan(L[Ly::QVEL + i]) ? 1.0f : 0.0f;
+  strided_for<NQ, TS>(l0, [&](int i) { nanp += isnan(L[Ly::QPOS + i]) ? 1.0f : 0.0f; });
+  strided_for<NV, TS>(l0, [&](int i) { nanp += isnan(L[Ly::QVEL + i]) ? 1.0f : 0.0f; });
   const bool nan = red(nanp) > 0.0f;
   float done = (L[Ly::SENS + c.sens_upvector + 2] < 0.0f || nan) ? 1.0f : 0.0f;
   // rewards (joystick.py:622-669, common/rewards.py:11-125, custom_rewards.py:4-148)
@@ -694,11 +705,11 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
   F[Lo.push + 1] = push[1];
   int step = step_prev + 1;
   iset(Lo.push_step, push_step + 1);
-  for (int a = l0; a < NU; a += TS) {
+  strided_for<NU, TS>(l0, [&](int a) {
     F[Lo.last_last_last_act + a] = F[Lo.last_last_act + a];
     F[Lo.last_last_act + a] = F[Lo.last_act + a];
     F[Lo.last_act + a] = F[Lo.action_history + a];  // this step's action
-  }
+  });
   if (step > 500) {
     float nc[7];
     sample_command(c, r, SLOT_CMD, nc);
@@ -744,8 +755,8 @@ DK void step_env(const KArgs& A, int e, int lane, Slice<SW> L, const FA& F, cons
       for (int k = 0; k < Lo.priv_size; k++) A.priv[(size_t)e * Lo.priv_size + k] = G[Lo.first_priv + k];
     }
   } else {
-    for (int i = l0; i < NQ; i += TS) F[Lo.qpos + i] = L[Ly::QPOS + i];
-    for (int i = l0; i < NV; i += TS) { F[Lo.qvel + i] = L[Ly::QVEL + i]; F[Lo.qacc_warmstart + i] = L[Ly::WARM + i]; }
+    strided_for<NQ, TS>(l0, [&](int i) { F[Lo.qpos + i] = L[Ly::QPOS + i]; });
+    strided_for<NV, TS>(l0, [&](int i) { F[Lo.qvel + i] = L[Ly::QVEL + i]; F[Lo.qacc_warmstart + i] = L[Ly::WARM + i]; });
   }
   F[Lo.reward] = reward;
   F[Lo.done] = done;
