@@ -181,6 +181,22 @@ DK void cdot5v(const float* x, const float* y, const float* z, const float* u, c
       : "i"(C0), "i"(C1), "i"(C2), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(y[0]), "v"(y[1]), "v"(y[2]),
         "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(u[0]), "v"(u[1]), "v"(u[2]), "v"(w[0]), "v"(w[1]), "v"(w[2]));
 }
+// o_i - c . x_i for the five vectors x, y, z, u, w and per-lane offsets o: the first product fused
+// with its offset (v_fmamk_f32: literal -c_0, no separate subtraction)
+template <int C0, int C1, int C2>
+DK void cdot5v_noff(const float* x, const float* y, const float* z, const float* u, const float* w, const float* o,
+                    float* r) {
+  asm("v_fmamk_f32 %0, %8, %5, %23\n\tv_fmamk_f32 %1, %11, %5, %24\n\tv_fmamk_f32 %2, %14, %5, %25\n\t"
+      "v_fmamk_f32 %3, %17, %5, %26\n\tv_fmamk_f32 %4, %20, %5, %27\n\t"
+      "v_fmac_f32_e32 %0, %6, %9\n\tv_fmac_f32_e32 %1, %6, %12\n\tv_fmac_f32_e32 %2, %6, %15\n\t"
+      "v_fmac_f32_e32 %3, %6, %18\n\tv_fmac_f32_e32 %4, %6, %21\n\t"
+      "v_fmac_f32_e32 %0, %7, %10\n\tv_fmac_f32_e32 %1, %7, %13\n\tv_fmac_f32_e32 %2, %7, %16\n\t"
+      "v_fmac_f32_e32 %3, %7, %19\n\tv_fmac_f32_e32 %4, %7, %22"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4])
+      : "i"(C0 ^ (int)0x80000000), "i"(C1 ^ (int)0x80000000), "i"(C2 ^ (int)0x80000000), "v"(x[0]), "v"(x[1]),
+        "v"(x[2]), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(u[0]), "v"(u[1]), "v"(u[2]),
+        "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]));
+}
 // a . x and b . x for two compile-time vectors a = (A0, A1, A2), b = (B0, B1, B2), interleaved
 template <int A0, int A1, int A2, int B0, int B1, int B2>
 DK void cdot2c(const float* x, float& ra, float& rb) {
@@ -1639,6 +1655,11 @@ struct TPhys {
     cdot5v<DUCK_C3(Md::hull_vert[K])>(x, y, z, u, w, r);
   }
   template <int K>
+  static DK void hv_noff5(const float* x, const float* y, const float* z, const float* u, const float* w, const float* o,
+                          float* r) {  // o_i - v_K . x_i
+    cdot5v_noff<DUCK_C3(Md::hull_vert[K])>(x, y, z, u, w, o, r);
+  }
+  template <int K>
   static DK void hv_dot2(const float* x, float& ra, float& rb) {  // vertices K and K + 1
     cdot2c<DUCK_C3(Md::hull_vert[K]), DUCK_C3(Md::hull_vert[K + 1])>(x, ra, rb);
   }
@@ -1751,7 +1772,9 @@ struct TPhys {
         pf = fminf(pf, d[2] - hk[1] * nz);
         pf = fminf(pf, d[3] - hk[2] * nz);
         const float ov = nf_off_minus<f>(pf);
-        const bool b = (ov < mo) | ((ov == mo) & (5 + f < mp));
+        // (equal overlaps keep the lower priority, and mp < 5 + f here: the screen's axes are 0-4 and
+        // the faces run in priority order, so the tie test of `take` is always false)
+        const bool b = ov < mo;
         mo = b ? ov : mo;
         mp = b ? 5 + f : mp;
       });
@@ -1769,10 +1792,18 @@ struct TPhys {
 #endif
     {
       const lds_float* SL = L + ((foot >> 1) - tw) * TL::STRIDE + HF_CINQ + (foot & 1) * HF_SLSZ;
-      const int n = ((const lds_int*)SL)[0];
+      const lds_int* SLi = (const lds_int*)SL;
+      const lds_f4* SLw = (const lds_f4*)(SL + HF_SLF);
+      const int n = SLi[0];
+      // each entry's words loaded one iteration ahead (the loop waited for its own loads); the load
+      // past the list's last entry reads unused words of the slice
+      int e_nx = SLi[1];
+      f4v w_nx = SLw[0];
       for (int i = 0; i < n; i++) {
-        const int e = ((const lds_int*)SL)[1 + i];
-        const f4v w = ((const lds_f4*)(SL + HF_SLF))[i];
+        const int e = e_nx;
+        const f4v w = w_nx;
+        e_nx = SLi[2 + i];
+        w_nx = SLw[1 + i];
         const float wv[3] = {w.x, w.y, w.z};
         const float q0 = dot3(wv, Tm[0]), q1 = dot3(wv, Tm[1]), q2 = dot3(wv, Tm[2]);
         const int kk = q0 >= q1 ? (q0 >= q2 ? 0 : 2) : (q1 >= q2 ? 1 : 2);
@@ -1782,7 +1813,9 @@ struct TPhys {
     STAGE_MARK(44);
     // top-edge pairs (hull edge e, prism top edge k: faces ntm, sm_k). Pass 1: the arcs cross when
     // CBA DBA < 0, ADC BDC < 0 and CBA BDC > 0 (C = -n_a, D = -n_b, B x A = sm_k x ntm: CBA =
-    // -phi_a), all three products negative: the sign bit of their maximum, bit 3 e + k of pm
+    // -phi_a), all three products negative: the sign bit of their maximum, bit q = NE k + e of pm.
+    // The bits are shifted into 32-bit words in q order (one v_alignbit per pair; placing each bit
+    // at its position took a shift, a mask and an or) and bit-reversed into pm afterwards
     unsigned long long pm[3] = {0ull, 0ull, 0ull};
 #if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 12
     for (int rep_ = 0; rep_ < 2; rep_++)
@@ -1797,6 +1830,10 @@ struct TPhys {
       const auto& ntm = ntm_l;
       const auto& sm = sm_l;
 #endif
+      constexpr int NQW = (3 * NE + 31) / 32;
+      unsigned qw[NQW];
+#pragma unroll
+      for (int j = 0; j < NQW; j++) qw[j] = 0u;
       float hx[3][3];
       for (int k = 0; k < 3; k++) cross3(hx[k], sm[k], ntm);
       // (one prism edge at a time: 30 face products live, not 90)
@@ -1814,8 +1851,8 @@ struct TPhys {
         auto arc = [&](auto eI, float BDC) {
           constexpr int e = decltype(eI)::value, fa = Md::hull_edge_face[e][0], fb = Md::hull_edge_face[e][1];
           const float mx = fmaxf(fmaxf(phi[fa] * phi[fb], ADC[e] * BDC), phi[fa] * BDC);
-          constexpr int p = 3 * e + k;
-          pm[p >> 6] |= (unsigned long long)(__float_as_uint(mx) >> 31) << (p & 63);
+          constexpr int q = NE * k + e;
+          qw[q >> 5] = (qw[q >> 5] << 1) | (__float_as_uint(mx) >> 31);
         };
         static_for<0, NE / 2>([&](auto eI) {
           constexpr int e = 2 * eI.value;
@@ -1826,6 +1863,12 @@ struct TPhys {
         });
         if constexpr (NE % 2) arc(std::integral_constant<int, NE - 1>{}, dxc_dot<NE - 1>(sm[k]));
       });
+      // word j holds pairs 32 j .. 32 j + n - 1, the first in its top bit
+      static_for<0, NQW>([&](auto jI) {
+        constexpr int j = jI.value, n = 3 * NE - 32 * j < 32 ? 3 * NE - 32 * j : 32;
+        const unsigned r = __builtin_bitreverse32(qw[j]) >> (32 - n);
+        pm[j >> 1] |= (unsigned long long)r << (32 * (j & 1));
+      });
     }
     STAGE_MARK(45);
 #ifdef DUCK_STAGE_PROF
@@ -1834,16 +1877,14 @@ struct TPhys {
       STAGE_ADD(49, (unsigned long long)(__popcll(pm[0]) + __popcll(pm[1]) + __popcll(pm[2])));
       int uni = 0;
       for (int e = 0; e < NE; e++) {
-        const int p0 = 3 * e;
-        const unsigned long long b3 = ((p0 >> 6) == ((p0 + 2) >> 6))
-                                          ? (pm[p0 >> 6] >> (p0 & 63)) & 7ull
-                                          : ((pm[p0 >> 6] >> (p0 & 63)) | (pm[(p0 >> 6) + 1] << (64 - (p0 & 63)))) & 7ull;
+        unsigned long long b3 = 0ull;
+        for (int k = 0; k < 3; k++) b3 |= (pm[(NE * k + e) >> 6] >> ((NE * k + e) & 63)) & 1ull;
         uni += __ballot(b3 != 0ull) != 0ull;
       }
       if ((int)threadIdx.x == __ffsll((long long)__ballot(1)) - 1) STAGE_ADD(50, (unsigned long long)uni);
     }
 #endif
-    // pass 2: each crossing pair's overlap along ev x em (lowest pair first)
+    // pass 2: each crossing pair's overlap along ev x em
 #if defined(DUCK_DOUBLE) && DUCK_DOUBLE == 11
     const unsigned long long pm_s[3] = {pm[0], pm[1], pm[2]};
     for (int rep_ = 0; rep_ < 2; rep_++) {
@@ -1855,12 +1896,13 @@ struct TPhys {
 #endif
       const bool z0 = pm[0] == 0ull, z1 = pm[1] == 0ull;
       const unsigned long long w = z0 ? (z1 ? pm[2] : pm[1]) : pm[0];
-      const int p = (z0 ? (z1 ? 128 : 64) : 0) + __builtin_ctzll(w);
+      const int q = (z0 ? (z1 ? 128 : 64) : 0) + __builtin_ctzll(w);
       const unsigned long long wc = w & (w - 1ull);
       pm[0] = z0 ? pm[0] : wc;
       pm[1] = z0 && !z1 ? wc : pm[1];
       pm[2] = z0 && z1 ? wc : pm[2];
-      const int e = p / 3, k = p - 3 * e, o = Md::B_HEDGE + 20 * e;
+      // (the pairs run in q order; the minimum over (overlap, priority p) does not depend on it)
+      const int k = q >= 2 * NE ? 2 : (q >= NE ? 1 : 0), e = q - NE * k, p = 3 * e + k, o = Md::B_HEDGE + 20 * e;
       const f4v ev4 = ht4(o + 12), v04 = ht4(o + 16);
       const float ev[3] = {ev4.x, ev4.y, ev4.z}, v0[3] = {v04.x, v04.y, v04.z};
       float em[3], tm[3], sk[3];
@@ -1913,16 +1955,17 @@ struct TPhys {
 #endif
     const float ptop = dot3(ntm, Tm[0]);
     const float smt[3] = {dot3(sm[0], Tm[0]), dot3(sm[1], Tm[1]), dot3(sm[2], Tm[2])};
+    const float offs[5] = {ptop, base, smt[0], smt[1], smt[2]};
     float W = 0.0f, Cx[3] = {0.0f, 0.0f, 0.0f};
     // (every vertex, without a wave-uniform skip of those above every lane's prism top: the 17
     // branches cost more than the distances they skipped, C4 -0.8 %; the weights are the same)
     static_for<0, NH>([&](auto kI) {
       constexpr int k = kI.value;
+      // (the distances below the top, above the base and inside the sides, each as o - v_k . x)
       float d[5];
-      hv_dot5<k>(ntm, zc, sm[0], sm[1], sm[2], d);
-      const float atop = ptop - d[0];
-      float pen = fminf(atop, d[1] - base);
-      for (int j = 0; j < 3; j++) pen = fminf(pen, smt[j] - d[2 + j]);
+      hv_noff5<k>(ntm, zc, sm[0], sm[1], sm[2], offs, d);
+      float pen = fminf(d[0], -d[1]);
+      for (int j = 0; j < 3; j++) pen = fminf(pen, d[2 + j]);
       const float w = fmaxf(pen, 0.0f);
       W += w;
       Cx[0] = cfma<fbits(Md::hull_vert[k][0])>(w, Cx[0]);
