@@ -68,6 +68,21 @@ template <int CTRL>
 DK int dppi(int v) {
   return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
+// min / max without the v_max_f32 x, x, x (canonicalize) that the compiler puts in front of fminf /
+// fmaxf for each operand it cannot prove canonical -- a DPP read, an output of a multi-result asm
+// statement: v_med3 with an infinite third operand (one instruction; a DPP read stays a separate
+// v_mov_b32_dpp, VOP3 has no DPP form here). Same results for every non-NaN operand
+// (the infinity opaque: with a constant one the compiler rewrites v_med3 as fminf / fmaxf again)
+DK float fmin_nc(float a, float b) {
+  float ninf = -__builtin_inff();
+  asm("" : "+s"(ninf));
+  return __builtin_amdgcn_fmed3f(a, b, ninf);
+}
+DK float fmax_nc(float a, float b) {
+  float inf = __builtin_inff();
+  asm("" : "+s"(inf));
+  return __builtin_amdgcn_fmed3f(a, b, inf);
+}
 // reductions over the 16 lanes of a DPP row (= one team); every lane gets the result
 DK float tsum(float v) {
   v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]
@@ -111,6 +126,14 @@ DK float hmax8(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));
   v = fmaxf(v, dppf<0x141>(v));
+  return v;
+}
+// the same with fmax_nc (the height field's reductions: C4 / C5 +0.4-0.6 %; in the flat scenes'
+// plane contacts the med3 form measured 0.4 % slower, C2)
+DK float hmax8_nc(float v) {
+  v = fmax_nc(v, dppf<0xB1>(v));
+  v = fmax_nc(v, dppf<0x4E>(v));
+  v = fmax_nc(v, dppf<0x141>(v));
   return v;
 }
 DK int hmin8i(int v) {
@@ -1620,7 +1643,7 @@ struct TPhys {
   // bottom-edge pairs are not tested (the oracle tests them; they are never the minimum while the
   // hull is above the prism's base, 0.1 m under the field: tests/test_oracle_physics.py).
   // Coordinates: "local" = the field's axes with the origin at the hull frame, "mesh" = the hull frame.
-  static DK float hmin8f(float v) { return -hmax8(-v); }
+  static DK float hmin8f(float v) { return -hmax8_nc(-v); }
   // this lane's rank within its 8-lane half of the wave's ballot word
   static DK unsigned half_bits(unsigned long long b, int lane) {
     const int base = ((int)threadIdx.x & 63) & ~7;
@@ -1767,7 +1790,7 @@ struct TPhys {
         constexpr int f = fI.value;
         float d[4];
         nf_dot4<f>(zc, Tm[0], Tm[1], Tm[2], d);
-        const float nz = fmaxf(d[0], 0.0f);
+        const float nz = fmax_nc(d[0], 0.0f);
         float pf = d[1] - hk[0] * nz;
         pf = fminf(pf, d[2] - hk[1] * nz);
         pf = fminf(pf, d[3] - hk[2] * nz);
@@ -2083,7 +2106,7 @@ struct TPhys {
         for (int a = 0; a < 3; a++) { lo[a] = fminf(lo[a], xl[i][a]); hi[a] = fmaxf(hi[a], xl[i][a]); }
       }
     }
-    for (int a = 0; a < 3; a++) { lo[a] = hmin8f(lo[a]); hi[a] = hmax8(hi[a]); }
+    for (int a = 0; a < 3; a++) { lo[a] = hmin8f(lo[a]); hi[a] = hmax8_nc(hi[a]); }
     // the field's box and the sub-grid (vertex columns cmin..cmax, rows rmin..rmax); grid
     // coordinates relative to the field's centre (vertex c at (c - (ncol - 1) / 2) dx): the robot
     // walks near the centre, where these keep fp32's resolution (x + size would round to ~1e-6 m)
@@ -2235,7 +2258,7 @@ struct TPhys {
       static_for<0, NH / 2>([&](auto kI) {
         float ha, hb;
         hv_dot2<2 * kI.value>(ntm, ha, hb);
-        hm = fminf(hm, fminf(ha, hb));
+        hm = fmin_nc(hm, fmin_nc(ha, hb));
       });
       if constexpr (NH % 2) hm = fminf(hm, hv_dot<NH - 1>(ntm));
       // priority order (equal overlaps: the first): top 0, sides 1-3, bottom 4, hull faces 5 + f
@@ -2375,7 +2398,7 @@ struct TPhys {
     float dmax = -1e30f;
 #pragma unroll
     for (int s = 0; s < PPL; s++) dmax = fmaxf(dmax, cd[s] > 0.0f ? cd[s] : -1e30f);
-    dmax = hmax8(dmax);
+    dmax = hmax8_nc(dmax);
     const bool any = dmax > 0.0f;
     int a_ = 1 << 20;
 #pragma unroll
@@ -2402,7 +2425,7 @@ struct TPhys {
       float mx = -1e30f;
 #pragma unroll
       for (int s = 0; s < PPL; s++) mx = fmaxf(mx, v[s]);
-      mx = hmax8(mx);
+      mx = hmax8_nc(mx);
       int best = 1 << 20;
 #pragma unroll
       for (int s = PPL - 1; s >= 0; s--)
@@ -2451,7 +2474,7 @@ struct TPhys {
         s2[s] = cd[s] > 0.0f ? fabsf(dot3(ap, ac)) : -1e30f;
         mx = fmaxf(mx, fmaxf(s1[s], s2[s]));
       }
-      mx = hmax8(mx);
+      mx = hmax8_nc(mx);
       int best = 1 << 20;
 #pragma unroll
       for (int s = PPL - 1; s >= 0; s--) {
