@@ -1978,17 +1978,19 @@ struct TPhys {
 #endif
     const float ptop = dot3(ntm, Tm[0]);
     const float smt[3] = {dot3(sm[0], Tm[0]), dot3(sm[1], Tm[1]), dot3(sm[2], Tm[2])};
-    const float offs[5] = {ptop, base, smt[0], smt[1], smt[2]};
     float W = 0.0f, Cx[3] = {0.0f, 0.0f, 0.0f};
     // (every vertex, without a wave-uniform skip of those above every lane's prism top: the 17
     // branches cost more than the distances they skipped, C4 -0.8 %; the weights are the same)
     static_for<0, NH>([&](auto kI) {
       constexpr int k = kI.value;
-      // (the distances below the top, above the base and inside the sides, each as o - v_k . x)
+      // (o - v_k . x with the offset fused into the first product, v_fmamk_f32, measured C4 +0.7 % and
+      // C5 +0.9 %, but moved the teacher-forced outliers: rough + DR seeds 7 / 11 / 13 / 17 10 / 24 /
+      // 16 / 12 of 10,240 with one unexplained, against 13 / 20 / 14 / 13 all explained -- not kept)
       float d[5];
-      hv_noff5<k>(ntm, zc, sm[0], sm[1], sm[2], offs, d);
-      float pen = fminf(d[0], -d[1]);
-      for (int j = 0; j < 3; j++) pen = fminf(pen, d[2 + j]);
+      hv_dot5<k>(ntm, zc, sm[0], sm[1], sm[2], d);
+      const float atop = ptop - d[0];
+      float pen = fminf(atop, d[1] - base);
+      for (int j = 0; j < 3; j++) pen = fminf(pen, smt[j] - d[2 + j]);
       const float w = fmaxf(pen, 0.0f);
       W += w;
       Cx[0] = cfma<fbits(Md::hull_vert[k][0])>(w, Cx[0]);
