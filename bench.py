@@ -24,18 +24,56 @@ Extra JSON objects:
                   bounded sample (rank 0, N=1 only), plus BASELINE configs[0] (C1): 1 env, 1 core.
 
 --strong keeps 4096 envs in total over the N ranks (strong scaling) instead of 4096 per rank.
+
+Launch: `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py <same args>` as a child process
+(before anything touches the GPU) and exits with its code; rank 0's JSON line reaches stdout
+unchanged. Under an external torch.distributed.run (WORLD_SIZE set) it runs as that rank.
 """
 
 from __future__ import annotations
 
-import argparse
-import glob
-import json
 import os
 import sys
-import time
 
-import numpy as np
+
+def _self_launch(argv) -> int:
+    """Start one rank per GPU through torch.distributed.run as a child process (common/runner.py:104-118
+    runs one pmap replica per local device; here one process per GPU). Nothing here initialises HIP:
+    the parent only parses --gpus and waits, so there is no exec after a GPU context exists."""
+    import socket
+    import subprocess
+    n = None
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            n = int(argv[i + 1])
+        elif a.startswith("--gpus="):
+            n = int(a.split("=", 1)[1])
+    if n is None or n <= 1:
+        return -1
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on these hosts (RCCL)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=env).returncode
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ:
+    _rc = _self_launch(sys.argv[1:])
+    if _rc >= 0:
+        sys.exit(_rc)
+
+import argparse  # noqa: E402
+import glob  # noqa: E402
+import json  # noqa: E402
+import time  # noqa: E402
+
+import numpy as np  # noqa: E402
 import torch
 import torch.distributed as dist
 
@@ -175,14 +213,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: one rank per GPU "
+                         "(run `bench.py --gpus N` directly, or under torch.distributed.run --nproc-per-node N)")
     ndev = torch.cuda.device_count()
+    backend = os.environ.get("DUCK_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only to rehearse on one GPU
+    if world > 1 and backend == "nccl" and world > ndev:
+        raise SystemExit(f"--gpus {world} but only {ndev} visible GPU(s): RCCL runs one rank per device "
+                         "(DUCK_DIST_BACKEND=gloo rehearses several ranks on one GPU)")
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("DUCK_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only to rehearse on one GPU
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:

@@ -82,7 +82,9 @@ int duck_reset(duck_sim* sim, int n_envs, float* fstate, int32_t* istate, const 
  * LATENCY while n_envs <= 4 x the device's CU count, PAIRED while n_envs <= 8 x, else THROUGHPUT.
  * Every mode gives the same results bit for bit (every scene; tests/test_gpu_env.py), so a run's
  * trajectories do not depend on the batch size or the GPU count that picked the kernel; bench.py
- * and the PPO runner still record which kernel ran. */
+ * and the PPO runner still record which kernel ran. A model whose LDS budget does not fit a
+ * latency split (model blob + hot state in LDS next to the env slices) is compiled without it:
+ * duck_set_step_mode refuses that mode with DUCK_EUNSUPPORTED and AUTO skips it. */
 enum { DUCK_STEP_AUTO = 0, DUCK_STEP_THROUGHPUT = 1, DUCK_STEP_LATENCY = 2, DUCK_STEP_PAIRED = 3 };
 int duck_set_step_mode(duck_sim* sim, int mode);
 /* the kernel duck_step would launch for n_envs envs: DUCK_STEP_THROUGHPUT, _LATENCY or _PAIRED */

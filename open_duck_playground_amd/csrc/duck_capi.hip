@@ -145,9 +145,8 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
   if (cfg->use_imitation && !ref) return duck_fail(DUCK_EINVAL, "use_imitation requires a reference-motion table");
   if (cfg->n_substeps < 1 || cfg->action_max_delay < 1 || cfg->action_max_delay > 3)
     return duck_fail(DUCK_EINVAL, "bad config (n_substeps >= 1, 1 <= action_max_delay <= 3)");
-  if (kVariants[v]->lds_bytes() > 160 * 1024 || kVariants[v]->lds_bytes_lat() > 160 * 1024 ||
-      kVariants[v]->lds_bytes_lat2() > 160 * 1024)
-    return duck_fail(DUCK_EUNSUPPORTED, "per-workgroup LDS over 160 KiB");
+  // the throughput kernel must fit; a latency split that does not is simply not compiled (lds 0)
+  if (kVariants[v]->lds_bytes() > 160 * 1024) return duck_fail(DUCK_EUNSUPPORTED, "per-workgroup LDS over 160 KiB");
   // the elevation is uploaded here, not baked (the fingerprint covers nrow / ncol / size only)
   if (kVariants[v]->floor_type == 1 && (!model->hfield_data || model->hfield_nrow < 2 || model->hfield_ncol < 2))
     return duck_fail(DUCK_EINVAL, "height-field model without hfield_data [nrow >= 2][ncol >= 2]");
@@ -157,6 +156,8 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
   s->device = device;
   s->variant = v;
   s->step_mode = DUCK_STEP_AUTO;
+  s->lat_ok = kVariants[v]->lds_bytes_lat() != 0;
+  s->lat2_ok = kVariants[v]->lds_bytes_lat2() != 0;
   {
     hipError_t e = hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) {
@@ -185,7 +186,7 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
   if (ref) {
     if (ref->n_dim != 40 || ref->n_dx > 16 || ref->n_dy > 16 || ref->n_dtheta > 16 || ref->nb_steps_in_period < 1 ||
         !ref->frames) {
-      delete s;
+      duck_destroy(s);  // frees the pinned error word allocated above
       return duck_fail(DUCK_EINVAL, "reference-motion table must be [<=16][<=16][<=16][nb][40] frames");
     }
     s->ref.n_dx = ref->n_dx; s->ref.n_dy = ref->n_dy; s->ref.n_dtheta = ref->n_dtheta;
@@ -263,6 +264,8 @@ int duck_physics_step(duck_sim* s, int n, float* qpos, float* qvel, float* warm,
 int duck_set_step_mode(duck_sim* s, int mode) {
   g_err.clear();
   if (!s || mode < DUCK_STEP_AUTO || mode > DUCK_STEP_PAIRED) return duck_fail(DUCK_EINVAL, "bad argument");
+  if ((mode == DUCK_STEP_LATENCY && !s->lat_ok) || (mode == DUCK_STEP_PAIRED && !s->lat2_ok))
+    return duck_fail(DUCK_EUNSUPPORTED, "this model's LDS budget does not fit that step kernel (AUTO skips it)");
   s->step_mode = mode;
   return DUCK_OK;
 }

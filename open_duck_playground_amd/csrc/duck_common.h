@@ -41,6 +41,7 @@ struct duck_sim {
   int nq, nv, nu;
   int step_mode;  // DUCK_STEP_*
   int n_cu;       // compute units of the device (DUCK_STEP_AUTO)
+  int lat_ok, lat2_ok;  // the latency / paired latency kernels are compiled for this model (TLay::FITS)
   volatile unsigned* err_h;  // sticky device error word (DUCK_DEVERR_*), host-mapped pinned memory
   unsigned* err_d;           // its device mapping (KArgs::err)
 };
@@ -67,10 +68,11 @@ struct VariantOps {
 
 // the step kernel duck_step launches for n envs (DUCK_STEP_THROUGHPUT / _LATENCY / _PAIRED): the mode
 // asked for, or under AUTO the latency kernel while n <= 4 envs per CU, the paired latency kernel
-// while n <= 8 per CU, else the throughput kernel
+// while n <= 8 per CU, else the throughput kernel; a split a model does not fit (lat_ok / lat2_ok) is
+// skipped: the paired kernel then covers <= 8 per CU, or the throughput kernel everything
 inline int step_kernel_choice(const duck_sim* s, int n) {
   if (s->step_mode != DUCK_STEP_AUTO) return s->step_mode;
-  if (n <= LAT_WG_HOST * s->n_cu) return DUCK_STEP_LATENCY;
-  if (n <= 2 * LAT_WG_HOST * s->n_cu) return DUCK_STEP_PAIRED;
+  if (s->lat_ok && n <= LAT_WG_HOST * s->n_cu) return DUCK_STEP_LATENCY;
+  if (s->lat2_ok && n <= 2 * LAT_WG_HOST * s->n_cu) return DUCK_STEP_PAIRED;
   return DUCK_STEP_THROUGHPUT;
 }

@@ -1069,13 +1069,14 @@ static size_t lds_bytes() {
   static_assert(WG == TEAM_WG, "team workgroup size");
   return (size_t)TLay<Md>::LDS_FLOATS * sizeof(float);
 }
+// 0 = the split does not fit this model's LDS and is not compiled (TLay::FITS)
 template <class Md>
 static size_t lds_bytes_lat() {
-  return (size_t)TLay<Md, 1>::LDS_FLOATS * sizeof(float);
+  return TLay<Md, 1>::FITS ? (size_t)TLay<Md, 1>::LDS_FLOATS * sizeof(float) : 0;
 }
 template <class Md>
 static size_t lds_bytes_lat2() {
-  return (size_t)TLay<Md, 2>::LDS_FLOATS * sizeof(float);
+  return TLay<Md, 2>::FITS ? (size_t)TLay<Md, 2>::LDS_FLOATS * sizeof(float) : 0;
 }
 
 template <class Md>
@@ -1124,10 +1125,17 @@ static int launch_step(duck_sim* s, int n, float* fs, int32_t* is, const float* 
   if (k == DUCK_STEP_LATENCY || k == DUCK_STEP_PAIRED) {
     const int wgl = k == DUCK_STEP_PAIRED ? 2 * LAT_WG : LAT_WG;
     const dim3 grid((A.n + wgl - 1) / wgl), block(TPB);
-    if (k == DUCK_STEP_PAIRED)
-      hipLaunchKernelGGL((step_kernel_lat<Md, 2>), grid, block, lds_bytes_lat2<Md>(), st, A);
-    else
-      hipLaunchKernelGGL((step_kernel_lat<Md, 1>), grid, block, lds_bytes_lat<Md>(), st, A);
+    if (k == DUCK_STEP_PAIRED) {
+      if constexpr (TLay<Md, 2>::FITS)
+        hipLaunchKernelGGL((step_kernel_lat<Md, 2>), grid, block, lds_bytes_lat2<Md>(), st, A);
+      else
+        return duck_fail(DUCK_EUNSUPPORTED, "the paired latency kernel does not fit this model in LDS");
+    } else {
+      if constexpr (TLay<Md, 1>::FITS)
+        hipLaunchKernelGGL((step_kernel_lat<Md, 1>), grid, block, lds_bytes_lat<Md>(), st, A);
+      else
+        return duck_fail(DUCK_EUNSUPPORTED, "the latency kernel does not fit this model in LDS");
+    }
     HIPCHECK(hipGetLastError());
     return DUCK_OK;
   }

@@ -339,7 +339,12 @@ struct TLay {
   static constexpr bool ES_LDS = (size_t)(ES + ES_FLOATS) <= LDS_MAX;
   static constexpr int EV = ES + (ES_LDS ? ES_FLOATS : 0);
   static constexpr int LDS_FLOATS = EV + 4 * NEV;
-  static_assert((size_t)LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
+  // whether this work split can run the model at all: the throughput kernel needs its env slices in
+  // LDS; the latency kernels also need the model blob and the hot state there (step_kernel_lat). A
+  // model that fits the throughput kernel but not a latency split compiles without that split
+  // (duck_env_kernels.h launch_step; AUTO then falls back, duck_set_step_mode refuses it)
+  static constexpr bool FITS = (size_t)LDS_FLOATS * 4 <= 160 * 1024 && (LAT == 0 || (TAB_LDS && ES_LDS));
+  static_assert(LAT || FITS, "LDS budget");
   static_assert(6 * Md::NV <= 4 * Ly::NROW, "crb scratch must fit in the row storage");
   static_assert(LAT || 18 * Md::NB <= Ly::HSZ + 4 * Ly::NROW, "rne scratch must fit in H + rows");
   static_assert(LAT || Md::FLOOR_TYPE != 1 || XSIL + 2 * HF_SLSZ <= Ly::CIN + 10 * Md::NB,

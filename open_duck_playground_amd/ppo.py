@@ -757,6 +757,17 @@ def _torch_unroll(env, net: ActorCritic, cfg: PPOConfig, data: Dict[str, torch.T
             data["next_priv"][t, cols] = state.obs[cfg.value_obs_key]
 
 
+def check_device_error(env, what: str) -> None:
+    """Raise DuckError when a launch on ``env``'s handle set its sticky device error word
+    (duck_device_error: e.g. a latency-kernel cross-wave wait that timed out and left NaN qpos in its
+    workgroup's envs). Call after a synchronise: the word is written by the kernel itself."""
+    err = env.device_error() if hasattr(env, "device_error") else 0
+    if err:
+        from .native import DuckError
+        raise DuckError(f"device error word 0x{err:x} set during the {what} (duck_device_error): the "
+                        "transitions of this batch are not valid")
+
+
 @dataclass
 class TrainResult:
     net: ActorCritic
@@ -841,6 +852,9 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
         else:
             _torch_unroll(env, net, cfg, data, state, unrolls_per_update, gen)
         _sync()
+        # a replayed graph never re-enters duck_step, whose entry check would raise: read the
+        # handle's sticky device error word here, before the batch reaches the learner
+        check_device_error(env, "rollout")
         t_learn = time.time()
         result.timing["rollout_s"] += t_learn - t_roll
         if cfg.normalize_observations:  # brax updates the normaliser with the fresh batch first
@@ -891,6 +905,9 @@ def evaluate(net: ActorCritic, eval_env, cfg: PPOConfig, rng: int) -> Dict[str, 
         ret += state.reward * active
         length += active
         active = active * (1.0 - state.done)
+    if eval_env.device.type == "cuda":
+        torch.cuda.synchronize(eval_env.device)
+    check_device_error(eval_env, "evaluation")   # the last launch is not followed by another duck_step
     return {"eval/episode_reward": float(ret.mean()), "eval/episode_reward_std": float(ret.std(unbiased=False)),
             "eval/avg_episode_length": float(length.mean())}
 

@@ -266,3 +266,30 @@ def test_round4_entry_points_refuse_bad_arguments():
     assert lib.duck_gather_columns(1, f, C.c_void_p(1), 4, None) < 0 and b"bad field" in lib.duck_last_error()
     assert lib.duck_set_step_mode(None, 0) < 0
     assert lib.duck_step_kernel_for(None, 4) < 0
+
+
+def test_bench_self_launch_command(monkeypatch):
+    """bench.py --gpus N (N > 1, no WORLD_SIZE) starts torch.distributed.run as a child with the same
+    arguments and returns its exit code; --gpus 1 runs in-process (VERDICT r05 #1). No GPU call here."""
+    import subprocess
+    import sys
+    import types
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    seen = {}
+
+    def fake_run(cmd, env=None, **kw):
+        seen["cmd"], seen["env"] = cmd, env
+        return types.SimpleNamespace(returncode=7)
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    assert bench._self_launch(["--gpus", "1", "--steps", "3"]) == -1 and not seen
+    assert bench._self_launch(["--gpus", "4", "--steps", "3", "--strong"]) == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3", "--strong"][-4:] and cmd[-5] == "--gpus"
+    assert os.path.basename(cmd[-6]) == "bench.py"
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert bench._self_launch(["--gpus=2"]) == 7 and "--nproc-per-node=2" in seen["cmd"]

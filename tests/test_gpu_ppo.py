@@ -49,6 +49,24 @@ def test_runner_cli_one_update(gpu, tmp_path, monkeypatch):
                  "--restore_checkpoint_path", str(tmp_path / "ck" / cks[-1])])
 
 
+def test_train_surfaces_latency_timeout(gpu, monkeypatch):
+    """The graph-captured rollout with the force_timeout test build (its latency-kernel waits in
+    workgroup 1 give up, which sets the device error word and NaN-s that workgroup's qpos): train()
+    raises DuckError instead of learning from the corrupted transitions."""
+    from open_duck_playground_amd import joystick as jmod
+    from open_duck_playground_amd.native import BUILD, DuckError
+    path = os.path.join(BUILD, "libduck_force_timeout.so")
+    assert os.path.exists(path), "built by __graft_entry__.build()"
+    monkeypatch.setattr(jmod, "model_library", lambda m: path)
+    n = 64
+    env = wrap_for_brax_training(Joystick("flat_terrain", num_envs=n, device=gpu), episode_length=1000)
+    env.set_step_mode("latency")
+    cfg = ppo.PPOConfig(num_envs=n, batch_size=2, num_minibatches=32, num_evals=0)
+    with pytest.raises(DuckError, match="device error word"):
+        ppo.train(env, cfg, max_updates=3, use_graph=True)
+    assert env.device_error(clear=True) == 1
+
+
 def test_graph_learner_matches_eager(gpu):
     """The HIP-graph learner replays the same update sequence as the eager one.
 

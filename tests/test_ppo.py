@@ -169,6 +169,36 @@ def test_ppo_learns_toy_env():
     assert ev["eval/episode_reward"] > 0.75 * cfg.episode_length
 
 
+class FaultyToyEnv(ToyEnv):
+    """ToyEnv whose handle reports a sticky device error word after ``fail_after`` steps, the way
+    libduck's duck_device_error does after a latency-kernel wait timed out. Its step never raises
+    itself, as a replayed HIP graph never re-enters duck_step's entry check."""
+
+    def __init__(self, fail_after, **kw):
+        super().__init__(**kw)
+        self.fail_after, self.steps = fail_after, 0
+
+    def step(self, state, action, inplace=True):
+        self.steps += 1
+        return super().step(state, action, inplace)
+
+    def device_error(self, clear=False):
+        return 1 if self.steps > self.fail_after else 0
+
+
+def test_train_raises_on_device_error_word():
+    """training must not run on after a launch set the device error word (NaN qpos in a
+    workgroup's envs): train() reads it after every rollout and raises DuckError."""
+    from open_duck_playground_amd.native import DuckError
+    env = FaultyToyEnv(fail_after=8 * 3 + 2)   # clean for 3 unrolls of 8 steps, faults in the 4th
+    res = []
+    with pytest.raises(DuckError, match="device error word 0x1 set during the rollout"):
+        ppo.train(env, small_cfg(), max_updates=6, progress_fn=lambda s, m: res.append(s))
+    assert res == [512, 1024, 1536]     # the three clean updates completed, the faulty batch did not
+    with pytest.raises(DuckError, match="during the evaluation"):
+        ppo.evaluate(ppo.ActorCritic(3, 4, 3, small_cfg()), FaultyToyEnv(fail_after=3, num_envs=8), small_cfg(), rng=0)
+
+
 def test_batch_size_contract():
     env = ToyEnv(num_envs=48)
     with pytest.raises(ValueError):
