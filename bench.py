@@ -15,10 +15,12 @@ synchronize and the max over ranks is reported.
 Extra JSON objects:
   roofline        the step kernel against HBM: algorithmic bytes per env-step
                   x envs per launch / average launch time from HIP events on the launch stream.
-  issue_roofline  the same kernel against the chip's FP32 VALU issue rate (78.6 T lane-instr/s; its
-                  real bound: one wave per SIMD on a dependent chain, which can issue at most half
-                  of that -- one_wave_ceiling), from the SQ counters of the committed rocprofv3 run
-                  of this library (profiles/, checked against the library's build id).
+  issue_roofline  the same kernel against the chip's FP32 VALU issue rate (78.6 T lane-instr/s, a
+                  wave64 v_fma_f32 every 2 cycles per SIMD), from the SQ counters of the committed
+                  rocprofv3 run of this library (profiles/, checked against the library's build id),
+                  with the rates measured on MI355X beside it (profiles/r06_valu_occupancy_probe.txt):
+                  55.7 T at 8 waves per SIMD (measured_peak) and 29.1 T for one wave per SIMD, this
+                  kernel's occupancy (one_wave_ceiling).
   cpu_baseline    the fp64 C oracle (oracle/, a restatement of the same step) over OpenMP on the
                   host cores this job may use (affinity, capped by the cgroup CPU quota), on a
                   bounded sample (rank 0, N=1 only), plus BASELINE configs[0] (C1): 1 env, 1 core.
@@ -60,7 +62,19 @@ def _self_launch(argv) -> int:
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on these hosts (RCCL)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
-    return subprocess.run(cmd, env=env).returncode
+    # the ranks' stdout is relayed line by line: the bench line to stdout, anything else the launcher or a
+    # communication library writes there (gloo announces its peers) to stderr, so stdout holds one line
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        k = line.find('{"metric"')
+        if k > 0:
+            sys.stderr.write(line[:k] + "\n")
+        if k >= 0:
+            sys.stdout.write(line[k:])
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return p.wait()
 
 
 if __name__ == "__main__" and "WORLD_SIZE" not in os.environ:
@@ -85,11 +99,14 @@ from open_duck_playground_amd.sharding import shard_from_env  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # FP32 VALU issue peak of the chip: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz = 78.6 T lane-instructions/s
-# (MI355X_MICROARCH.md, v_fma_f32 wave64: 2 cycles on the 32-wide SIMD) = the 157.3 TFLOPS vector spec / 2 (FMA)
+# (a wave64 v_fma_f32 every 2 cycles on the 32-lane SIMD = the 157.3 TFLOPS vector spec / 2 for the FMA).
+# Measured (profiles/r06_valu_occupancy_probe.txt, tools/valu_occupancy_probe.hip: independent v_fma_f32
+# streams, wall clock of the whole launch): one wave per SIMD issues every 4.9 cycles (29.1 T for the
+# chip), two waves 47.6 T, eight 55.7 T -- so the SIMD does issue faster than one wave alone can, and a
+# kernel that registers hold at one wave per SIMD (this one) is capped near the one-wave rate
 VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12
-# what one wave alone on a SIMD can issue (same row: 4 cycles per wave64 instruction), i.e. the ceiling of a
-# kernel that registers hold at one wave per SIMD: half the chip's rate
-VALU_ONE_WAVE_TLANE = VALU_PEAK_TLANE / 2
+VALU_MEASURED_PEAK_TLANE = 55.74     # 8 waves per SIMD
+VALU_ONE_WAVE_TLANE = 29.12          # 1 wave per SIMD
 # newest tools/gpu_pmc.sh <rNN> C2 summary; only used when its build id matches the loaded library
 PMC_PROFILE = (sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_c2.json")))
                or [os.path.join(ROOT, "profiles", "r02_pmc_c2.json")])[-1]
@@ -204,9 +221,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline sampling (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this job may use")
     ap.add_argument("--strong", action="store_true", help="4096 envs in total over the ranks (strong scaling)")
-    ap.add_argument("--step-mode", default="auto", choices=["auto", "throughput", "latency", "paired"],
-                    help="duck_set_step_mode: auto = the latency kernel at <= 4 envs per CU, the paired latency "
-                         "kernel at <= 8 (strong scaling)")
+    ap.add_argument("--step-mode", default="auto", choices=["auto", "throughput", "latency", "paired", "latency_x2"],
+                    help="duck_set_step_mode: auto = the latency kernel at <= 4 envs per CU, at <= 8 the latency "
+                         "kernel at two workgroups per CU (flat scenes) or the paired latency kernel (strong scaling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -299,7 +316,9 @@ def main():
             traffic = prof["hbm_bytes_per_launch"]
             valu = prof["SQ_INSTS_VALU"] * 64 / (kern_ms * 1e-3) / 1e12     # lane-instructions / s
             issue_rf = {"bound": "valu", "achieved": valu, "peak": VALU_PEAK_TLANE, "unit": "T lane-instr/s",
-                        "frac": valu / VALU_PEAK_TLANE, "one_wave_ceiling": VALU_ONE_WAVE_TLANE,
+                        "frac": valu / VALU_PEAK_TLANE, "measured_peak": VALU_MEASURED_PEAK_TLANE,
+                        "frac_of_measured_peak": valu / VALU_MEASURED_PEAK_TLANE,
+                        "one_wave_ceiling": VALU_ONE_WAVE_TLANE,
                         "frac_of_one_wave_ceiling": valu / VALU_ONE_WAVE_TLANE,
                         "valu_insts_per_launch": prof["SQ_INSTS_VALU"],
                         "valu_busy_frac": prof["valu_busy_frac"], "waitcnt_frac": prof["waitcnt_frac"], **src}
@@ -329,7 +348,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": {"throughput": "step_kernel", "latency": "step_kernel_lat<1>",
-                                    "paired": "step_kernel_lat<2>"}[env.step_kernel],
+                                    "paired": "step_kernel_lat<2>", "latency_x2": "step_kernel_lat_x2"}[env.step_kernel],
                          "kernel_ms": kern_ms, "bytes_per_env_step": B},
             "issue_roofline": issue_rf,
             "cpu_baseline": cpu,

@@ -79,15 +79,21 @@ int duck_reset(duck_sim* sim, int n_envs, float* fstate, int32_t* istate, const 
  * split over its 4 waves (the shortest env-step: strong scaling over GPUs, <= 4 envs per CU);
  * PAIRED runs 8 envs per workgroup, each set of 4 on a pair of waves that split the stages
  * (the shortest env-step at 4-8 envs per CU: 4,096 envs over 2 GPUs). AUTO (the default) picks
- * LATENCY while n_envs <= 4 x the device's CU count, PAIRED while n_envs <= 8 x, else THROUGHPUT.
+ * LATENCY while n_envs <= 4 x the device's CU count, LATENCY_X2 (where compiled, below) or else PAIRED
+ * while n_envs <= 8 x, else THROUGHPUT.
  * Every mode gives the same results bit for bit (every scene; tests/test_gpu_env.py), so a run's
  * trajectories do not depend on the batch size or the GPU count that picked the kernel; bench.py
  * and the PPO runner still record which kernel ran. A model whose LDS budget does not fit a
  * latency split (model blob + hot state in LDS next to the env slices) is compiled without it:
- * duck_set_step_mode refuses that mode with DUCK_EUNSUPPORTED and AUTO skips it. */
-enum { DUCK_STEP_AUTO = 0, DUCK_STEP_THROUGHPUT = 1, DUCK_STEP_LATENCY = 2, DUCK_STEP_PAIRED = 3 };
+ * duck_set_step_mode refuses that mode with DUCK_EUNSUPPORTED and AUTO skips it.
+ * LATENCY_X2 (round 6) is the LATENCY kernel compiled for two waves per SIMD (<= 256 registers per
+ * lane), so that two of its 4-env workgroups share a CU: the shortest env-step at 4-8 envs per CU in
+ * the plane-floor scenes without backlash, the only models it is compiled for (elsewhere its register
+ * spills make it slower than PAIRED); AUTO takes it there instead of PAIRED. */
+enum { DUCK_STEP_AUTO = 0, DUCK_STEP_THROUGHPUT = 1, DUCK_STEP_LATENCY = 2, DUCK_STEP_PAIRED = 3,
+       DUCK_STEP_LATENCY_X2 = 4 };
 int duck_set_step_mode(duck_sim* sim, int mode);
-/* the kernel duck_step would launch for n_envs envs: DUCK_STEP_THROUGHPUT, _LATENCY or _PAIRED */
+/* the kernel duck_step would launch for n_envs envs: DUCK_STEP_THROUGHPUT, _LATENCY, _PAIRED or _LATENCY_X2 */
 int duck_step_kernel_for(const duck_sim* sim, int n_envs);
 /* debug: latency-mode event waits that gave up (a broken cross-wave schedule; must stay 0) */
 int duck_debug_lat_timeouts(const duck_sim* sim, unsigned* out, int reset);

@@ -158,6 +158,7 @@ int duck_create(const duck_model_desc* model, const duck_env_config* cfg, const 
   s->step_mode = DUCK_STEP_AUTO;
   s->lat_ok = kVariants[v]->lds_bytes_lat() != 0;
   s->lat2_ok = kVariants[v]->lds_bytes_lat2() != 0;
+  s->latx2_ok = kVariants[v]->lds_bytes_lat_x2() != 0;
   {
     hipError_t e = hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) {
@@ -263,9 +264,11 @@ int duck_physics_step(duck_sim* s, int n, float* qpos, float* qvel, float* warm,
 
 int duck_set_step_mode(duck_sim* s, int mode) {
   g_err.clear();
-  if (!s || mode < DUCK_STEP_AUTO || mode > DUCK_STEP_PAIRED) return duck_fail(DUCK_EINVAL, "bad argument");
-  if ((mode == DUCK_STEP_LATENCY && !s->lat_ok) || (mode == DUCK_STEP_PAIRED && !s->lat2_ok))
-    return duck_fail(DUCK_EUNSUPPORTED, "this model's LDS budget does not fit that step kernel (AUTO skips it)");
+  if (!s || mode < DUCK_STEP_AUTO || mode > DUCK_STEP_LATENCY_X2) return duck_fail(DUCK_EINVAL, "bad argument");
+  if ((mode == DUCK_STEP_LATENCY && !s->lat_ok) || (mode == DUCK_STEP_PAIRED && !s->lat2_ok) ||
+      (mode == DUCK_STEP_LATENCY_X2 && !s->latx2_ok))
+    return duck_fail(DUCK_EUNSUPPORTED, "that step kernel is not compiled for this model (LDS budget, or "
+                                        "LATENCY_X2 outside the plane-floor scenes; AUTO skips it)");
   s->step_mode = mode;
   return DUCK_OK;
 }

@@ -42,6 +42,7 @@ struct duck_sim {
   int step_mode;  // DUCK_STEP_*
   int n_cu;       // compute units of the device (DUCK_STEP_AUTO)
   int lat_ok, lat2_ok;  // the latency / paired latency kernels are compiled for this model (TLay::FITS)
+  int latx2_ok;         // the two-workgroups-per-CU latency kernel is (LatX2::PAYS)
   volatile unsigned* err_h;  // sticky device error word (DUCK_DEVERR_*), host-mapped pinned memory
   unsigned* err_d;           // its device mapping (KArgs::err)
 };
@@ -64,15 +65,20 @@ struct VariantOps {
   int (*lat_timeouts)(unsigned* out, int reset);
   size_t (*lds_bytes_lat)();
   size_t (*lds_bytes_lat2)();
+  size_t (*lds_bytes_lat_x2)();
 };
 
-// the step kernel duck_step launches for n envs (DUCK_STEP_THROUGHPUT / _LATENCY / _PAIRED): the mode
-// asked for, or under AUTO the latency kernel while n <= 4 envs per CU, the paired latency kernel
-// while n <= 8 per CU, else the throughput kernel; a split a model does not fit (lat_ok / lat2_ok) is
-// skipped: the paired kernel then covers <= 8 per CU, or the throughput kernel everything
+// the step kernel duck_step launches for n envs (DUCK_STEP_THROUGHPUT / _LATENCY / _PAIRED /
+// _LATENCY_X2): the mode asked for, or under AUTO the latency kernel while n <= 4 envs per CU, then
+// while n <= 8 per CU the two-workgroups-per-CU latency kernel where the model has it (flat scenes)
+// or else the paired latency kernel, else the throughput kernel; a split a model does not fit
+// (lat_ok / lat2_ok / latx2_ok) is skipped
 inline int step_kernel_choice(const duck_sim* s, int n) {
   if (s->step_mode != DUCK_STEP_AUTO) return s->step_mode;
   if (s->lat_ok && n <= LAT_WG_HOST * s->n_cu) return DUCK_STEP_LATENCY;
-  if (s->lat2_ok && n <= 2 * LAT_WG_HOST * s->n_cu) return DUCK_STEP_PAIRED;
+  if (n <= 2 * LAT_WG_HOST * s->n_cu) {
+    if (s->latx2_ok) return DUCK_STEP_LATENCY_X2;
+    if (s->lat2_ok) return DUCK_STEP_PAIRED;
+  }
   return DUCK_STEP_THROUGHPUT;
 }

@@ -898,8 +898,9 @@ __global__ void __launch_bounds__(TPB) step_kernel(KArgs A) {
 // the smooth acceleration (M's factorization and solve). Same stage code and arithmetic as step_kernel, so the
 // results are the same bit for bit (test_gpu_env.py::test_latency_mode_matches_throughput_mode);
 // one env-step of a small batch takes the critical path through the waves instead of the sum.
+// (the body of step_kernel_lat and step_kernel_lat_x2 below)
 template <class Md, int LAT>
-__global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
+__device__ __forceinline__ void step_lat_body(KArgs A) {
   using TL = TLay<Md, LAT>;
   using TPL = TPhys<Md, LAT>;
   constexpr int WGL = TL::NWG;
@@ -996,6 +997,36 @@ __global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
   }
 }
 
+template <class Md, int LAT>
+__global__ void __launch_bounds__(TPB) step_kernel_lat(KArgs A) {
+  step_lat_body<Md, LAT>(A);
+}
+
+// Two latency workgroups per CU (DUCK_STEP_LATENCY_X2, round 6): the four-wave latency kernel capped at
+// 256 VGPR + AGPR per lane (amdgpu_waves_per_eu(2, 2)), so that a CU holds two of its workgroups -- two
+// waves per SIMD, each hiding the other's stalls -- where the LDS allows (2 x lds_bytes_lat <= 160 KiB).
+// Measured (profiles/r06_two_waves.txt): flat, 2 VGPRs spilled, C2 at 2,048 envs 0.1692 ms per env-step
+// against 0.1744 (paired) and 0.2822 (latency, two rounds); the rough scenes spill 86-114 VGPRs and lose
+// to the paired kernel (C4 0.387 vs 0.335 ms, C5 0.427 vs 0.370), and at <= 1,024 envs (one workgroup
+// per CU anyway) the spills cost 6 % against the uncapped kernel. So it is compiled for plane-floor
+// models without backlash hinges only (lat_x2_pays) and AUTO takes it at 4-8 envs per CU there.
+// Its stage code is instantiated with LAT = LAT_X2, which every LAT test treats as LAT = 1 (same work
+// split, same layout): a separate TPhys instantiation, so that its out-of-line rare paths (newton_dense,
+// collide_hulls_rare) are compiled within the 256-register budget too -- shared with the uncapped kernel
+// they would take its budget and hold this one at one wave per SIMD.
+constexpr int LAT_X2 = 5;
+template <class Md>
+struct LatX2 {
+  static_assert(TLay<Md, LAT_X2>::LDS_FLOATS == TLay<Md, 1>::LDS_FLOATS && TLay<Md, LAT_X2>::NWG == LAT_WG,
+                "LAT_X2 is the LAT = 1 layout");
+  static constexpr bool PAYS = TLay<Md, 1>::FITS && 2 * (size_t)TLay<Md, 1>::LDS_FLOATS * 4 <= 160 * 1024 &&
+                               Md::FLOOR_TYPE == 0 && Md::NV <= 20;
+};
+template <class Md>
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2, 2))) step_kernel_lat_x2(KArgs A) {
+  if constexpr (LatX2<Md>::PAYS) step_lat_body<Md, LAT_X2>(A);
+}
+
 template <class Md, int WG>
 __global__ void __launch_bounds__(TPB) physics_kernel(KArgs A, float* qpos_g, float* qvel_g, float* warm_g,
                                                      const float* ctrl_g, int nsub, float* aux) {
@@ -1078,6 +1109,10 @@ template <class Md>
 static size_t lds_bytes_lat2() {
   return TLay<Md, 2>::FITS ? (size_t)TLay<Md, 2>::LDS_FLOATS * sizeof(float) : 0;
 }
+template <class Md>
+static size_t lds_bytes_lat_x2() {
+  return LatX2<Md>::PAYS ? (size_t)TLay<Md, 1>::LDS_FLOATS * sizeof(float) : 0;
+}
 
 template <class Md>
 static int aux_size_of() {
@@ -1122,10 +1157,15 @@ static int launch_step(duck_sim* s, int n, float* fs, int32_t* is, const float* 
   // whole CU, one wave of 512 registers per SIMD)
   static_assert(LAT_WG == LAT_WG_HOST, "latency workgroup size");
   const int k = step_kernel_choice(s, n);
-  if (k == DUCK_STEP_LATENCY || k == DUCK_STEP_PAIRED) {
+  if (k == DUCK_STEP_LATENCY || k == DUCK_STEP_PAIRED || k == DUCK_STEP_LATENCY_X2) {
     const int wgl = k == DUCK_STEP_PAIRED ? 2 * LAT_WG : LAT_WG;
     const dim3 grid((A.n + wgl - 1) / wgl), block(TPB);
-    if (k == DUCK_STEP_PAIRED) {
+    if (k == DUCK_STEP_LATENCY_X2) {
+      if constexpr (LatX2<Md>::PAYS)
+        hipLaunchKernelGGL((step_kernel_lat_x2<Md>), grid, block, lds_bytes_lat_x2<Md>(), st, A);
+      else
+        return duck_fail(DUCK_EUNSUPPORTED, "the two-workgroups-per-CU latency kernel is not compiled for this model");
+    } else if (k == DUCK_STEP_PAIRED) {
       if constexpr (TLay<Md, 2>::FITS)
         hipLaunchKernelGGL((step_kernel_lat<Md, 2>), grid, block, lds_bytes_lat2<Md>(), st, A);
       else
@@ -1201,6 +1241,6 @@ static int stage_cycles_of(unsigned long long* out, int reset) {
                                    lds_bytes<MODEL>,    MODEL::FLOOR_TYPE,      launch_reset<MODEL>, \
                                    launch_step<MODEL>,  launch_randomize<MODEL>, launch_physics<MODEL>, \
                                    stage_cycles_of,     lat_timeouts_of,        lds_bytes_lat<MODEL>, \
-                                   lds_bytes_lat2<MODEL>};                                              \
+                                   lds_bytes_lat2<MODEL>, lds_bytes_lat_x2<MODEL>};                     \
     return &ops;                                                                                \
   }

@@ -42,7 +42,7 @@ from .refmotion import PolyReferenceMotion
 USE_IMITATION_REWARD = cfgmod.USE_IMITATION_REWARD
 USE_MOTOR_SPEED_LIMITS = cfgmod.USE_MOTOR_SPEED_LIMITS
 # duck_set_step_mode (include/duck.h DUCK_STEP_*)
-STEP_MODES = {"auto": 0, "throughput": 1, "latency": 2, "paired": 3}
+STEP_MODES = {"auto": 0, "throughput": 1, "latency": 2, "paired": 3, "latency_x2": 4}
 
 
 @dataclass
@@ -218,12 +218,13 @@ class Joystick(OpenDuckMiniV2Env):
             check(self._lib.duck_set_step_mode(self._sim, STEP_MODES[self._step_mode]), self._lib)
 
     def set_step_mode(self, mode: str) -> None:
-        """duck_set_step_mode: "auto" (default), "throughput", "latency" or "paired". The same stage code
+        """duck_set_step_mode: "auto" (default), "throughput", "latency", "paired" or "latency_x2". The same stage code
         in a different work split: "throughput" runs 16 envs per workgroup on one team each; "latency"
         splits each substep's stages over four waves per 4 envs (a shorter env-step for small batches,
         e.g. a 4096-env job strong-scaled over 4 or 8 GPUs); "paired" splits them over a pair of waves
         per 4 envs, 8 envs per workgroup (4096 envs over 2 GPUs); "auto" takes latency at <= 4 envs
-        per CU and paired at <= 8. Every mode gives bit-identical results (include/duck.h)."""
+        per CU and paired at <= 8 -- "latency_x2" instead in the plane-floor scenes without backlash: the latency
+        kernel at two workgroups per CU. Every mode gives bit-identical results (include/duck.h)."""
         if mode not in STEP_MODES:
             raise DuckError(f"step mode {mode!r} not in {sorted(STEP_MODES)}")
         if not hasattr(self._lib, "duck_set_step_mode") and mode in ("auto", "throughput"):
@@ -233,12 +234,12 @@ class Joystick(OpenDuckMiniV2Env):
 
     @property
     def step_kernel(self) -> str:
-        """The kernel step() launches for this batch: "throughput", "latency" or "paired"."""
+        """The kernel step() launches for this batch: "throughput", "latency", "paired" or "latency_x2"."""
         if not hasattr(self._lib, "duck_step_kernel_for"):
             return "throughput"
         k = self._lib.duck_step_kernel_for(self._sim, self.num_envs)
         check(min(k, 0), self._lib)
-        return {1: "throughput", 2: "latency", 3: "paired"}[k]
+        return {1: "throughput", 2: "latency", 3: "paired", 4: "latency_x2"}[k]
 
     def device_error(self, clear: bool = False) -> int:
         """The handle's sticky device error word (duck_device_error; DUCK_DEVERR_* bits, 0 = none). While

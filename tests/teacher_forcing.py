@@ -259,6 +259,9 @@ CASES = {
     # the paired latency kernel (each substep's stages over a pair of waves per 4 envs)
     "flat_paired_kernel": dict(task="flat_terrain", imitation=True, force_push=True, force_resample=True,
                                step_mode="paired"),
+    # the latency kernel at two workgroups per CU (round 6; plane-floor scenes without backlash)
+    "flat_latency_x2_kernel": dict(task="flat_terrain", imitation=True, force_push=True, force_resample=True,
+                                   step_mode="latency_x2"),
     "rough_backlash_dr_paired_kernel": dict(task="rough_terrain_backlash", imitation=False, dr=True,
                                             force_push=True, step_mode="paired"),
 }

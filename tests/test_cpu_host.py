@@ -268,7 +268,7 @@ def test_round4_entry_points_refuse_bad_arguments():
     assert lib.duck_step_kernel_for(None, 4) < 0
 
 
-def test_bench_self_launch_command(monkeypatch):
+def test_bench_self_launch_command(monkeypatch, capsys):
     """bench.py --gpus N (N > 1, no WORLD_SIZE) starts torch.distributed.run as a child with the same
     arguments and returns its exit code; --gpus 1 runs in-process (VERDICT r05 #1). No GPU call here."""
     import subprocess
@@ -279,11 +279,17 @@ def test_bench_self_launch_command(monkeypatch):
     import bench
     seen = {}
 
-    def fake_run(cmd, env=None, **kw):
-        seen["cmd"], seen["env"] = cmd, env
-        return types.SimpleNamespace(returncode=7)
+    class FakePopen:
+        def __init__(self, cmd, env=None, **kw):
+            seen["cmd"], seen["env"] = cmd, env
+            # what the ranks write: gloo's peer notice glued to the front of rank 0's line
+            self.stdout = iter(["[Gloo] Rank 0 is connected to 1 peer ranks.[Gloo] Rank\n",
+                                '1 is connected{"metric": "m", "value": 1}\n'])
 
-    monkeypatch.setattr(subprocess, "run", fake_run)
+        def wait(self):
+            return 7
+
+    monkeypatch.setattr(subprocess, "Popen", FakePopen)
     assert bench._self_launch(["--gpus", "1", "--steps", "3"]) == -1 and not seen
     assert bench._self_launch(["--gpus", "4", "--steps", "3", "--strong"]) == 7
     cmd = seen["cmd"]
@@ -293,3 +299,6 @@ def test_bench_self_launch_command(monkeypatch):
     assert os.path.basename(cmd[-6]) == "bench.py"
     assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
     assert bench._self_launch(["--gpus=2"]) == 7 and "--nproc-per-node=2" in seen["cmd"]
+    out = capsys.readouterr()
+    assert out.out.splitlines() == ['{"metric": "m", "value": 1}'] * 2     # stdout: only the bench lines
+    assert "[Gloo]" in out.err and "1 is connected" in out.err

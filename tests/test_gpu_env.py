@@ -186,7 +186,8 @@ def test_full_size_runs_are_deterministic(cfg, gpu):
 
 @pytest.mark.parametrize("cfg,n,mode", [("C2", 512, "latency"), ("C3", 1021, "latency"), ("C4", 1024, "latency"),
                                         ("C5", 510, "latency"), ("C2", 2048, "paired"), ("C3", 1021, "paired"),
-                                        ("C4", 2044, "paired"), ("C5", 2048, "paired")])
+                                        ("C4", 2044, "paired"), ("C5", 2048, "paired"), ("C2", 2048, "latency_x2"),
+                                        ("C3", 1021, "latency_x2")])
 def test_latency_mode_matches_throughput_mode(cfg, n, mode, gpu):
     """The latency kernel (each substep's stages split over four waves per 4 envs, DUCK_STEP_LATENCY)
     and the paired latency kernel (the stages over a pair of waves per 4 envs, 8 envs per workgroup,
@@ -222,7 +223,7 @@ def test_latency_mode_matches_throughput_mode(cfg, n, mode, gpu):
     assert envs["latency"].lat_timeouts() == 0
 
 
-@pytest.mark.parametrize("mode,wg_envs", [("latency", 4), ("paired", 8)])
+@pytest.mark.parametrize("mode,wg_envs", [("latency", 4), ("paired", 8), ("latency_x2", 4)])
 def test_latency_timeout_surfaces(mode, wg_envs, gpu, monkeypatch):
     """A latency-kernel launch whose cross-wave wait gives up is not silent: the test build
     (native.debug_library "force_timeout", -DDUCK_LAT_FORCE_TIMEOUT: in workgroup 1 the waits for the
@@ -265,9 +266,15 @@ def test_step_mode_auto_selects_by_batch(gpu):
     """AUTO: the latency kernel while the batch leaves a CU per 4 envs, the paired latency kernel while
     it leaves a CU per 8, the throughput kernel above."""
     ncu = torch.cuda.get_device_properties(gpu).multi_processor_count
-    for n, want in ((4 * ncu, "latency"), (4 * ncu + 1, "paired"), (8 * ncu, "paired"), (8 * ncu + 1, "throughput")):
-        env = Joystick("flat_terrain", num_envs=n, device=gpu, use_imitation=False)
-        assert env.step_kernel == want, (n, ncu)
+    for task, mid in (("flat_terrain", "latency_x2"), ("rough_terrain", "paired"), ("rough_terrain_backlash", "paired"),
+                      ("flat_terrain_backlash", "paired")):
+        for n, want in ((4 * ncu, "latency"), (4 * ncu + 1, mid), (8 * ncu, mid), (8 * ncu + 1, "throughput")):
+            env = Joystick(task, num_envs=n, device=gpu, use_imitation=False)
+            assert env.step_kernel == want, (task, n, ncu)
+    # a mode the model is not compiled for is refused (LATENCY_X2 exists for the plane floor without backlash)
+    from open_duck_playground_amd.native import DuckError
+    with pytest.raises(DuckError, match="not compiled for this model"):
+        Joystick("rough_terrain", num_envs=64, device=gpu, use_imitation=False).set_step_mode("latency_x2")
 
 
 def test_full_size_long_rollout_with_auto_reset(gpu):

@@ -54,10 +54,10 @@ def test_direct_launch_two_ranks(gpu):
     assert d["config"]["total_envs"] == 8192 and d["config"]["step_kernel"] == "throughput"
 
 
-def test_direct_launch_strong_takes_paired_kernel(gpu):
+def test_direct_launch_strong_takes_the_x2_latency_kernel(gpu):
     d = _bench_direct(["--strong"])
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["envs_per_gpu"] == 2048
-    assert d["config"]["step_kernel"] == "paired"
+    assert d["config"]["step_kernel"] == "latency_x2"
 
 
 def test_two_rank_weak_scaling_line(gpu):
