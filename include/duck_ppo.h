@@ -21,6 +21,13 @@ extern "C" {
  *   delta_t = (r_t + discount (1 - term_t) v_{t+1} - v_t)(1 - trunc_t),  v_T = bootstrap
  *   acc_t   = delta_t + discount (1 - term_t)(1 - trunc_t) lambda acc_{t+1},  vs_t = acc_t + v_t
  *   adv_t   = (r_t + discount (1 - term_t) vs_{t+1} - v_t)(1 - trunc_t),  vs_T = bootstrap */
+/* duck_gae from the rollout's raw fields in one launch for B <= 1024 trajectories: termination =
+ * done (1 - truncation), rewards scaled by reward_scale (brax's reward_scaling), then, when
+ * normalize_advantage, stats[2] = {mean, 1 / (population std + 1e-8)} of all T x B advantages (else
+ * {0, 1}) for duck_ppo_loss_stats. (Round 6: one launch instead of five per learner minibatch.) */
+int duck_gae_stats(int T, int B, const float* truncation, const float* done, const float* reward, float reward_scale,
+                   const float* value, const float* bootstrap, float lambda_, float discount, float* vs, float* adv,
+                   int normalize_advantage, float* stats, void* stream);
 int duck_gae(int T, int B, const float* truncation, const float* termination, const float* reward,
              const float* value, const float* bootstrap, float lambda_, float discount, float* vs, float* adv,
              void* stream);
@@ -39,6 +46,13 @@ int duck_ppo_loss(int N, int A, const float* logits, const float* raw_action, co
                   const float* advantage, const float* value_target, const float* baseline, const float* eps,
                   float clip_eps, float entropy_cost, int normalize_advantage, float* out, float* grad_logits,
                   float* grad_baseline, void* stream);
+/* duck_ppo_loss with the advantage statistics given (stats[2] = {mean, 1 / (std + 1e-8)} of the
+ * advantages, as duck_gae_stats writes them; the advantages are normalised with them): one launch
+ * fewer. Same out / gradient contract. (Round 6.) */
+int duck_ppo_loss_stats(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
+                        const float* advantage, const float* value_target, const float* baseline, const float* eps,
+                        float clip_eps, float entropy_cost, const float* stats, float* out, float* grad_logits,
+                        float* grad_baseline, void* stream);
 /* 4 + 2 + 3 ceil(N / 16): the length of duck_ppo_loss's out array (A <= 31) */
 int duck_ppo_loss_out_size(int N);
 
@@ -53,6 +67,12 @@ typedef struct {
   int T, B, w;
 } duck_gather_field;
 int duck_gather_columns(int nfields, const duck_gather_field* fields, const long long* idx, int m, void* stream);
+/* duck_gather_columns with an observation normaliser per field: norm[2 f], norm[2 f + 1] = mean[w_f],
+ * 1 / std[w_f] (both NULL: a plain copy), dst = (src - mean[c]) * istd[c] -- the op(X) the first MLP
+ * layers otherwise apply on their loads, in the same fp32 expression, so the results are unchanged.
+ * (Round 6: the forward and weight-gradient GEMMs of the first layers then read plain rows.) */
+int duck_gather_columns_norm(int nfields, const duck_gather_field* fields, const float* const* norm,
+                             const long long* idx, int m, void* stream);
 
 /* The policy / value MLP layers (brax ppo/networks.py: Dense + swish; nn.Linear weight layout
  * W [M][R] row-major, bias [M]) on fp32 MFMA, row-major activations [N][.]:
@@ -83,6 +103,10 @@ typedef struct {
   float* partial;
 } duck_mlp_problem;
 int duck_mlp_group(int n, const duck_mlp_problem* problems, void* stream);
+/* duck_mlp_group with output tiles 64 rows x `bn` columns (32 or 64; duck_mlp_group = 32). Every output
+ * element's reduction runs in the same order whatever the tile, so the results are bit-identical;
+ * 64-wide tiles halve the re-reads of the row operand for the wide layers. (Round 6.) */
+int duck_mlp_group_bn(int n, const duck_mlp_problem* problems, int bn, void* stream);
 /* grad[i] = sum_{s < splits} partial[s][i] in order (deterministic), i < P */
 int duck_mlp_wgrad_reduce(int P, int splits, const float* partial, float* grad, void* stream);
 /* The rollout's policy sample (brax NormalTanhDistribution): for each of N rows of logits [N][2A]

@@ -33,7 +33,7 @@
 namespace {
 
 constexpr int BM = 64;    // output tile rows (the batch rows for the forward / data-gradient GEMMs)
-constexpr int BN = 32;    // output tile columns
+constexpr int BN = 32;    // output tile columns (duck_mlp_gemm / duck_mlp_wgrad; duck_mlp_group_bn takes 32 or 64)
 // reduction chunk. Deeper chunks mean fewer memory round trips per tile but more LDS per workgroup:
 // KC = 128 (49.5 KB, 3 workgroups per CU) made training 1.9 -> 1.2 M env-steps/s same-box against
 // KC = 32 (12.7 KB): the resident workgroups hiding each other's load latency matter more
@@ -173,15 +173,15 @@ __device__ __forceinline__ void mma_chunk(const float* As, const float* Bs, int 
 
 // Forward (MODE 0: Y = op(A) W^T + b; MODE 1: the same, Y = Z and Y2 = silu(Z)) and the data gradient
 // (MODE 2: Y = (A W) * silu'(aux), A = dZ [N][R], W [R][Mo], aux = Z_prev). Output [N][Mo].
-template <int MODE>
+template <int MODE, int BNT = BN>
 __device__ __forceinline__ void gemm_tile(int bx, int by, float* As, float* Bs, int N, int R, int Mo,
                                           const float* __restrict__ A, const float* __restrict__ W,
                                           const float* __restrict__ bias, const float* __restrict__ aux,
                                           float* __restrict__ Y, float* __restrict__ Y2,
                                           const float* __restrict__ mean, const float* __restrict__ istd) {
-  constexpr int TI = BM / 32, TJ = BN / 32;
-  const int r0 = bx * BM, c0 = by * BN;
-  const int w = threadIdx.x >> 6, wr = (BM / 2) * (w >> 1), wc = (BN / 2) * (w & 1);
+  constexpr int TI = BM / 32, TJ = BNT / 32;
+  const int r0 = bx * BM, c0 = by * BNT;
+  const int w = threadIdx.x >> 6, wr = (BM / 2) * (w >> 1), wc = (BNT / 2) * (w & 1);
   f4 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; i++)
@@ -190,8 +190,8 @@ __device__ __forceinline__ void gemm_tile(int bx, int by, float* As, float* Bs, 
   // two register sets of staged chunks (set k & 1 holds chunk k): chunk c + 2's loads are issued while
   // chunk c's MFMAs run and stored a whole chunk later, so each load has two chunks of MFMAs to land
   RowTile<BM> la[2];
-  RowTile<BN> lbr[2];  // MODE 0/1: the rows of W (output columns), reduction contiguous
-  ColTile<BN> lbc[2];  // MODE 2: W [R][Mo], reduction over its rows
+  RowTile<BNT> lbr[2];  // MODE 0/1: the rows of W (output columns), reduction contiguous
+  ColTile<BNT> lbc[2];  // MODE 2: W [R][Mo], reduction over its rows
   for (int q = 0; q < 2; q++) {
     la[q].init(A, R, N, r0);
     if (MODE != 2) lbr[q].init(W, R, Mo, c0);
@@ -270,21 +270,22 @@ __global__ __launch_bounds__(256) void mlp_gemm_kernel(int N, int R, int Mo, con
 // [dW | db][m][k] = sum over this workgroup's rows n of dZ[n][m] [op(H) | 1][n][k]: partial s =
 // blockIdx.z, written to part + s * P at the layer's offsets (weights at offw, bias at offb; P = the
 // parameter count of the networks sharing the partial array).
+template <int BNT = BN>
 __device__ __forceinline__ void wgrad_tile(int bx, int by, int bz, float* As, float* Bs, int N, int Mo, int Ki,
                                            const float* __restrict__ dZ, const float* __restrict__ H,
                                            const float* __restrict__ mean, const float* __restrict__ istd,
                                            int rows_per_split, float* __restrict__ part, int P, int offw, int offb) {
-  constexpr int TI = BM / 32, TJ = BN / 32;
-  const int m0 = bx * BM, k0c = by * BN, s = bz;
+  constexpr int TI = BM / 32, TJ = BNT / 32;
+  const int m0 = bx * BM, k0c = by * BNT, s = bz;
   const int n_lo = s * rows_per_split, R = min(N, n_lo + rows_per_split) - n_lo;
-  const int w = threadIdx.x >> 6, wr = (BM / 2) * (w >> 1), wc = (BN / 2) * (w & 1);
+  const int w = threadIdx.x >> 6, wr = (BM / 2) * (w >> 1), wc = (BNT / 2) * (w & 1);
   f4 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; i++)
 #pragma unroll
     for (int j = 0; j < TJ; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   ColTile<BM> la[2];  // A = dZ^T: columns m, reduction n over the rows (two staged chunks, as above)
-  ColTile<BN> lb[2];  // B = [op(H) | 1]: columns k, rows n
+  ColTile<BNT> lb[2];  // B = [op(H) | 1]: columns k, rows n
   const float* dz = dZ + (size_t)(R > 0 ? n_lo : 0) * Mo;
   const float* h = H + (size_t)(R > 0 ? n_lo : 0) * Ki;
   auto load = [&](auto S, int n0) {
@@ -354,8 +355,9 @@ struct MlpGroupArgs {
   int gx[DUCK_MLP_GROUP_MAX], gy[DUCK_MLP_GROUP_MAX], rps[DUCK_MLP_GROUP_MAX];
   duck_mlp_problem p[DUCK_MLP_GROUP_MAX];
 };
+template <int BNT>
 __global__ __launch_bounds__(256) void mlp_group_kernel(MlpGroupArgs g) {
-  __shared__ float As[BM * LDP], Bs[BN * LDP];
+  __shared__ float As[BM * LDP], Bs[BNT * LDP];
   const int b = blockIdx.x;
   int q = 0;
 #pragma unroll
@@ -364,12 +366,12 @@ __global__ __launch_bounds__(256) void mlp_group_kernel(MlpGroupArgs g) {
   const int t = b - g.start[q], gx = g.gx[q], gy = g.gy[q];
   const int bz = t / (gx * gy), rem = t - bz * gx * gy, by = rem / gx, bx = rem - by * gx;
   switch (p.kind) {
-    case 0: gemm_tile<0>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, p.mean, p.istd); break;
-    case 1: gemm_tile<1>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, p.mean, p.istd); break;
-    case 2: gemm_tile<2>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, nullptr, nullptr); break;
+    case 0: gemm_tile<0, BNT>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, p.mean, p.istd); break;
+    case 1: gemm_tile<1, BNT>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, p.mean, p.istd); break;
+    case 2: gemm_tile<2, BNT>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, nullptr, nullptr); break;
     default:
-      wgrad_tile(bx, by, bz, As, Bs, p.N, p.M, p.R, p.A, p.W, p.mean, p.istd, g.rps[q], p.partial, p.P, p.off_w,
-                 p.off_b);
+      wgrad_tile<BNT>(bx, by, bz, As, Bs, p.N, p.M, p.R, p.A, p.W, p.mean, p.istd, g.rps[q], p.partial, p.P, p.off_w,
+                      p.off_b);
   }
 }
 
@@ -461,10 +463,22 @@ __global__ __launch_bounds__(ADAM_TPB) void adam_update_kernel(int P, int nblk, 
                                                                float* __restrict__ v, const float* __restrict__ partial,
                                                                const int* __restrict__ step, float lr, float b1,
                                                                float b2, float eps, float max_norm) {
+  // the partials' sum in one fixed order in every workgroup (the same norm everywhere): thread t sums
+  // partials t, t + 256, .. in double, then the wave sums and the 4 wave totals in order. (A serial
+  // sum on thread 0 -- 230 dependent loads at the learner's 0.47 M parameters -- took 3/4 of this
+  // launch's 15.7 us, profiles/r06_ppo_trace_summary_before.txt)
+  __shared__ double wsum[ADAM_TPB / 64];
   __shared__ float coef;
+  {
+    double t = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += ADAM_TPB) t += partial[b];
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_down(t, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0;
-    for (int b = 0; b < nblk; b++) t += partial[b];
+    for (int w = 0; w < ADAM_TPB / 64; w++) t += wsum[w];
     const float norm = sqrtf((float)t);
     const float c = max_norm > 0.f ? max_norm / (norm + 1e-6f) : 1.f;
     coef = c < 1.f ? c : 1.f;
@@ -527,8 +541,10 @@ extern "C" int duck_mlp_wgrad(int N, int M, int K, const float* dZ, const float*
   return DUCK_OK;
 }
 
-extern "C" int duck_mlp_group(int n, const duck_mlp_problem* probs, void* stream) {
+extern "C" int duck_mlp_group_bn(int n, const duck_mlp_problem* probs, int bn, void* stream) {
   if (n < 0 || n > DUCK_MLP_GROUP_MAX) return duck_fail(DUCK_EINVAL, "duck_mlp_group: 0 .. DUCK_MLP_GROUP_MAX problems");
+  if (bn != 32 && bn != 64) return duck_fail(DUCK_EINVAL, "duck_mlp_group_bn: tile width 32 or 64");
+  const int BN = bn;  // (shadows the default tile width for the grid arithmetic below)
   if (n == 0) return DUCK_OK;
   if (!probs) return duck_fail(DUCK_EINVAL, "duck_mlp_group: null pointer");
   MlpGroupArgs g;
@@ -563,9 +579,16 @@ extern "C" int duck_mlp_group(int n, const duck_mlp_problem* probs, void* stream
   g.start[n] = (int)tot;
   for (int k = n; k <= DUCK_MLP_GROUP_MAX; k++) g.start[k] = (int)tot;
   if (tot == 0) return DUCK_OK;
-  hipLaunchKernelGGL(mlp_group_kernel, dim3((unsigned)tot), dim3(256), 0, (hipStream_t)stream, g);
+  if (bn == 64)
+    hipLaunchKernelGGL(mlp_group_kernel<64>, dim3((unsigned)tot), dim3(256), 0, (hipStream_t)stream, g);
+  else
+    hipLaunchKernelGGL(mlp_group_kernel<32>, dim3((unsigned)tot), dim3(256), 0, (hipStream_t)stream, g);
   HIPCHECK(hipGetLastError());
   return DUCK_OK;
+}
+
+extern "C" int duck_mlp_group(int n, const duck_mlp_problem* probs, void* stream) {
+  return duck_mlp_group_bn(n, probs, 32, stream);
 }
 
 extern "C" int duck_mlp_wgrad_reduce(int P, int splits, const float* partial, float* grad, void* stream) {

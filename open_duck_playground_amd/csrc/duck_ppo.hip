@@ -52,6 +52,60 @@ __device__ float block_sum(float v, float* red) {
     return r;
 }
 
+// GAE straight from the rollout fields, with the advantage statistics, in one workgroup (B <= 1024
+// trajectories: the learner's minibatch is 256): termination = done (1 - truncation) and the reward
+// scaling (what ppo.FusedGrad computed with three torch launches), the recursion of gae_kernel, then
+// the mean and population std of all T x B advantages as adv_stats_kernel computes them (two passes;
+// each thread re-reads the advantages it wrote). One launch instead of five per minibatch.
+__global__ __launch_bounds__(1024) void gae_stats_kernel(int T, int B, const float* __restrict__ trunc,
+                                                        const float* __restrict__ done, const float* __restrict__ rew,
+                                                        float rscale, const float* __restrict__ val,
+                                                        const float* __restrict__ boot, float lam, float disc,
+                                                        float* __restrict__ vs, float* adv, int normalize,
+                                                        float* __restrict__ stats) {
+    __shared__ float red[16];
+    const int b = threadIdx.x;
+    float s = 0.f;
+    if (b < B) {
+        float v_next = boot[b], vs_next = boot[b], acc = 0.f;
+        for (int t = T - 1; t >= 0; --t) {
+            const size_t i = (size_t)t * B + b;
+            const float tr = trunc[i];
+            const float keep = 1.f - tr;
+            // rounded products (no FMA contraction into the sums below): the values the separate torch
+            // launches produced, so the recursion is gae_kernel's bit for bit
+            const float term = __fmul_rn(done[i], 1.f - tr);
+            const float cont = disc * (1.f - term);
+            const float r = __fmul_rn(rew[i], rscale), v = val[i];
+            const float delta = (r + cont * v_next - v) * keep;
+            acc = delta + cont * keep * lam * acc;
+            const float vs_t = acc + v;
+            const float a = (r + cont * vs_next - v) * keep;
+            adv[i] = a;
+            vs[i] = vs_t;
+            s += a;
+            v_next = v;
+            vs_next = vs_t;
+        }
+    }
+    const float invN = 1.f / (float)(T * B);
+    float mean = 0.f, inv_std = 1.f;
+    if (normalize) {
+        mean = block_sum(s, red) * invN;
+        float q = 0.f;
+        if (b < B)
+            for (int t = 0; t < T; t++) {
+                const float d = adv[(size_t)t * B + b] - mean;
+                q += d * d;
+            }
+        inv_std = 1.f / (sqrtf(block_sum(q, red) * invN) + 1e-8f);
+    }
+    if (threadIdx.x == 0) {
+        stats[0] = mean;
+        stats[1] = inv_std;
+    }
+}
+
 __device__ __forceinline__ float softplusf(float x) { return x > 20.f ? x : log1pf(expf(x)); }
 __device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
 // log |d tanh(x)/dx| = 2 (log 2 - x - softplus(-2x)) and its derivative -2 tanh(x)
@@ -276,6 +330,8 @@ __global__ __launch_bounds__(1024) void ppo_loss_sum_kernel(int N, int nblk, con
 struct GatherArgs {
     duck_gather_field f[DUCK_GATHER_MAX];
     long long start[DUCK_GATHER_MAX + 1];  // prefix sums of T_f m w_f
+    const float* mean[DUCK_GATHER_MAX];    // per-field normaliser (duck_gather_columns_norm), or null
+    const float* istd[DUCK_GATHER_MAX];
 };
 
 // one thread per copied float: the field by the prefix sums, then (t, j, c)
@@ -289,12 +345,14 @@ __global__ __launch_bounds__(256) void gather_kernel(int nf, GatherArgs a, const
     const long long row = o / w;
     const int c = (int)(o - row * w);
     const int t = (int)(row / m), j = (int)(row - (long long)t * m);
-    a.f[f].dst[o] = a.f[f].src[((long long)t * a.f[f].B + idx[j]) * w + c];
+    const float x = a.f[f].src[((long long)t * a.f[f].B + idx[j]) * w + c];
+    a.f[f].dst[o] = a.mean[f] ? (x - a.mean[f][c]) * a.istd[f][c] : x;
 }
 
 }  // namespace
 
-extern "C" int duck_gather_columns(int nf, const duck_gather_field* fields, const long long* idx, int m, void* stream) {
+extern "C" int duck_gather_columns_norm(int nf, const duck_gather_field* fields, const float* const* norm,
+                                        const long long* idx, int m, void* stream) {
     if (nf < 0 || nf > DUCK_GATHER_MAX || m < 0) return duck_fail(DUCK_EINVAL, "duck_gather_columns: bad field count or size");
     if (nf == 0 || m == 0) return DUCK_OK;
     if (!fields || !idx) return duck_fail(DUCK_EINVAL, "duck_gather_columns: null pointer");
@@ -307,12 +365,21 @@ extern "C" int duck_gather_columns(int nf, const duck_gather_field* fields, cons
             return duck_fail(DUCK_EINVAL, "duck_gather_columns: bad field");
         a.f[k] = f;
         a.start[k + 1] = a.start[k] + (long long)f.T * m * f.w;
+        if (norm) {
+            a.mean[k] = norm[2 * k];
+            a.istd[k] = norm[2 * k + 1];
+            if (!a.mean[k] != !a.istd[k]) return duck_fail(DUCK_EINVAL, "duck_gather_columns_norm: mean without istd");
+        }
     }
     const long long tot = a.start[nf];
     if (tot == 0) return DUCK_OK;
     hipLaunchKernelGGL(gather_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, nf, a, idx, m);
     HIPCHECK(hipGetLastError());
     return DUCK_OK;
+}
+
+extern "C" int duck_gather_columns(int nf, const duck_gather_field* fields, const long long* idx, int m, void* stream) {
+    return duck_gather_columns_norm(nf, fields, nullptr, idx, m, stream);
 }
 
 extern "C" int duck_gae(int T, int B, const float* truncation, const float* termination, const float* reward,
@@ -328,10 +395,47 @@ extern "C" int duck_gae(int T, int B, const float* truncation, const float* term
     return DUCK_OK;
 }
 
+extern "C" int duck_gae_stats(int T, int B, const float* truncation, const float* done, const float* reward,
+                              float reward_scale, const float* value, const float* bootstrap, float lambda_,
+                              float discount, float* vs, float* adv, int normalize_advantage, float* stats,
+                              void* stream) {
+    if (T <= 0 || B <= 0 || B > 1024) return duck_fail(DUCK_EINVAL, "duck_gae_stats: 1 <= B <= 1024 trajectories, T >= 1");
+    if (!truncation || !done || !reward || !value || !bootstrap || !vs || !adv || !stats)
+        return duck_fail(DUCK_EINVAL, "duck_gae_stats: null pointer");
+    const int tpb = ((B + 63) / 64) * 64;
+    hipLaunchKernelGGL(gae_stats_kernel, dim3(1), dim3(tpb), 0, (hipStream_t)stream, T, B, truncation, done, reward,
+                       reward_scale, value, bootstrap, lambda_, discount, vs, adv, normalize_advantage, stats);
+    HIPCHECK(hipGetLastError());
+    return DUCK_OK;
+}
+
+static int ppo_loss_launch(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
+                           const float* advantage, const float* value_target, const float* baseline,
+                           const float* eps, float clip_eps, float entropy_cost, int normalize_advantage,
+                           const float* stats_in, float* out, float* grad_logits, float* grad_baseline, void* stream);
+
 extern "C" int duck_ppo_loss(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
                              const float* advantage, const float* value_target, const float* baseline,
                              const float* eps, float clip_eps, float entropy_cost, int normalize_advantage,
                              float* out, float* grad_logits, float* grad_baseline, void* stream) {
+    return ppo_loss_launch(N, A, logits, raw_action, old_logprob, advantage, value_target, baseline, eps, clip_eps,
+                           entropy_cost, normalize_advantage, nullptr, out, grad_logits, grad_baseline, stream);
+}
+
+extern "C" int duck_ppo_loss_stats(int N, int A, const float* logits, const float* raw_action,
+                                   const float* old_logprob, const float* advantage, const float* value_target,
+                                   const float* baseline, const float* eps, float clip_eps, float entropy_cost,
+                                   const float* stats, float* out, float* grad_logits, float* grad_baseline,
+                                   void* stream) {
+    if (!stats) return duck_fail(DUCK_EINVAL, "duck_ppo_loss_stats: null stats");
+    return ppo_loss_launch(N, A, logits, raw_action, old_logprob, advantage, value_target, baseline, eps, clip_eps,
+                           entropy_cost, 1, stats, out, grad_logits, grad_baseline, stream);
+}
+
+static int ppo_loss_launch(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
+                           const float* advantage, const float* value_target, const float* baseline,
+                           const float* eps, float clip_eps, float entropy_cost, int normalize_advantage,
+                           const float* stats_in, float* out, float* grad_logits, float* grad_baseline, void* stream) {
     if (N <= 0 || A <= 0) return duck_fail(DUCK_EINVAL, "duck_ppo_loss: empty batch");
     const size_t lds = sizeof(float) * PPO_TPB * (4 * A + 3);
     if (lds > 64 * 1024) return duck_fail(DUCK_EINVAL, "duck_ppo_loss: action size too large");
@@ -345,7 +449,10 @@ extern "C" int duck_ppo_loss(int N, int A, const float* logits, const float* raw
     float* stats = out + 4;
     float* partial = out + 6;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(adv_stats_kernel, dim3(1), dim3(1024), 0, st, N, advantage, normalize_advantage, stats);
+    if (stats_in)  // computed by duck_gae_stats
+        stats = const_cast<float*>(stats_in);
+    else
+        hipLaunchKernelGGL(adv_stats_kernel, dim3(1), dim3(1024), 0, st, N, advantage, normalize_advantage, stats);
     if (team)
         hipLaunchKernelGGL(ppo_loss_team_kernel, dim3(nblk), dim3(256), 0, st, N, A, logits, raw_action, old_logprob,
                            advantage, value_target, baseline, eps, clip_eps, entropy_cost, stats, partial, grad_logits,

@@ -20,6 +20,7 @@ train.py; running_statistics.py) on torch tensors that never leave the GPU:
 
 from __future__ import annotations
 
+import ctypes as C
 import math
 import os
 import time
@@ -437,7 +438,18 @@ class FusedGrad:
     def _group(self, probs, stream):
         from .native import DuckMlpProblem, check
         arr = (DuckMlpProblem * len(probs))(*probs)
-        check(self.lib.duck_mlp_group(len(probs), arr, stream))
+        bn = self._tile_width(probs)
+        if bn != 32 and hasattr(self.lib, "duck_mlp_group_bn"):
+            check(self.lib.duck_mlp_group_bn(len(probs), arr, bn, stream))
+        else:
+            check(self.lib.duck_mlp_group(len(probs), arr, stream))
+
+    @staticmethod
+    def _tile_width(probs) -> int:
+        """Output tile width of a grouped launch (duck_mlp_group_bn; bit-identical either way). 32: with 64
+        every launch but the first layer's forward ran slower, and the whole update 1 % slower once the
+        normaliser moved into the gather (profiles/r06_ppo_learner.txt). DUCK_MLP_BN = 64 to try it."""
+        return 64 if os.environ.get("DUCK_MLP_BN", "32") == "64" else 32
 
     def _backward(self, layers, b, x, norm, dout, n, stream):
         from .native import check
@@ -475,8 +487,12 @@ class FusedGrad:
             torch.index_select(data["next_priv"][-1], 0, idx, out=self._xv[self.N:])
             return {**self._mb, "xv": self._xv}
         # every field in one duck_gather_columns launch (the rollout buffers and these are persistent,
-        # so the field table is built once; a captured learner graph replays the same pointers)
-        key = (tuple(v.data_ptr() for v in data.values()), idx.data_ptr())
+        # so the field table is built once; a captured learner graph replays the same pointers); with the
+        # observation normalisers applied on the way (duck_gather_columns_norm), so the first layers'
+        # GEMMs read plain rows
+        on, pn = (self.net.obs_norm, self.net.priv_norm) if self.net.normalize else (None, None)
+        pre = on is not None and hasattr(self.lib, "duck_gather_columns_norm")
+        key = (tuple(v.data_ptr() for v in data.values()), idx.data_ptr(), pre)
         if getattr(self, "_gkey", None) != key:
             fl = []
             for k, buf in self._mb.items():
@@ -490,10 +506,21 @@ class FusedGrad:
                     raise ValueError("duck_gather_columns needs contiguous float32 rollout buffers")
             self._gfields = (DuckGatherField * len(fl))(*[DuckGatherField(v.data_ptr(), d.data_ptr(), t, b, w)
                                                           for v, d, t, b, w in fl])
+            if pre:
+                names = list(self._mb) + ["priv", "next_priv"]
+                ptr = []
+                for k in names:
+                    nm = on if k == "obs" else (pn if k in ("priv", "next_priv") else None)
+                    ptr += [nm.mean32.data_ptr(), nm.istd32.data_ptr()] if nm is not None else [None, None]
+                self._gnorm = (C.c_void_p * len(ptr))(*ptr)
             self._gkey = key
         if idx.dtype != torch.int64:
             raise ValueError("minibatch indices must be int64")
         st = torch.cuda.current_stream(idx.device).cuda_stream
+        if pre:
+            check(self.lib.duck_gather_columns_norm(len(self._gfields), self._gfields, self._gnorm, idx.data_ptr(), mb,
+                                                    st))
+            return {**self._mb, "xv": self._xv, "normalized": True}
         check(self.lib.duck_gather_columns(len(self._gfields), self._gfields, idx.data_ptr(), mb, st))
         return {**self._mb, "xv": self._xv}
 
@@ -506,7 +533,8 @@ class FusedGrad:
         if N != self.N or self.Nv != N + B:
             raise ValueError(f"FusedGrad was sized for {self.N} rows, got {T} x {B}")
         st = torch.cuda.current_stream(self.flat.device).cuda_stream
-        on, pn = (net.obs_norm, net.priv_norm) if net.normalize else (None, None)
+        # (gather's rows may already be normalised: then the first layers take no op(X))
+        on, pn = (net.obs_norm, net.priv_norm) if net.normalize and not mb.get("normalized", False) else (None, None)
         obs = mb["obs"].reshape(N, -1)
         xv = mb["xv"] if "xv" in mb else torch.cat([mb["priv"].reshape(N, -1), mb["next_priv"][-1]], 0)
         grouped = hasattr(self.lib, "duck_mlp_group") and len(self.pol) == len(self.val)
@@ -519,17 +547,36 @@ class FusedGrad:
             logits = self._forward(self.pol, self.bp, obs, on, N, st)
             v_all = self._forward(self.val, self.bv, xv, pn, self.Nv, st).view(-1)
         baseline, bootstrap = v_all[:N].view(T, B), v_all[N:]
-        truncation = mb["truncation"]
-        termination = mb["done"] * (1.0 - truncation)
-        vs, adv = compute_gae(truncation, termination, mb["reward"] * cfg.reward_scaling, baseline, bootstrap,
-                              cfg.gae_lambda, cfg.discounting)
         A = logits.shape[-1] // 2
-        eps = torch.randn((T, B, A), device=logits.device, generator=gen)  # the entropy sample, as NormalTanh draws it
         ra, olp = mb["raw_action"].contiguous(), mb["log_prob"].contiguous()
-        check(self.lib.duck_ppo_loss(N, A, logits.data_ptr(), ra.data_ptr(), olp.data_ptr(), adv.data_ptr(),
-                                     vs.data_ptr(), baseline.data_ptr(), eps.data_ptr(), float(cfg.clipping_epsilon),
-                                     float(cfg.entropy_cost), int(bool(cfg.normalize_advantage)),
-                                     self.loss_out.data_ptr(), self.g_lg.data_ptr(), self.d_val.data_ptr(), st))
+        if hasattr(self.lib, "duck_gae_stats") and B <= 1024:
+            # GAE from the raw done / truncation / reward fields and the advantage statistics in one launch,
+            # the loss with those statistics (round 6: 2 launches instead of 7 per minibatch)
+            if getattr(self, "_vs", None) is None or self._vs.shape != (T, B):
+                self._vs = torch.empty(T, B, device=logits.device)
+                self._adv = torch.empty(T, B, device=logits.device)
+                self._stats = torch.empty(2, device=logits.device)
+            tr, dn, rw = (mb[k].contiguous() for k in ("truncation", "done", "reward"))
+            check(self.lib.duck_gae_stats(T, B, tr.data_ptr(), dn.data_ptr(), rw.data_ptr(), float(cfg.reward_scaling),
+                                          baseline.data_ptr(), bootstrap.data_ptr(), float(cfg.gae_lambda),
+                                          float(cfg.discounting), self._vs.data_ptr(), self._adv.data_ptr(),
+                                          int(bool(cfg.normalize_advantage)), self._stats.data_ptr(), st))
+            eps = torch.randn((T, B, A), device=logits.device, generator=gen)  # the entropy sample (NormalTanh)
+            check(self.lib.duck_ppo_loss_stats(N, A, logits.data_ptr(), ra.data_ptr(), olp.data_ptr(),
+                                               self._adv.data_ptr(), self._vs.data_ptr(), baseline.data_ptr(),
+                                               eps.data_ptr(), float(cfg.clipping_epsilon), float(cfg.entropy_cost),
+                                               self._stats.data_ptr(), self.loss_out.data_ptr(), self.g_lg.data_ptr(),
+                                               self.d_val.data_ptr(), st))
+        else:
+            truncation = mb["truncation"]
+            termination = mb["done"] * (1.0 - truncation)
+            vs, adv = compute_gae(truncation, termination, mb["reward"] * cfg.reward_scaling, baseline, bootstrap,
+                                  cfg.gae_lambda, cfg.discounting)
+            eps = torch.randn((T, B, A), device=logits.device, generator=gen)  # the entropy sample, as NormalTanh draws it
+            check(self.lib.duck_ppo_loss(N, A, logits.data_ptr(), ra.data_ptr(), olp.data_ptr(), adv.data_ptr(),
+                                         vs.data_ptr(), baseline.data_ptr(), eps.data_ptr(), float(cfg.clipping_epsilon),
+                                         float(cfg.entropy_cost), int(bool(cfg.normalize_advantage)),
+                                         self.loss_out.data_ptr(), self.g_lg.data_ptr(), self.d_val.data_ptr(), st))
         if grouped:
             for i in range(len(self.pol) - 1, -1, -1):
                 self._group(self._probs_bwd(self.pol, self.bp, obs, on, self.g_lg, N, i) +
@@ -614,10 +661,11 @@ class _Learner:
         self.g1 = self.g2 = None
         self.out = None
 
-    def _fwd_bwd(self):
+    def _fwd_bwd(self, idx: Optional[torch.Tensor] = None):
+        idx = self.idx if idx is None else idx
         if self.fused is not None:   # writes every .grad (views of one flat buffer)
-            return self.fused(self.fused.gather(self.data, self.idx), self.cfg, None)
-        mbatch = {k: v[:, self.idx] for k, v in self.data.items()}
+            return self.fused(self.fused.gather(self.data, idx), self.cfg, None)
+        mbatch = {k: v[:, idx] for k, v in self.data.items()}
         loss, m = ppo_loss(self.net, mbatch, self.cfg, None)
         # gradients set to None before the backward that is captured: it then writes them instead of
         # zero-filling and accumulating (one fill + one add kernel per parameter tensor saved)
@@ -659,6 +707,49 @@ class _Learner:
         allreduce_grads(self.params)
         self.g2.replay()
         return self.out
+
+    def _epoch_graph_ok(self) -> bool:
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        return self.use_graph and self.fused is not None and world == 1 and \
+            os.environ.get("DUCK_PPO_EPOCH_GRAPH", "1") != "0"
+
+    def epoch(self, perm: torch.Tensor, mb: int) -> Dict[str, torch.Tensor]:
+        """One pass over the shuffled batch: minibatch k takes perm[k mb : (k + 1) mb]. With one rank and
+        the fused learner the whole epoch -- every minibatch's gather, loss, backward, clip and Adam -- is
+        ONE captured graph reading its indices from a static permutation buffer, replayed per epoch (round
+        6: the per-minibatch replays cost a host round trip, an index copy, the generator-state fills of
+        each replay and the gap between the two graphs, ~30 us of a ~390 us minibatch,
+        profiles/r06_ppo_trace_summary_before.txt). Several ranks keep the per-minibatch graphs: the
+        gradient all-reduce runs between them."""
+        n = perm.numel() // mb
+        if not self._epoch_graph_ok():
+            out = None
+            for k in range(n):
+                out = self.step(perm[k * mb:(k + 1) * mb])
+            return out
+        if getattr(self, "eg", None) is None and self.calls < self.WARMUP:
+            # the first epoch runs eagerly on a side stream (real updates: torch's capture recipe)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for k in range(n):
+                    self.idx.copy_(perm[k * mb:(k + 1) * mb])
+                    out = self._fwd_bwd()
+                    self._apply()
+            torch.cuda.current_stream().wait_stream(s)
+            self.calls += n
+            return out
+        if getattr(self, "eg", None) is None:
+            self.perm_buf = torch.empty_like(perm)
+            self.eg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.eg):
+                for k in range(n):
+                    self.eout = self._fwd_bwd(self.perm_buf[k * mb:(k + 1) * mb])
+                    self._apply()
+        self.perm_buf.copy_(perm)
+        self.eg.replay()
+        self.calls += n
+        return self.eout
 
 
 class _Rollout:
@@ -863,8 +954,7 @@ def train(env, cfg: PPOConfig, progress_fn: Optional[Callable[[int, dict], None]
         # ---- learning: epochs x shuffled minibatches of whole trajectories ----
         for _ in range(cfg.num_updates_per_batch):
             perm = torch.randperm(B, device=device, generator=gen)
-            for i in range(0, B - mb + 1, mb):
-                last = learner.step(perm[i:i + mb])
+            last = learner.epoch(perm, mb)
         _sync()
         result.timing["learn_s"] += time.time() - t_learn
         result.env_steps += steps_per_update

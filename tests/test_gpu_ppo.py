@@ -99,6 +99,51 @@ def test_gae_kernel_matches_restatement(gpu, T, B):
     np.testing.assert_allclose(adv.cpu().numpy(), adv_n, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("T,B,normalize", [(20, 256, True), (7, 1000, True), (3, 5, False), (1, 1024, True)])
+def test_gae_stats_kernel_matches_torch(gpu, T, B, normalize):
+    """duck_gae_stats (one launch: termination = done (1 - truncation), reward scaling, GAE, the advantage
+    mean / 1 / (std + 1e-8)) against the torch expressions FusedGrad used and duck_gae, then
+    duck_ppo_loss_stats with those statistics against duck_ppo_loss computing its own."""
+    from open_duck_playground_amd.native import check, lib
+    L = lib()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=gpu).manual_seed(T * 7 + B)
+    r, v = torch.randn(T, B, device=gpu, generator=g), torch.randn(T, B, device=gpu, generator=g)
+    boot = torch.randn(B, device=gpu, generator=g)
+    done = (torch.rand(T, B, device=gpu, generator=g) < 0.1).float()
+    trunc = done * (torch.rand(T, B, device=gpu, generator=g) < 0.5).float()
+    vs_ref, adv_ref = ppo.compute_gae(trunc, done * (1.0 - trunc), r * 0.7, v, boot, 0.95, 0.97)
+    vs, adv, stats = torch.empty(T, B, device=gpu), torch.empty(T, B, device=gpu), torch.empty(2, device=gpu)
+    check(L.duck_gae_stats(T, B, trunc.data_ptr(), done.data_ptr(), r.data_ptr(), 0.7, v.data_ptr(), boot.data_ptr(),
+                           0.95, 0.97, vs.data_ptr(), adv.data_ptr(), int(normalize), stats.data_ptr(), st))
+    torch.cuda.synchronize()
+    assert torch.equal(vs, vs_ref) and torch.equal(adv, adv_ref)      # the same fp32 expressions, in order
+    a64 = adv_ref.double()
+    want = (a64.mean(), 1 / (a64.std(unbiased=False) + 1e-8)) if normalize else (0.0, 1.0)
+    assert abs(float(stats[0]) - float(want[0])) <= 1e-5 and abs(float(stats[1]) / float(want[1]) - 1) <= 1e-5
+    assert L.duck_gae_stats(T, 1025, trunc.data_ptr(), done.data_ptr(), r.data_ptr(), 0.7, v.data_ptr(),
+                            boot.data_ptr(), 0.95, 0.97, vs.data_ptr(), adv.data_ptr(), 1, stats.data_ptr(), st) < 0
+    if not normalize:
+        return
+    A, N = 14, T * B
+    logits, ra = torch.randn(N, 2 * A, device=gpu, generator=g), torch.randn(N, A, device=gpu, generator=g)
+    olp, base, eps = torch.randn(N, device=gpu, generator=g), torch.randn(N, device=gpu, generator=g), \
+        torch.randn(N, A, device=gpu, generator=g)
+    res = []
+    for fn in ("duck_ppo_loss", "duck_ppo_loss_stats"):
+        out = torch.empty(L.duck_ppo_loss_out_size(N), device=gpu)
+        gl, gb = torch.empty(N, 2 * A, device=gpu), torch.empty(N, device=gpu)
+        args = [N, A, logits.data_ptr(), ra.data_ptr(), olp.data_ptr(), adv.data_ptr(), vs.data_ptr(), base.data_ptr(),
+                eps.data_ptr(), 0.2, 0.005]
+        args += [1] if fn == "duck_ppo_loss" else [stats.data_ptr()]
+        check(getattr(L, fn)(*args, out.data_ptr(), gl.data_ptr(), gb.data_ptr(), st))
+        torch.cuda.synchronize()
+        res.append((out[:4].clone(), gl, gb))
+    (o0, g0, b0), (o1, g1, b1) = res
+    assert torch.allclose(o0, o1, rtol=1e-5, atol=1e-7) and torch.allclose(g0, g1, rtol=1e-4, atol=1e-9)
+    assert torch.equal(b0, b1)
+
+
 def test_runner_standing_env(gpu, tmp_path, monkeypatch):
     monkeypatch.chdir(tmp_path)
     monkeypatch.setattr(runner.BaseRunner, "make_ppo_params",
@@ -273,6 +318,7 @@ def test_clip_adam_matches_torch(gpu):
 def test_gather_columns_matches_index_select(gpu):
     """duck_gather_columns (one launch for every field of a minibatch) == torch.index_select per field,
     including a one-row field (the bootstrap observation) and a field of width 1."""
+    import ctypes
     import ctypes as C
     from open_duck_playground_amd.native import DuckGatherField, check, lib
     g = torch.Generator(device=gpu)
@@ -292,6 +338,18 @@ def test_gather_columns_matches_index_select(gpu):
         assert torch.equal(dst[k], torch.index_select(src[k], 1, idx)), k
     assert torch.equal(dst["np"], torch.index_select(src["np"][-1], 0, idx))
     assert lib().duck_gather_columns(9, arr, idx.data_ptr(), m, None) < 0
+    # duck_gather_columns_norm: fields 0 (obs) and 3 (the bootstrap row) through a normaliser, the rest copied
+    mo, io = torch.randn(101, device=gpu, generator=g), torch.rand(101, device=gpu, generator=g) + 0.5
+    mp, ip = torch.randn(172, device=gpu, generator=g), torch.rand(172, device=gpu, generator=g) + 0.5
+    norm = (ctypes.c_void_p * 8)(mo.data_ptr(), io.data_ptr(), None, None, None, None, mp.data_ptr(), ip.data_ptr())
+    for v in dst.values():
+        v.fill_(float("nan"))
+    check(lib().duck_gather_columns_norm(len(f), arr, norm, idx.data_ptr(), m, torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert torch.equal(dst["obs"], (torch.index_select(src["obs"], 1, idx) - mo) * io)
+    assert torch.equal(dst["np"], (torch.index_select(src["np"][-1], 0, idx) - mp) * ip)
+    for k in ("r", "a"):
+        assert torch.equal(dst[k], torch.index_select(src[k], 1, idx)), k
 
 
 def test_mlp_group_equals_separate_launches(gpu):
@@ -332,6 +390,17 @@ def test_mlp_group_equals_separate_launches(gpu):
             check(L.duck_mlp_group(3, (DuckMlpProblem * 3)(*probs), st))
         torch.cuda.synchronize()
         outs[how] = (Y, Y2, dX, part)
+        if how == "group":   # 64-wide output tiles: the same reduction order per element, the same bits
+            Y, Y2, dX = torch.empty(N, M, device=gpu), torch.empty(N, M, device=gpu), torch.empty(N, R, device=gpu)
+            part = torch.zeros(3 * P, device=gpu)
+            probs[0].Y, probs[0].Y2, probs[1].Y, probs[2].partial = Y.data_ptr(), Y2.data_ptr(), dX.data_ptr(), \
+                part.data_ptr()
+            check(L.duck_mlp_group_bn(3, (DuckMlpProblem * 3)(*probs), 64, st))
+            torch.cuda.synchronize()
+            outs["group64"] = (Y, Y2, dX, part)
+    for a, b in zip(outs["separate"], outs["group64"]):
+        assert torch.equal(a, b)
+    assert L.duck_mlp_group_bn(1, (DuckMlpProblem * 1)(probs[0]), 48, st) < 0
     for a, b in zip(outs["separate"], outs["group"]):
         assert torch.equal(a, b)
     assert L.duck_mlp_group(5, (DuckMlpProblem * 5)(), st) < 0
