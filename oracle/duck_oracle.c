@@ -1582,6 +1582,18 @@ void oracle_set_force_start(int mode) { g_force_start = mode; }
 static _Thread_local double g_start_costs[2];
 void oracle_last_start_costs(double out[2]) { out[0] = g_start_costs[0]; out[1] = g_start_costs[1]; }
 
+/* test aid (oracle_ls_trace, tools/ls_divergence.py): the iteration counts of this thread's line searches
+ * since the last reset, in call order (the first 4096 kept) */
+static _Thread_local int g_ls_hist[4096];
+static _Thread_local int g_ls_n;
+int oracle_ls_trace(int* out, int cap, int reset) {
+  const int n = g_ls_n < cap ? g_ls_n : cap;
+  if (out) memcpy(out, g_ls_hist, sizeof(int) * (size_t)(n < 4096 ? n : 4096));
+  const int tot = g_ls_n;
+  if (reset) g_ls_n = 0;
+  return tot;
+}
+
 static void linesearch(const oracle_model* m, const oracle_data* d, const fwd_ws* w, sctx* c) {
   int nv = m->nv;
   double snorm = 0;
@@ -1627,6 +1639,8 @@ static void linesearch(const oracle_model* m, const oracle_data* d, const fwd_ws
     swap = s1 || s2 || s3 || s4;
     iter++;
   }
+  if (g_ls_n < 4096) g_ls_hist[g_ls_n] = iter;
+  g_ls_n++;
   int improved = (lo.cost < p0.cost) || (hi.cost < p0.cost);
   double alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
   if (improved) {

@@ -121,6 +121,9 @@ int oracle_batch_reset(const oracle_model* const* models, int n_models, const du
                        const duck_refmotion* ref, int n_envs, uint64_t seed, int64_t env_offset,
                        double* fstate, int32_t* istate, double* obs, double* priv, int n_threads);
 
+/* test aid: iteration counts of this thread's line searches since the last reset (tools/ls_divergence.py) */
+int oracle_ls_trace(int* out, int cap, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,6 +82,7 @@ def lib():
                                       dp, C.POINTER(OracleData)]
         L.oracle_set_trace.argtypes = [dp]
         L.oracle_set_ls_floor.argtypes = [C.c_double]
+        L.oracle_ls_trace.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.oracle_set_force_start.argtypes = [C.c_int]
         L.oracle_set_hdump.argtypes = [dp]
         L.oracle_set_hf_band_scale.argtypes = [C.c_double]
