@@ -32,7 +32,10 @@
 
 namespace {
 
-constexpr int BM = 64;    // output tile rows (the batch rows for the forward / data-gradient GEMMs)
+#ifndef DUCK_MLP_BM
+#define DUCK_MLP_BM 64
+#endif
+constexpr int BM = DUCK_MLP_BM;  // output tile rows (the batch rows for the forward / data-gradient GEMMs)
 constexpr int BN = 32;    // output tile columns (duck_mlp_gemm / duck_mlp_wgrad; duck_mlp_group_bn takes 32 or 64)
 // reduction chunk. Deeper chunks mean fewer memory round trips per tile but more LDS per workgroup:
 // KC = 128 (49.5 KB, 3 workgroups per CU) made training 1.9 -> 1.2 M env-steps/s same-box against
