@@ -17,7 +17,7 @@
 // in flight during the current chunk's MFMAs; 12.7 KB of LDS and small tiles keep several
 // workgroups per CU resident, so one workgroup's load latency hides behind another's MFMAs (the
 // learner's GEMMs are 5120 rows deep and at most 512 wide: a 64 x 64 tile left ~1 workgroup per CU
-// and ran 3-4x slower). LDS rows padded to 33 floats.
+// and ran 3-4x slower). LDS tile layouts: see swz_word / tile_ksteps below.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -28,6 +28,11 @@
 
 #ifndef DUCK_MLP_KC
 #define DUCK_MLP_KC 32
+#endif
+// resident waves per SIMD the grouped 64 x 32-tile kernel is compiled for (6: 80 registers, no spills;
+// uncapped it takes 82 and holds 5)
+#ifndef DUCK_MLP_WPE
+#define DUCK_MLP_WPE 6
 #endif
 
 namespace {
@@ -41,9 +46,31 @@ constexpr int BN = 32;    // output tile columns (duck_mlp_gemm / duck_mlp_wgrad
 // KC = 128 (49.5 KB, 3 workgroups per CU) made training 1.9 -> 1.2 M env-steps/s same-box against
 // KC = 32 (12.7 KB): the resident workgroups hiding each other's load latency matter more
 constexpr int KC = DUCK_MLP_KC;
-constexpr int LDP = KC + 1;
 constexpr int KPT = KC / 8;  // reduction indices per thread of a row tile (8 threads cover a chunk row)
 using f4 = __attribute__((ext_vector_type(4))) float;
+
+// LDS tile layouts (round 6). An MFMA 16x16x4 k-step reads, per lane (li = l & 15, lk = l >> 4), element
+// (row li, k 4 s + lk) of each operand. With [row][k] rows padded to 33 words those ds_read_b32 met 2-way
+// bank conflicts in every 32-lane group, 24 of them per wave and chunk:
+//  * operands whose reduction index is contiguous in memory (RowTile: X, dZ, W's rows) are stored
+//    [row][lk][s] -- a lane's 8 k-steps of a chunk in 8 consecutive words, read as two ds_read_b128 -- with
+//    the 4-word blocks of row r XOR-swizzled by f(r) = (2 r + (r >> 3)) & 7 (r mod 16): conflict-free for
+//    the b128 reads' 16-lane groups and for the tile stores' ds_write_b32 (a search over swizzles);
+//  * operands whose reduction runs over their rows (ColTile: W in the data gradient, dZ and H in the
+//    weight gradient) are stored as they are loaded, [k][col] with rows padded to COLS + 16 words: one
+//    ds_write_b128 per loaded vector, and ds_read_b32 reads whose two 16-lane halves fall 16 banks apart.
+// Every lane feeds the MFMAs the same values in the same k order as before: bit-identical results.
+static_assert(KC == 32, "the tile layouts assume 32-deep reduction chunks");
+__device__ __forceinline__ int swz_word(int row, int k) {
+  const int kp = (k & 3) * 8 + (k >> 2), r = row & 15;
+  return row * KC + ((((kp >> 2) ^ ((2 * r + (r >> 3)) & 7))) << 2) + (kp & 3);
+}
+template <int COLS>
+constexpr int nat_ld() { return COLS + 16; }
+template <int ROWS, int COLS>
+constexpr int tile_words() {  // LDS words of a tile buffer that holds either layout
+  return ROWS * KC > KC * nat_ld<COLS>() ? ROWS * KC : KC * nat_ld<COLS>();
+}
 
 __device__ __forceinline__ float sigm(float z) { return 1.f / (1.f + __expf(-z)); }
 
@@ -97,13 +124,13 @@ struct RowTile {
         }
     }
   }
-  __device__ void store(float* S) const {  // S[row][k]
+  __device__ void store(float* S) const {  // the swizzled [row][lk][s] layout (swz_word)
     const int c = KPT * ((int)threadIdx.x & 7);
 #pragma unroll
     for (int p = 0; p < P; p++) {
       const int r = ((int)threadIdx.x >> 3) + 32 * p;
 #pragma unroll
-      for (int q = 0; q < KPT; q++) S[r * LDP + c + q] = v[KPT * p + q];
+      for (int q = 0; q < KPT; q++) S[swz_word(r, c + q)] = v[KPT * p + q];
     }
   }
 };
@@ -144,33 +171,48 @@ struct ColTile {
       }
     }
   }
-  __device__ void store(float* S) const {
+  __device__ void store(float* S) const {  // [k][col], rows of nat_ld<COLS>() words
     const int c = 4 * ((int)threadIdx.x % TPR);
 #pragma unroll
     for (int p = 0; p < P; p++) {
       const int r = (int)threadIdx.x / TPR + RSTEP * p;
-#pragma unroll
-      for (int q = 0; q < 4; q++) S[(c + q) * LDP + r] = v[4 * p + q];
+      *(f4*)(S + r * nat_ld<COLS>() + c) = f4{v[4 * p], v[4 * p + 1], v[4 * p + 2], v[4 * p + 3]};
     }
   }
 };
 
-// this wave's TI x TJ MFMA tiles over one LDS chunk: As[row][k], Bs[col][k]
-template <int TI, int TJ>
+// k-steps 4 h .. 4 h + 3 of a lane's row (or column) x of one operand tile: one ds_read_b128 from the
+// swizzled layout (SWZ, RowTile), or 4 ds_read_b32 from the [k][col] layout with rows of LD words (ColTile)
+template <bool SWZ, int LD>
+__device__ __forceinline__ f4 tile_ksteps(const float* S, int x, int lk, int h) {
+  if constexpr (SWZ) {
+    const int r = x & 15, f = (2 * r + (r >> 3)) & 7;
+    return *(const f4*)(S + x * KC + (((2 * lk + h) ^ f) << 2));
+  } else {
+    f4 o;
+#pragma unroll
+    for (int s = 0; s < 4; s++) o[s] = S[(4 * (4 * h + s) + lk) * LD + x];
+    return o;
+  }
+}
+
+// this wave's TI x TJ MFMA tiles over one LDS chunk (layouts: tile_ksteps), in two halves of 4 k-steps
+template <int TI, int TJ, bool ASWZ, int LDA, bool BSWZ, int LDB>
 __device__ __forceinline__ void mma_chunk(const float* As, const float* Bs, int wr, int wc, f4 (&acc)[TI][TJ]) {
   const int l = threadIdx.x & 63, li = l & 15, lk = l >> 4;
 #pragma unroll
-  for (int s = 0; s < KC / 4; s++) {
-    const int k = 4 * s + lk;
-    float a[TI], b[TJ];
+  for (int h = 0; h < 2; h++) {
+    f4 a[TI], b[TJ];
 #pragma unroll
-    for (int i = 0; i < TI; i++) a[i] = As[(wr + 16 * i + li) * LDP + k];
+    for (int i = 0; i < TI; i++) a[i] = tile_ksteps<ASWZ, LDA>(As, wr + 16 * i + li, lk, h);
 #pragma unroll
-    for (int j = 0; j < TJ; j++) b[j] = Bs[(wc + 16 * j + li) * LDP + k];
+    for (int j = 0; j < TJ; j++) b[j] = tile_ksteps<BSWZ, LDB>(Bs, wc + 16 * j + li, lk, h);
 #pragma unroll
-    for (int i = 0; i < TI; i++)
+    for (int s = 0; s < 4; s++)
 #pragma unroll
-      for (int j = 0; j < TJ; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < TI; i++)
+#pragma unroll
+        for (int j = 0; j < TJ; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
   }
 }
 
@@ -221,7 +263,7 @@ __device__ __forceinline__ void gemm_tile(int bx, int by, float* As, float* Bs, 
   __syncthreads();
   auto body = [&](int c, auto S, auto SN) {
     if (c + 2 < nch) load(S, KC * (c + 2));  // set S held chunk c (already in LDS)
-    mma_chunk<TI, TJ>(As, Bs, wr, wc, acc);
+    mma_chunk<TI, TJ, true, 0, MODE != 2, nat_ld<BNT>()>(As, Bs, wr, wc, acc);
     __syncthreads();
     if (c + 1 < nch) {
       store(SN);
@@ -266,7 +308,7 @@ __global__ __launch_bounds__(256) void mlp_gemm_kernel(int N, int R, int Mo, con
                                                        const float* __restrict__ aux, float* __restrict__ Y,
                                                        float* __restrict__ Y2, const float* __restrict__ mean,
                                                        const float* __restrict__ istd) {
-  __shared__ float As[BM * LDP], Bs[BN * LDP];
+  __shared__ __attribute__((aligned(16))) float As[tile_words<BM, BM>()], Bs[tile_words<BN, BN>()];
   gemm_tile<MODE>(blockIdx.x, blockIdx.y, As, Bs, N, R, Mo, A, W, bias, aux, Y, Y2, mean, istd);
 }
 
@@ -312,7 +354,7 @@ __device__ __forceinline__ void wgrad_tile(int bx, int by, int bz, float* As, fl
   __syncthreads();
   auto body = [&](int c, auto S, auto SN) {
     if (c + 2 < nch) load(S, KC * (c + 2));
-    mma_chunk<TI, TJ>(As, Bs, wr, wc, acc);
+    mma_chunk<TI, TJ, false, nat_ld<BM>(), false, nat_ld<BNT>()>(As, Bs, wr, wc, acc);
     __syncthreads();
     if (c + 1 < nch) {
       store(SN);
@@ -343,7 +385,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(int N, int Mo, int Ki, c
                                                         const float* __restrict__ H, const float* __restrict__ mean,
                                                         const float* __restrict__ istd, int rows_per_split,
                                                         float* __restrict__ part, int P, int offw, int offb) {
-  __shared__ float As[BM * LDP], Bs[BN * LDP];
+  __shared__ __attribute__((aligned(16))) float As[tile_words<BM, BM>()], Bs[tile_words<BN, BN>()];
   wgrad_tile(blockIdx.x, blockIdx.y, blockIdx.z, As, Bs, N, Mo, Ki, dZ, H, mean, istd, rows_per_split, part, P, offw,
              offb);
 }
@@ -359,8 +401,8 @@ struct MlpGroupArgs {
   duck_mlp_problem p[DUCK_MLP_GROUP_MAX];
 };
 template <int BNT>
-__global__ __launch_bounds__(256) void mlp_group_kernel(MlpGroupArgs g) {
-  __shared__ float As[BM * LDP], Bs[BNT * LDP];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNT == 32 ? DUCK_MLP_WPE : 1))) void mlp_group_kernel(MlpGroupArgs g) {
+  __shared__ __attribute__((aligned(16))) float As[tile_words<BM, BM>()], Bs[tile_words<BNT, BNT>()];
   const int b = blockIdx.x;
   int q = 0;
 #pragma unroll
