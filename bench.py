@@ -65,6 +65,12 @@ def _self_launch(argv) -> int:
     # the ranks' stdout is relayed line by line: the bench line to stdout, anything else the launcher or a
     # communication library writes there (gloo announces its peers) to stderr, so stdout holds one line
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    import signal
+
+    def _forward(sig, _frame):  # a time limit that stops this process stops the ranks too
+        p.send_signal(sig)
+    signal.signal(signal.SIGTERM, _forward)
+    signal.signal(signal.SIGINT, _forward)
     for line in p.stdout:
         k = line.find('{"metric"')
         if k > 0:
