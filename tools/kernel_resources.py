@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Register / LDS / scratch use of every step kernel in a HIP fat binary (CPU only): the code objects'
 AMDGPU metadata notes (.vgpr_count, .agpr_count, .sgpr_spill_count, .vgpr_spill_count,
-.private_segment_fixed_size, .group_segment_fixed_size). usage: python tools/kernel_resources.py [lib.so]"""
+.private_segment_fixed_size, .group_segment_fixed_size). usage: python tools/kernel_resources.py [lib.so] [name substring, default step_kernel]"""
 import os
 import re
 import subprocess
@@ -13,6 +13,7 @@ READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 
 
 def main():
+    match = sys.argv[2] if len(sys.argv) > 2 else "step_kernel"
     path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(__file__), "..", "open_duck_playground_amd", "libduck.so")
     with tempfile.TemporaryDirectory() as tmp:
         fat = os.path.join(tmp, "fat.bin")
@@ -31,7 +32,7 @@ def main():
             for blk in re.split(r"\n\s+- \.agpr_count", notes)[1:]:
                 blk = ".agpr_count" + blk
                 name = re.search(r"\.name:\s+(\S+)", blk)
-                if not name or "step_kernel" not in name.group(1):
+                if not name or match not in name.group(1):
                     continue
                 f = {k: re.search(rf"\.{k}:\s+(\S+)", blk) for k in
                      ("agpr_count", "vgpr_count", "sgpr_count", "vgpr_spill_count", "sgpr_spill_count",
