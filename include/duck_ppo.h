@@ -17,6 +17,14 @@
 extern "C" {
 #endif
 
+/* The batch moments of brax running_statistics.update (ppo.RunningStatistics.update; brax
+ * normalizes observations with it, the reference through ppo.train at common/runner.py:104-118):
+ * x [N][F] float32 row-major -> out[f] = sum_n x[n][f], out[F + f] = sum_n x[n][f]^2, in fp64, in a
+ * fixed order (two launches; the same bits on every run). scratch: duck_column_stats_scratch(N, F)
+ * doubles of device memory. (Round 6: torch's fp64 column reductions took 1.8 ms per call.) */
+int duck_column_stats(int N, int F, const float* x, double* out, double* scratch, void* stream);
+int duck_column_stats_scratch(int N, int F);
+
 /* vs[t][b], adv[t][b] from truncation/termination/reward/value [T][B] and bootstrap [B]:
  *   delta_t = (r_t + discount (1 - term_t) v_{t+1} - v_t)(1 - trunc_t),  v_T = bootstrap
  *   acc_t   = delta_t + discount (1 - term_t)(1 - trunc_t) lambda acc_{t+1},  vs_t = acc_t + v_t

@@ -349,7 +349,75 @@ __global__ __launch_bounds__(256) void gather_kernel(int nf, GatherArgs a, const
     a.f[f].dst[o] = a.mean[f] ? (x - a.mean[f][c]) * a.istd[f][c] : x;
 }
 
+// Column sums and sums of squares of a rollout batch x [N][F] in fp64 (brax running_statistics.update,
+// ppo.RunningStatistics). Pass 1: workgroup (rb, ct) takes rows rb * CS_ROWS .. + CS_ROWS - 1 of the 64
+// columns of tile ct; lane = column (one coalesced 256-B row segment per wave load), wave w every 4th row
+// from w; the 4 waves' sums combined in wave order. Pass 2: one thread per column sums the row blocks'
+// partials in order. Fixed order throughout: the same bits on every run.
+constexpr int CS_ROWS = 1024;
+__global__ __launch_bounds__(256) void column_stats_kernel(int N, int F, const float* __restrict__ x,
+                                                           double* __restrict__ part) {
+    __shared__ double red[2][4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.y * 64 + lane, r0 = blockIdx.x * CS_ROWS;
+    const int r1 = min(N, r0 + CS_ROWS);
+    double s = 0.0, q = 0.0;
+    if (c < F) {
+        int r = r0 + w;
+        // four rows in flight per iteration (independent loads, then the dependent sums in row order)
+        for (; r + 12 < r1; r += 16) {
+            const float a0 = x[(size_t)r * F + c], a1 = x[(size_t)(r + 4) * F + c];
+            const float a2 = x[(size_t)(r + 8) * F + c], a3 = x[(size_t)(r + 12) * F + c];
+            s += (double)a0; q += (double)a0 * (double)a0;
+            s += (double)a1; q += (double)a1 * (double)a1;
+            s += (double)a2; q += (double)a2 * (double)a2;
+            s += (double)a3; q += (double)a3 * (double)a3;
+        }
+        for (; r < r1; r += 4) {
+            const double a = (double)x[(size_t)r * F + c];
+            s += a; q += a * a;
+        }
+    }
+    red[0][w][lane] = s;
+    red[1][w][lane] = q;
+    __syncthreads();
+    if (w == 0 && c < F) {
+        const double ts = ((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane];
+        const double tq = ((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane];
+        part[(size_t)blockIdx.x * 2 * F + c] = ts;
+        part[(size_t)blockIdx.x * 2 * F + F + c] = tq;
+    }
+}
+__global__ __launch_bounds__(256) void column_stats_sum_kernel(int F, int nrb, const double* __restrict__ part,
+                                                               double* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;  // 0 .. 2F - 1: sums then squares
+    if (i >= 2 * F) return;
+    double t = 0.0;
+    for (int b = 0; b < nrb; b++) t += part[(size_t)b * 2 * F + i];
+    out[i] = t;
+}
+
 }  // namespace
+
+extern "C" int duck_column_stats_scratch(int N, int F) {
+    if (N <= 0 || F <= 0) return 0;
+    return ((N + CS_ROWS - 1) / CS_ROWS) * 2 * F;
+}
+
+extern "C" int duck_column_stats(int N, int F, const float* x, double* out, double* scratch, void* stream) {
+    if (N < 0 || F <= 0) return duck_fail(DUCK_EINVAL, "duck_column_stats: bad size");
+    if (!out || (N > 0 && (!x || !scratch))) return duck_fail(DUCK_EINVAL, "duck_column_stats: null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    if (N == 0) {
+        HIPCHECK(hipMemsetAsync(out, 0, sizeof(double) * 2 * (size_t)F, st));
+        return DUCK_OK;
+    }
+    const int nrb = (N + CS_ROWS - 1) / CS_ROWS;
+    hipLaunchKernelGGL(column_stats_kernel, dim3(nrb, (F + 63) / 64), dim3(256), 0, st, N, F, x, scratch);
+    hipLaunchKernelGGL(column_stats_sum_kernel, dim3((2 * F + 255) / 256), dim3(256), 0, st, F, nrb, scratch, out);
+    HIPCHECK(hipGetLastError());
+    return DUCK_OK;
+}
 
 extern "C" int duck_gather_columns_norm(int nf, const duck_gather_field* fields, const float* const* norm,
                                         const long long* idx, int m, void* stream) {

@@ -31,6 +31,25 @@ def main():
     for k in range(L):
         print(f"{k:3d} {dur[k] / n:8.2f} us  gap {gap[k] / n:6.2f} us  {seqs[0][k][2][:100]}")
     print(f"busy {sum(dur) / n:.1f} us, gaps {sum(gap) / n:.1f} us, span gather..last end {span:.1f} us per minibatch")
+    # idle time in front of every minibatch (inside an epoch graph, at epoch boundaries) and the
+    # longest idle stretches of the whole trace with the kernels around them
+    pre = sorted(((ev[i][0] - ev[i - 1][1]) / 1e3, i) for i in starts if i > 0)
+    if pre:
+        g = [x for x, _ in pre]
+        print(f"idle before a minibatch's gather: median {g[len(g) // 2]:.2f} us, max {g[-1]:.1f} us, "
+              f"sum {sum(g):.1f} us over {len(g)}")
+    idle = sorted((((ev[i][0] - ev[i - 1][1]) / 1e3, i) for i in range(1, len(ev))), reverse=True)[:12]
+    for x, i in idle:
+        print(f"  idle {x:9.1f} us  after {ev[i - 1][2][:60]}  before {ev[i][2][:60]}")
+    agg = defaultdict(lambda: [0, 0.0])
+    for a, b, k in ev:
+        agg[k[:70]][0] += 1
+        agg[k[:70]][1] += (b - a) / 1e3
+    print("busiest kernels of the trace (count, total us):")
+    for k, (c, t) in sorted(agg.items(), key=lambda x: -x[1][1])[:25]:
+        print(f"  {c:6d} {t:10.1f}  {k}")
+    print(f"trace: {len(ev)} dispatches over {(ev[-1][1] - ev[0][0]) / 1e6:.2f} ms, busy "
+          f"{sum(b - a for a, b, _ in ev) / 1e6:.2f} ms")
 
 
 if __name__ == "__main__":
