@@ -61,6 +61,15 @@ int duck_ppo_loss_stats(int N, int A, const float* logits, const float* raw_acti
                         const float* advantage, const float* value_target, const float* baseline, const float* eps,
                         float clip_eps, float entropy_cost, const float* stats, float* out, float* grad_logits,
                         float* grad_baseline, void* stream);
+/* duck_ppo_loss_stats without the loss sums (A <= 16): the gradients and the per-workgroup partial sums
+ * only; duck_ppo_loss_sums(N, A, entropy_cost, out) forms out[0..3] from the partials the last call left
+ * in out. The learner's epoch graph reports the last minibatch's loss only: one launch fewer for the
+ * others. (Round 6.) */
+int duck_ppo_loss_grad(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
+                       const float* advantage, const float* value_target, const float* baseline, const float* eps,
+                       float clip_eps, float entropy_cost, const float* stats, float* out, float* grad_logits,
+                       float* grad_baseline, void* stream);
+int duck_ppo_loss_sums(int N, int A, float entropy_cost, float* out, void* stream);
 /* 4 + 2 + 3 ceil(N / 16): the length of duck_ppo_loss's out array (A <= 31) */
 int duck_ppo_loss_out_size(int N);
 
@@ -132,6 +141,12 @@ int duck_policy_sample(int N, int A, const float* logits, unsigned long long see
 int duck_clip_adam(int P, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float* scratch,
                    int* step, float lr, float beta1, float beta2, float eps, float max_norm, void* stream);
 int duck_clip_adam_scratch_size(int P);
+/* duck_mlp_wgrad_reduce(P, splits, partial, grad) and duck_clip_adam in two launches instead of three
+ * (one rank: no gradient all-reduce between them): grad is written as duck_mlp_wgrad_reduce writes it and
+ * the update is bit-identical. (Round 6.) */
+int duck_clip_adam_reduce(int P, int splits, const float* partial, float* param, float* grad, float* exp_avg,
+                          float* exp_avg_sq, float* scratch, int* step, float lr, float beta1, float beta2, float eps,
+                          float max_norm, void* stream);
 
 #ifdef __cplusplus
 }

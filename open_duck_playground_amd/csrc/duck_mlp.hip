@@ -503,6 +503,47 @@ __global__ __launch_bounds__(ADAM_TPB) void adam_norm_kernel(int P, const float*
   }
 }
 
+// Launch 1 with the split-K weight-gradient partials summed first (duck_clip_adam_reduce, one rank): each
+// thread forms its 8 gradient entries as duck_mlp_wgrad_reduce does (splits in order), stores them and
+// sums their squares in adam_norm_kernel's order -- the same gradient and the same norm, one launch fewer.
+__global__ __launch_bounds__(ADAM_TPB) void adam_reduce_norm_kernel(int P, int S, const float* __restrict__ part,
+                                                                    float* __restrict__ g,
+                                                                    float* __restrict__ partial,
+                                                                    int* __restrict__ step) {
+  __shared__ float red[ADAM_TPB / 64];
+  const int base = blockIdx.x * ADAM_TPB * ADAM_PER;
+  // (the 8 entries' sums side by side, split s outer: 8 independent loads per split in flight; each
+  // entry still sums its splits in order)
+  float gi[ADAM_PER];
+#pragma unroll
+  for (int j = 0; j < ADAM_PER; j++) gi[j] = 0.f;
+  for (int s = 0; s < S; s++) {
+    const float* ps = part + (size_t)s * P;
+#pragma unroll
+    for (int j = 0; j < ADAM_PER; j++) {
+      const int i = base + j * ADAM_TPB + threadIdx.x;
+      gi[j] += i < P ? ps[i] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < ADAM_PER; j++) {
+    const int i = base + j * ADAM_TPB + threadIdx.x;
+    if (i < P) g[i] = gi[j];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < ADAM_PER; j++) s += gi[j] * gi[j];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < ADAM_TPB / 64; w++) t += red[w];
+    partial[blockIdx.x] = t;
+    if (blockIdx.x == 0) *step += 1;
+  }
+}
+
 __global__ __launch_bounds__(ADAM_TPB) void adam_update_kernel(int P, int nblk, float* __restrict__ p,
                                                                const float* __restrict__ g, float* __restrict__ m,
                                                                float* __restrict__ v, const float* __restrict__ partial,
@@ -667,6 +708,22 @@ extern "C" int duck_clip_adam(int P, float* param, const float* grad, float* exp
   const int nblk = (P + ADAM_TPB * ADAM_PER - 1) / (ADAM_TPB * ADAM_PER);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(adam_norm_kernel, dim3(nblk), dim3(ADAM_TPB), 0, st, P, grad, scratch, step);
+  hipLaunchKernelGGL(adam_update_kernel, dim3(nblk), dim3(ADAM_TPB), 0, st, P, nblk, param, grad, exp_avg, exp_avg_sq,
+                     scratch, step, lr, beta1, beta2, eps, max_norm);
+  HIPCHECK(hipGetLastError());
+  return DUCK_OK;
+}
+
+extern "C" int duck_clip_adam_reduce(int P, int splits, const float* partial, float* param, float* grad,
+                                     float* exp_avg, float* exp_avg_sq, float* scratch, int* step, float lr,
+                                     float beta1, float beta2, float eps, float max_norm, void* stream) {
+  if (P <= 0 || splits <= 0) return duck_fail(DUCK_EINVAL, "duck_clip_adam_reduce: bad size");
+  if (!partial || !param || !grad || !exp_avg || !exp_avg_sq || !scratch || !step)
+    return duck_fail(DUCK_EINVAL, "duck_clip_adam_reduce: null pointer");
+  const int nblk = (P + ADAM_TPB * ADAM_PER - 1) / (ADAM_TPB * ADAM_PER);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adam_reduce_norm_kernel, dim3(nblk), dim3(ADAM_TPB), 0, st, P, splits, partial, grad, scratch,
+                     step);
   hipLaunchKernelGGL(adam_update_kernel, dim3(nblk), dim3(ADAM_TPB), 0, st, P, nblk, param, grad, exp_avg, exp_avg_sq,
                      scratch, step, lr, beta1, beta2, eps, max_norm);
   HIPCHECK(hipGetLastError());

@@ -480,7 +480,8 @@ extern "C" int duck_gae_stats(int T, int B, const float* truncation, const float
 static int ppo_loss_launch(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
                            const float* advantage, const float* value_target, const float* baseline,
                            const float* eps, float clip_eps, float entropy_cost, int normalize_advantage,
-                           const float* stats_in, float* out, float* grad_logits, float* grad_baseline, void* stream);
+                           const float* stats_in, float* out, float* grad_logits, float* grad_baseline, void* stream,
+                           bool sums = true);
 
 extern "C" int duck_ppo_loss(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
                              const float* advantage, const float* value_target, const float* baseline,
@@ -503,7 +504,8 @@ extern "C" int duck_ppo_loss_stats(int N, int A, const float* logits, const floa
 static int ppo_loss_launch(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
                            const float* advantage, const float* value_target, const float* baseline,
                            const float* eps, float clip_eps, float entropy_cost, int normalize_advantage,
-                           const float* stats_in, float* out, float* grad_logits, float* grad_baseline, void* stream) {
+                           const float* stats_in, float* out, float* grad_logits, float* grad_baseline, void* stream,
+                           bool sums) {
     if (N <= 0 || A <= 0) return duck_fail(DUCK_EINVAL, "duck_ppo_loss: empty batch");
     const size_t lds = sizeof(float) * PPO_TPB * (4 * A + 3);
     if (lds > 64 * 1024) return duck_fail(DUCK_EINVAL, "duck_ppo_loss: action size too large");
@@ -529,7 +531,27 @@ static int ppo_loss_launch(int N, int A, const float* logits, const float* raw_a
         hipLaunchKernelGGL(ppo_loss_kernel, dim3(nblk), dim3(PPO_TPB), lds, st, N, A, logits, raw_action, old_logprob,
                            advantage, value_target, baseline, eps, clip_eps, entropy_cost, stats, partial, grad_logits,
                            grad_baseline);
-    hipLaunchKernelGGL(ppo_loss_sum_kernel, dim3(1), dim3(1024), 0, st, N, nblk, partial, entropy_cost, out);
+    if (sums) hipLaunchKernelGGL(ppo_loss_sum_kernel, dim3(1), dim3(1024), 0, st, N, nblk, partial, entropy_cost, out);
+    HIPCHECK(hipGetLastError());
+    return DUCK_OK;
+}
+
+extern "C" int duck_ppo_loss_grad(int N, int A, const float* logits, const float* raw_action, const float* old_logprob,
+                                  const float* advantage, const float* value_target, const float* baseline,
+                                  const float* eps, float clip_eps, float entropy_cost, const float* stats, float* out,
+                                  float* grad_logits, float* grad_baseline, void* stream) {
+    if (!stats) return duck_fail(DUCK_EINVAL, "duck_ppo_loss_grad: null stats");
+    if (A > 16) return duck_fail(DUCK_EINVAL, "duck_ppo_loss_grad: action size above 16");
+    return ppo_loss_launch(N, A, logits, raw_action, old_logprob, advantage, value_target, baseline, eps, clip_eps,
+                           entropy_cost, 1, stats, out, grad_logits, grad_baseline, stream, false);
+}
+
+extern "C" int duck_ppo_loss_sums(int N, int A, float entropy_cost, float* out, void* stream) {
+    if (N <= 0 || A <= 0 || A > 16) return duck_fail(DUCK_EINVAL, "duck_ppo_loss_sums: bad size");
+    if (!out) return duck_fail(DUCK_EINVAL, "duck_ppo_loss_sums: null pointer");
+    const int nblk = (N + PPO_SPW - 1) / PPO_SPW;
+    hipLaunchKernelGGL(ppo_loss_sum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, N, nblk, out + 6,
+                       entropy_cost, out);
     HIPCHECK(hipGetLastError());
     return DUCK_OK;
 }

@@ -26,7 +26,8 @@ EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get"
            "duck_policy_sample", "duck_clip_adam", "duck_clip_adam_scratch_size", "duck_set_step_mode",
            "duck_step_kernel_for", "duck_debug_lat_timeouts", "duck_gather_columns", "duck_mlp_group",
            "duck_device_error", "duck_gae_stats", "duck_ppo_loss_stats", "duck_mlp_group_bn", "duck_gather_columns_norm",
-           "duck_column_stats", "duck_column_stats_scratch"]
+           "duck_column_stats", "duck_column_stats_scratch", "duck_clip_adam_reduce", "duck_ppo_loss_grad",
+           "duck_ppo_loss_sums"]
 
 
 class DuckMlpProblem(C.Structure):
@@ -300,6 +301,12 @@ def lib(path: str = None):
         if hasattr(L, "duck_gather_columns_norm"):
             L.duck_gather_columns_norm.argtypes = [C.c_int, C.POINTER(DuckGatherField), C.POINTER(C.c_void_p), vp,
                                                    C.c_int, vp]
+        if hasattr(L, "duck_clip_adam_reduce"):
+            L.duck_clip_adam_reduce.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_float,
+                                                C.c_float, C.c_float, C.c_float, vp]
+            L.duck_ppo_loss_grad.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_float, vp,
+                                             vp, vp, vp, vp]
+            L.duck_ppo_loss_sums.argtypes = [C.c_int, C.c_int, C.c_float, vp, vp]
         if hasattr(L, "duck_column_stats"):
             L.duck_column_stats.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp]
             L.duck_column_stats_scratch.argtypes = [C.c_int, C.c_int]

@@ -394,6 +394,9 @@ class FusedGrad:
         self.adam_scratch = torch.zeros(self.lib.duck_clip_adam_scratch_size(self.P), device=device)
         # zeroed once: a layer that uses fewer row blocks than SPLITS leaves its other partials at 0
         self.part = torch.zeros(self.SPLITS * self.P, device=device)
+        # one rank (set by _Learner): the weight-gradient partials are summed by the update's first launch
+        # (duck_clip_adam_reduce) instead of a duck_mlp_wgrad_reduce launch of their own
+        self.defer_reduce = False
         self.pol = [m for m in net.policy if isinstance(m, nn.Linear)]
         self.val = [m for m in net.value if isinstance(m, nn.Linear)]
         self.N, self.Nv = rows, rows + boot_rows
@@ -542,7 +545,8 @@ class FusedGrad:
         check(self.lib.duck_gather_columns(len(self._gfields), self._gfields, idx.data_ptr(), mb, st))
         return {**self._mb, "xv": self._xv}
 
-    def __call__(self, mb: Dict[str, torch.Tensor], cfg: PPOConfig, gen: Optional[torch.Generator]):
+    def __call__(self, mb: Dict[str, torch.Tensor], cfg: PPOConfig, gen: Optional[torch.Generator],
+                 metrics: bool = True):
         """mb: the minibatch [T, B, ...] (gather's output, or any dict with obs, priv, next_priv, ...)"""
         from .native import check
         net = self.net
@@ -580,7 +584,10 @@ class FusedGrad:
                                           float(cfg.discounting), self._vs.data_ptr(), self._adv.data_ptr(),
                                           int(bool(cfg.normalize_advantage)), self._stats.data_ptr(), st))
             eps = torch.randn((T, B, A), device=logits.device, generator=gen)  # the entropy sample (NormalTanh)
-            check(self.lib.duck_ppo_loss_stats(N, A, logits.data_ptr(), ra.data_ptr(), olp.data_ptr(),
+            # (metrics=False: the gradients without the loss sums, which only the reported minibatch needs)
+            loss_fn = self.lib.duck_ppo_loss_stats if metrics or A > 16 or not hasattr(self.lib, "duck_ppo_loss_grad") \
+                else self.lib.duck_ppo_loss_grad
+            check(loss_fn(N, A, logits.data_ptr(), ra.data_ptr(), olp.data_ptr(),
                                                self._adv.data_ptr(), self._vs.data_ptr(), baseline.data_ptr(),
                                                eps.data_ptr(), float(cfg.clipping_epsilon), float(cfg.entropy_cost),
                                                self._stats.data_ptr(), self.loss_out.data_ptr(), self.g_lg.data_ptr(),
@@ -602,7 +609,8 @@ class FusedGrad:
         else:
             self._backward(self.pol, self.bp, obs, on, self.g_lg, N, st)
             self._backward(self.val, self.bv, xv, pn, self.d_val, self.Nv, st)
-        check(self.lib.duck_mlp_wgrad_reduce(self.P, self.SPLITS, self.part.data_ptr(), self.flat.data_ptr(), st))
+        if not self.defer_reduce:
+            check(self.lib.duck_mlp_wgrad_reduce(self.P, self.SPLITS, self.part.data_ptr(), self.flat.data_ptr(), st))
         o = self.loss_out
         return {"loss": o[0], "policy_loss": o[1], "v_loss": o[2], "entropy": o[3]}
 
@@ -611,6 +619,12 @@ def _fused_update(fg: "FusedGrad", cfg: PPOConfig) -> None:
     """clip_grad_norm_(max_grad_norm) + Adam(learning_rate) on FusedGrad's flat buffers (duck_clip_adam)"""
     from .native import check
     st = torch.cuda.current_stream(fg.flat.device).cuda_stream
+    if fg.defer_reduce:  # the weight-gradient partials summed into fg.flat by the first launch
+        check(fg.lib.duck_clip_adam_reduce(fg.P, fg.SPLITS, fg.part.data_ptr(), fg.pflat.data_ptr(), fg.flat.data_ptr(),
+                                           fg.exp_avg.data_ptr(), fg.exp_avg_sq.data_ptr(), fg.adam_scratch.data_ptr(),
+                                           fg.adam_step.data_ptr(), float(cfg.learning_rate), 0.9, 0.999, 1e-8,
+                                           float(cfg.max_grad_norm or 0.0), st))
+        return
     check(fg.lib.duck_clip_adam(fg.P, fg.pflat.data_ptr(), fg.flat.data_ptr(), fg.exp_avg.data_ptr(),
                                 fg.exp_avg_sq.data_ptr(), fg.adam_scratch.data_ptr(), fg.adam_step.data_ptr(),
                                 float(cfg.learning_rate), 0.9, 0.999, 1e-8, float(cfg.max_grad_norm or 0.0), st))
@@ -673,16 +687,19 @@ class _Learner:
             fused_mlp = fused_grad_available(device)
         T = cfg.unroll_length
         self.fused = FusedGrad(net, T * mb, mb, device) if fused_mlp else None
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        if self.fused is not None and world == 1 and hasattr(self.fused.lib, "duck_clip_adam_reduce"):
+            self.fused.defer_reduce = True   # no all-reduce between the backward and the update
         self.idx = torch.zeros(mb, dtype=torch.long, device=device)
         self.use_graph = use_graph
         self.calls = 0
         self.g1 = self.g2 = None
         self.out = None
 
-    def _fwd_bwd(self, idx: Optional[torch.Tensor] = None):
+    def _fwd_bwd(self, idx: Optional[torch.Tensor] = None, metrics: bool = True):
         idx = self.idx if idx is None else idx
         if self.fused is not None:   # writes every .grad (views of one flat buffer)
-            return self.fused(self.fused.gather(self.data, idx), self.cfg, None)
+            return self.fused(self.fused.gather(self.data, idx), self.cfg, None, metrics)
         mbatch = {k: v[:, idx] for k, v in self.data.items()}
         loss, m = ppo_loss(self.net, mbatch, self.cfg, None)
         # gradients set to None before the backward that is captured: it then writes them instead of
@@ -762,7 +779,8 @@ class _Learner:
             self.eg = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.eg):
                 for k in range(n):
-                    self.eout = self._fwd_bwd(self.perm_buf[k * mb:(k + 1) * mb])
+                    # (the loss sums of the epoch's last minibatch only: the others' are never read)
+                    self.eout = self._fwd_bwd(self.perm_buf[k * mb:(k + 1) * mb], metrics=k == n - 1)
                     self._apply()
         self.perm_buf.copy_(perm)
         self.eg.replay()

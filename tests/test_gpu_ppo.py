@@ -348,6 +348,69 @@ def test_clip_adam_matches_torch(gpu):
         assert err <= 1e-6, (scale, err)
 
 
+def test_clip_adam_reduce_equals_reduce_then_clip_adam(gpu):
+    """duck_clip_adam_reduce (the weight-gradient partials summed by the update's first launch, one rank)
+    gives the same bits as duck_mlp_wgrad_reduce + duck_clip_adam: gradient, moments, parameters, step."""
+    from open_duck_playground_amd.native import check, lib
+    L = lib()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=gpu).manual_seed(11)
+    P, S = 300_001, 8
+    p0 = torch.randn(P, device=gpu, generator=g)
+    runs = []
+    for fused in (False, True):
+        p, grad = p0.clone(), torch.zeros(P, device=gpu)
+        m, v = torch.zeros(P, device=gpu), torch.zeros(P, device=gpu)
+        step = torch.zeros(1, dtype=torch.int32, device=gpu)
+        scratch = torch.zeros(L.duck_clip_adam_scratch_size(P), device=gpu)
+        g.manual_seed(12)
+        for k in range(4):
+            part = torch.randn(S * P, device=gpu, generator=g) * (3.0 if k % 2 else 1e-3)
+            if fused:
+                check(L.duck_clip_adam_reduce(P, S, part.data_ptr(), p.data_ptr(), grad.data_ptr(), m.data_ptr(),
+                                              v.data_ptr(), scratch.data_ptr(), step.data_ptr(), 3e-4, 0.9, 0.999,
+                                              1e-8, 1.0, st))
+            else:
+                check(L.duck_mlp_wgrad_reduce(P, S, part.data_ptr(), grad.data_ptr(), st))
+                check(L.duck_clip_adam(P, p.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                       scratch.data_ptr(), step.data_ptr(), 3e-4, 0.9, 0.999, 1e-8, 1.0, st))
+        torch.cuda.synchronize()
+        runs.append((p, grad, m, v, step))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+    assert L.duck_clip_adam_reduce(P, 0, part.data_ptr(), p.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                   scratch.data_ptr(), step.data_ptr(), 3e-4, 0.9, 0.999, 1e-8, 1.0, st) < 0
+
+
+def test_ppo_loss_grad_then_sums_equals_loss_stats(gpu):
+    """duck_ppo_loss_grad (gradients and partial sums, no loss sums) + duck_ppo_loss_sums == duck_ppo_loss_stats,
+    bit for bit: the learner's epoch graph skips the sums for every minibatch but the reported one."""
+    from open_duck_playground_amd.native import check, lib
+    L = lib()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=gpu).manual_seed(5)
+    N, A = 5120, 14
+    ins = [torch.randn(N, 2 * A, device=gpu, generator=g), torch.randn(N, A, device=gpu, generator=g)] + \
+        [torch.randn(N, device=gpu, generator=g) for _ in range(4)] + [torch.randn(N, A, device=gpu, generator=g)]
+    stats = torch.tensor([0.1, 1.3], device=gpu)
+    res = []
+    for split in (False, True):
+        out = torch.empty(L.duck_ppo_loss_out_size(N), device=gpu)
+        gl, gb = torch.empty(N, 2 * A, device=gpu), torch.empty(N, device=gpu)
+        args = [N, A] + [t.data_ptr() for t in ins] + [0.2, 0.005, stats.data_ptr(), out.data_ptr(), gl.data_ptr(),
+                                                       gb.data_ptr(), st]
+        if split:
+            check(L.duck_ppo_loss_grad(*args))
+            check(L.duck_ppo_loss_sums(N, A, 0.005, out.data_ptr(), st))
+        else:
+            check(L.duck_ppo_loss_stats(*args))
+        torch.cuda.synchronize()
+        res.append((out[:4].clone(), gl, gb))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert L.duck_ppo_loss_sums(N, 17, 0.005, out.data_ptr(), st) < 0
+
+
 def test_gather_columns_matches_index_select(gpu):
     """duck_gather_columns (one launch for every field of a minibatch) == torch.index_select per field,
     including a one-row field (the bootstrap observation) and a field of width 1."""
