@@ -6,7 +6,7 @@
 set -o pipefail
 TAG=${1:-r02}
 CFG=${2:-C2}
-OUT=gpurun_out/pmc_$TAG
+OUT=gpurun_out/pmc_${TAG}_$CFG
 export TMPDIR=/tmp
 rm -rf $OUT; mkdir -p $OUT
 B="python3 bench.py --config $CFG --cpu-budget 0"
