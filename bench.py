@@ -114,8 +114,12 @@ VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12
 VALU_MEASURED_PEAK_TLANE = 55.74     # 8 waves per SIMD
 VALU_ONE_WAVE_TLANE = 29.12          # 1 wave per SIMD
 # newest tools/gpu_pmc.sh <rNN> C2 summary; only used when its build id matches the loaded library
-PMC_PROFILE = (sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_c2.json")))
-               or [os.path.join(ROOT, "profiles", "r02_pmc_c2.json")])[-1]
+def pmc_profile(config: str) -> str:
+    """the newest committed rocprofv3 summary of a configuration (tools/gpu_pmc.sh), or a path that
+    does not exist"""
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_pmc_{config.lower()}.json")))
+    return found[-1] if found else os.path.join(ROOT, "profiles", f"r00_pmc_{config.lower()}.json")
+
 
 # BASELINE.json configs[1..4] (configs[0] is the reference's 1-env CPU plumbing case)
 CONFIGS = {
@@ -314,10 +318,11 @@ def main():
     # PMC numbers of the committed rocprofv3 run of this configuration (tools/gpu_pmc.sh); valid
     # only for the library they were measured on
     traffic, issue_rf = None, None
-    if os.path.exists(PMC_PROFILE) and args.config == "C2" and n == CONFIGS["C2"]["envs"]:
-        prof = json.load(open(PMC_PROFILE))
+    pmc = pmc_profile(args.config)
+    if os.path.exists(pmc) and n == CONFIGS[args.config]["envs"]:
+        prof = json.load(open(pmc))
         current = prof.get("build_id") == build_id()
-        src = {"source": os.path.relpath(PMC_PROFILE, ROOT), "build_id_matches": current}
+        src = {"source": os.path.relpath(pmc, ROOT), "build_id_matches": current}
         if current:
             traffic = prof["hbm_bytes_per_launch"]
             valu = prof["SQ_INSTS_VALU"] * 64 / (kern_ms * 1e-3) / 1e12     # lane-instructions / s
