@@ -99,7 +99,8 @@ def test_gae_kernel_matches_restatement(gpu, T, B):
     np.testing.assert_allclose(adv.cpu().numpy(), adv_n, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("T,B,normalize", [(20, 256, True), (7, 1000, True), (3, 5, False), (1, 1024, True)])
+@pytest.mark.parametrize("T,B,normalize", [(20, 256, True), (7, 1000, True), (3, 5, False), (1, 1024, True),
+                                              (24, 256, True), (25, 256, False)])
 def test_gae_stats_kernel_matches_torch(gpu, T, B, normalize):
     """duck_gae_stats (one launch: termination = done (1 - truncation), reward scaling, GAE, the advantage
     mean / 1 / (std + 1e-8)) against the torch expressions FusedGrad used and duck_gae, then
