@@ -828,26 +828,54 @@ class _Rollout:
                 inp = self.H[i]
         return self.logits
 
+    def _store(self, pairs, st) -> None:
+        """Rows [n, ...] into rows of the time-major buffers: every (source, destination) pair in one
+        duck_gather_columns launch with the identity index (one launch per env-step instead of six
+        copies); a pair that is not two contiguous float32 tensors is copied by torch."""
+        from .native import DuckGatherField, check
+        n = self.n
+        if getattr(self, "_ident", None) is None:
+            self._ident = torch.arange(n, dtype=torch.int64, device=self.logits.device)
+        ok = [(a, b) for a, b in pairs if a.dtype == b.dtype == torch.float32 and a.is_contiguous()
+              and b.is_contiguous() and a.numel() == b.numel() and a.numel() % n == 0]
+        for a, b in pairs:
+            if not any(a is x and b is y for x, y in ok):
+                b.copy_(a)
+        if not ok:
+            return
+        if not hasattr(self.lib, "duck_gather_columns"):
+            for a, b in ok:
+                b.copy_(a)
+            return
+        fl = (DuckGatherField * len(ok))(*[DuckGatherField(a.data_ptr(), b.data_ptr(), 1, n, a.numel() // n)
+                                           for a, b in ok])
+        check(self.lib.duck_gather_columns(len(ok), fl, self._ident.data_ptr(), n, st))
+
     def _unroll(self, state):
         from .native import check
         cfg, data, n = self.cfg, self.data, self.n
         st = torch.cuda.current_stream(self.logits.device).cuda_stream
         A = self.action.shape[1]
+        pk, vk, T = cfg.policy_obs_key, cfg.value_obs_key, cfg.unroll_length
         for u in range(self.unrolls):
             cols = slice(u * n, (u + 1) * n)
-            for t in range(cfg.unroll_length):
-                obs, priv = state.obs[cfg.policy_obs_key], state.obs[cfg.value_obs_key]
-                data["obs"][t, cols] = obs
-                data["priv"][t, cols] = priv
-                logits = self._policy(obs, st)
+            self._store([(state.obs[pk], data["obs"][0, cols]), (state.obs[vk], data["priv"][0, cols])], st)
+            for t in range(T):
+                logits = self._policy(state.obs[pk], st)
                 check(self.lib.duck_policy_sample(n, A, logits.data_ptr(), self.seed, self.ctr.data_ptr(),
                                                   data["raw_action"][t, cols].data_ptr(),
                                                   data["log_prob"][t, cols].data_ptr(), self.action.data_ptr(), st))
                 self.env.step(state, self.action, inplace=True)  # obs already copied out
-                data["reward"][t, cols] = state.reward
-                data["done"][t, cols] = state.done
-                data["truncation"][t, cols] = state.info["truncation"]
-                data["next_priv"][t, cols] = state.obs[cfg.value_obs_key]
+                # the transition's outcome, and the observations the next env-step starts from (the
+                # state's obs after this step: they are row t + 1 of obs / priv, and next_priv's last row
+                # -- the only one the learner reads, the bootstrap observation)
+                out = [(state.reward, data["reward"][t, cols]), (state.done, data["done"][t, cols]),
+                       (state.info["truncation"], data["truncation"][t, cols])]
+                if t + 1 < T:
+                    out += [(state.obs[pk], data["obs"][t + 1, cols]), (state.obs[vk], data["priv"][t + 1, cols])]
+                else:
+                    out.append((state.obs[vk], data["next_priv"][t, cols]))
+                self._store(out, st)
 
     @torch.no_grad()
     def run(self, state) -> None:
