@@ -371,6 +371,8 @@ class FusedGrad:
     set to None), so the all-reduce over ranks is a single collective on that buffer."""
 
     SPLITS = 16      # partial products per weight gradient at most (duck_mlp_wgrad's row blocks)
+    # workgroups a weight gradient aims for (its 64 x 32 tiles times its row blocks)
+    WGRAD_TARGET = int(os.environ.get("DUCK_WGRAD_TARGET", "768"))
 
     def __init__(self, net: ActorCritic, rows: int, boot_rows: int, device):
         from .native import lib
@@ -446,7 +448,7 @@ class FusedGrad:
         h = x if i == 0 else b["H"][i - 1]
         mean, istd = (norm.mean32.data_ptr(), norm.istd32.data_ptr()) if (i == 0 and norm is not None) else (None, None)
         tiles = -(-m.out_features // 64) * -(-(m.in_features + 1) // 32)
-        splits = max(1, min(self.SPLITS, -(-768 // tiles), n // 64))
+        splits = max(1, min(self.SPLITS, -(-self.WGRAD_TARGET // tiles), n // 64))
         out = [DuckMlpProblem(3, n, m.in_features, m.out_features, d.data_ptr(), h.data_ptr(), None, None, None, None,
                               mean, istd, splits, self.P, self.off[id(m.weight)], self.off[id(m.bias)],
                               self.part.data_ptr())]
@@ -481,7 +483,7 @@ class FusedGrad:
             mean, istd = (norm.mean32.data_ptr(), norm.istd32.data_ptr()) if (i == 0 and norm is not None) else (None, None)
             # row blocks: enough workgroups to fill the chip (64 x 32 tiles over [W | b])
             tiles = -(-m.out_features // 64) * -(-(m.in_features + 1) // 32)
-            splits = max(1, min(self.SPLITS, -(-768 // tiles), n // 64))
+            splits = max(1, min(self.SPLITS, -(-self.WGRAD_TARGET // tiles), n // 64))
             check(self.lib.duck_mlp_wgrad(n, m.out_features, m.in_features, d.data_ptr(), h.data_ptr(), mean, istd,
                                           splits, self.part.data_ptr(), self.P, self.off[id(m.weight)],
                                           self.off[id(m.bias)], stream))
