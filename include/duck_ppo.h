@@ -124,6 +124,10 @@ int duck_mlp_group(int n, const duck_mlp_problem* problems, void* stream);
  * element's reduction runs in the same order whatever the tile, so the results are bit-identical;
  * 64-wide tiles halve the re-reads of the row operand for the wide layers. (Round 6.) */
 int duck_mlp_group_bn(int n, const duck_mlp_problem* problems, int bn, void* stream);
+/* duck_mlp_group with output tiles `bm` x `bn`: 64 x 32, 64 x 64 or 32 x 32 (bit-identical, as above). The
+ * 32 x 32 tiles give a launch with few tiles and short reductions twice the workgroups (the learner's
+ * third and fourth layers: 16 -> 12 us for the deepest backward launch). (Round 6.) */
+int duck_mlp_group_tiles(int n, const duck_mlp_problem* problems, int bm, int bn, void* stream);
 /* grad[i] = sum_{s < splits} partial[s][i] in order (deterministic), i < P */
 int duck_mlp_wgrad_reduce(int P, int splits, const float* partial, float* grad, void* stream);
 /* The rollout's policy sample (brax NormalTanhDistribution): for each of N rows of logits [N][2A]

@@ -218,15 +218,15 @@ __device__ __forceinline__ void mma_chunk(const float* As, const float* Bs, int 
 
 // Forward (MODE 0: Y = op(A) W^T + b; MODE 1: the same, Y = Z and Y2 = silu(Z)) and the data gradient
 // (MODE 2: Y = (A W) * silu'(aux), A = dZ [N][R], W [R][Mo], aux = Z_prev). Output [N][Mo].
-template <int MODE, int BNT = BN>
+template <int MODE, int BNT = BN, int BMT = BM>
 __device__ __forceinline__ void gemm_tile(int bx, int by, float* As, float* Bs, int N, int R, int Mo,
                                           const float* __restrict__ A, const float* __restrict__ W,
                                           const float* __restrict__ bias, const float* __restrict__ aux,
                                           float* __restrict__ Y, float* __restrict__ Y2,
                                           const float* __restrict__ mean, const float* __restrict__ istd) {
-  constexpr int TI = BM / 32, TJ = BNT / 32;
-  const int r0 = bx * BM, c0 = by * BNT;
-  const int w = threadIdx.x >> 6, wr = (BM / 2) * (w >> 1), wc = (BNT / 2) * (w & 1);
+  constexpr int TI = BMT / 32, TJ = BNT / 32;
+  const int r0 = bx * BMT, c0 = by * BNT;
+  const int w = threadIdx.x >> 6, wr = (BMT / 2) * (w >> 1), wc = (BNT / 2) * (w & 1);
   f4 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; i++)
@@ -234,7 +234,7 @@ __device__ __forceinline__ void gemm_tile(int bx, int by, float* As, float* Bs, 
     for (int j = 0; j < TJ; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   // two register sets of staged chunks (set k & 1 holds chunk k): chunk c + 2's loads are issued while
   // chunk c's MFMAs run and stored a whole chunk later, so each load has two chunks of MFMAs to land
-  RowTile<BM> la[2];
+  RowTile<BMT> la[2];
   RowTile<BNT> lbr[2];  // MODE 0/1: the rows of W (output columns), reduction contiguous
   ColTile<BNT> lbc[2];  // MODE 2: W [R][Mo], reduction over its rows
   for (int q = 0; q < 2; q++) {
@@ -315,21 +315,21 @@ __global__ __launch_bounds__(256) void mlp_gemm_kernel(int N, int R, int Mo, con
 // [dW | db][m][k] = sum over this workgroup's rows n of dZ[n][m] [op(H) | 1][n][k]: partial s =
 // blockIdx.z, written to part + s * P at the layer's offsets (weights at offw, bias at offb; P = the
 // parameter count of the networks sharing the partial array).
-template <int BNT = BN>
+template <int BNT = BN, int BMT = BM>
 __device__ __forceinline__ void wgrad_tile(int bx, int by, int bz, float* As, float* Bs, int N, int Mo, int Ki,
                                            const float* __restrict__ dZ, const float* __restrict__ H,
                                            const float* __restrict__ mean, const float* __restrict__ istd,
                                            int rows_per_split, float* __restrict__ part, int P, int offw, int offb) {
-  constexpr int TI = BM / 32, TJ = BNT / 32;
-  const int m0 = bx * BM, k0c = by * BNT, s = bz;
+  constexpr int TI = BMT / 32, TJ = BNT / 32;
+  const int m0 = bx * BMT, k0c = by * BNT, s = bz;
   const int n_lo = s * rows_per_split, R = min(N, n_lo + rows_per_split) - n_lo;
-  const int w = threadIdx.x >> 6, wr = (BM / 2) * (w >> 1), wc = (BNT / 2) * (w & 1);
+  const int w = threadIdx.x >> 6, wr = (BMT / 2) * (w >> 1), wc = (BNT / 2) * (w & 1);
   f4 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; i++)
 #pragma unroll
     for (int j = 0; j < TJ; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  ColTile<BM> la[2];  // A = dZ^T: columns m, reduction n over the rows (two staged chunks, as above)
+  ColTile<BMT> la[2];  // A = dZ^T: columns m, reduction n over the rows (two staged chunks, as above)
   ColTile<BNT> lb[2];  // B = [op(H) | 1]: columns k, rows n
   const float* dz = dZ + (size_t)(R > 0 ? n_lo : 0) * Mo;
   const float* h = H + (size_t)(R > 0 ? n_lo : 0) * Ki;
@@ -354,7 +354,7 @@ __device__ __forceinline__ void wgrad_tile(int bx, int by, int bz, float* As, fl
   __syncthreads();
   auto body = [&](int c, auto S, auto SN) {
     if (c + 2 < nch) load(S, KC * (c + 2));
-    mma_chunk<TI, TJ, false, nat_ld<BM>(), false, nat_ld<BNT>()>(As, Bs, wr, wc, acc);
+    mma_chunk<TI, TJ, false, nat_ld<BMT>(), false, nat_ld<BNT>()>(As, Bs, wr, wc, acc);
     __syncthreads();
     if (c + 1 < nch) {
       store(SN);
@@ -400,9 +400,11 @@ struct MlpGroupArgs {
   int gx[DUCK_MLP_GROUP_MAX], gy[DUCK_MLP_GROUP_MAX], rps[DUCK_MLP_GROUP_MAX];
   duck_mlp_problem p[DUCK_MLP_GROUP_MAX];
 };
-template <int BNT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNT == 32 ? DUCK_MLP_WPE : 1))) void mlp_group_kernel(MlpGroupArgs g) {
-  __shared__ __attribute__((aligned(16))) float As[tile_words<BM, BM>()], Bs[tile_words<BNT, BNT>()];
+// BMT = 32 (duck_mlp_group_tiles): half-height tiles, twice the workgroups, 58 registers and 12 KB of LDS
+// (8 waves per SIMD) -- for the launches with few tiles and short reductions (FusedGrad._row_tile)
+template <int BNT, int BMT = BM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNT == 32 ? (BMT == 32 ? 8 : DUCK_MLP_WPE) : 1))) void mlp_group_kernel(MlpGroupArgs g) {
+  __shared__ __attribute__((aligned(16))) float As[tile_words<BMT, BMT>()], Bs[tile_words<BNT, BNT>()];
   const int b = blockIdx.x;
   int q = 0;
 #pragma unroll
@@ -411,12 +413,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNT == 32 ?
   const int t = b - g.start[q], gx = g.gx[q], gy = g.gy[q];
   const int bz = t / (gx * gy), rem = t - bz * gx * gy, by = rem / gx, bx = rem - by * gx;
   switch (p.kind) {
-    case 0: gemm_tile<0, BNT>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, p.mean, p.istd); break;
-    case 1: gemm_tile<1, BNT>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, p.mean, p.istd); break;
-    case 2: gemm_tile<2, BNT>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, nullptr, nullptr); break;
+    case 0: gemm_tile<0, BNT, BMT>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, p.mean, p.istd); break;
+    case 1: gemm_tile<1, BNT, BMT>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, p.mean, p.istd); break;
+    case 2: gemm_tile<2, BNT, BMT>(bx, by, As, Bs, p.N, p.R, p.M, p.A, p.W, p.bias, p.aux, p.Y, p.Y2, nullptr, nullptr); break;
     default:
-      wgrad_tile<BNT>(bx, by, bz, As, Bs, p.N, p.M, p.R, p.A, p.W, p.mean, p.istd, g.rps[q], p.partial, p.P, p.off_w,
-                      p.off_b);
+      wgrad_tile<BNT, BMT>(bx, by, bz, As, Bs, p.N, p.M, p.R, p.A, p.W, p.mean, p.istd, g.rps[q], p.partial, p.P,
+                           p.off_w, p.off_b);
   }
 }
 
@@ -627,10 +629,12 @@ extern "C" int duck_mlp_wgrad(int N, int M, int K, const float* dZ, const float*
   return DUCK_OK;
 }
 
-extern "C" int duck_mlp_group_bn(int n, const duck_mlp_problem* probs, int bn, void* stream) {
+extern "C" int duck_mlp_group_tiles(int n, const duck_mlp_problem* probs, int bm, int bn, void* stream) {
   if (n < 0 || n > DUCK_MLP_GROUP_MAX) return duck_fail(DUCK_EINVAL, "duck_mlp_group: 0 .. DUCK_MLP_GROUP_MAX problems");
   if (bn != 32 && bn != 64) return duck_fail(DUCK_EINVAL, "duck_mlp_group_bn: tile width 32 or 64");
-  const int BN = bn;  // (shadows the default tile width for the grid arithmetic below)
+  if ((bm != 32 && bm != BM) || (bm == 32 && bn != 32))
+    return duck_fail(DUCK_EINVAL, "duck_mlp_group_tiles: tiles 64 x 32, 64 x 64 or 32 x 32");
+  const int BN = bn, BM = bm;  // (shadow the default tile sizes for the grid arithmetic below)
   if (n == 0) return DUCK_OK;
   if (!probs) return duck_fail(DUCK_EINVAL, "duck_mlp_group: null pointer");
   MlpGroupArgs g;
@@ -667,10 +671,16 @@ extern "C" int duck_mlp_group_bn(int n, const duck_mlp_problem* probs, int bn, v
   if (tot == 0) return DUCK_OK;
   if (bn == 64)
     hipLaunchKernelGGL(mlp_group_kernel<64>, dim3((unsigned)tot), dim3(256), 0, (hipStream_t)stream, g);
+  else if (bm == 32)
+    hipLaunchKernelGGL((mlp_group_kernel<32, 32>), dim3((unsigned)tot), dim3(256), 0, (hipStream_t)stream, g);
   else
     hipLaunchKernelGGL(mlp_group_kernel<32>, dim3((unsigned)tot), dim3(256), 0, (hipStream_t)stream, g);
   HIPCHECK(hipGetLastError());
   return DUCK_OK;
+}
+
+extern "C" int duck_mlp_group_bn(int n, const duck_mlp_problem* probs, int bn, void* stream) {
+  return duck_mlp_group_tiles(n, probs, BM, bn, stream);
 }
 
 extern "C" int duck_mlp_group(int n, const duck_mlp_problem* probs, void* stream) {

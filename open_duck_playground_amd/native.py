@@ -27,7 +27,7 @@ EXPORTS = ["duck_version", "duck_build_id", "duck_last_error", "duck_layout_get"
            "duck_step_kernel_for", "duck_debug_lat_timeouts", "duck_gather_columns", "duck_mlp_group",
            "duck_device_error", "duck_gae_stats", "duck_ppo_loss_stats", "duck_mlp_group_bn", "duck_gather_columns_norm",
            "duck_column_stats", "duck_column_stats_scratch", "duck_clip_adam_reduce", "duck_ppo_loss_grad",
-           "duck_ppo_loss_sums"]
+           "duck_ppo_loss_sums", "duck_mlp_group_tiles"]
 
 
 class DuckMlpProblem(C.Structure):
@@ -298,6 +298,8 @@ def lib(path: str = None):
             L.duck_mlp_group.argtypes = [C.c_int, C.POINTER(DuckMlpProblem), vp]
         if hasattr(L, "duck_mlp_group_bn"):
             L.duck_mlp_group_bn.argtypes = [C.c_int, C.POINTER(DuckMlpProblem), C.c_int, vp]
+        if hasattr(L, "duck_mlp_group_tiles"):
+            L.duck_mlp_group_tiles.argtypes = [C.c_int, C.POINTER(DuckMlpProblem), C.c_int, C.c_int, vp]
         if hasattr(L, "duck_gather_columns_norm"):
             L.duck_gather_columns_norm.argtypes = [C.c_int, C.POINTER(DuckGatherField), C.POINTER(C.c_void_p), vp,
                                                    C.c_int, vp]

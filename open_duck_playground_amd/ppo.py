@@ -462,10 +462,31 @@ class FusedGrad:
         from .native import DuckMlpProblem, check
         arr = (DuckMlpProblem * len(probs))(*probs)
         bn = self._tile_width(probs)
-        if bn != 32 and hasattr(self.lib, "duck_mlp_group_bn"):
+        bm = self._row_tile(probs) if bn == 32 else 64
+        if bm == 32 and hasattr(self.lib, "duck_mlp_group_tiles"):
+            check(self.lib.duck_mlp_group_tiles(len(probs), arr, 32, 32, stream))
+        elif bn != 32 and hasattr(self.lib, "duck_mlp_group_bn"):
             check(self.lib.duck_mlp_group_bn(len(probs), arr, bn, stream))
         else:
             check(self.lib.duck_mlp_group(len(probs), arr, stream))
+
+    @staticmethod
+    def _row_tile(probs) -> int:
+        """Output tile height of a grouped launch (duck_mlp_group_tiles; bit-identical either way): 32 when
+        the launch has fewer than 2,048 of the 64 x 32 tiles and no GEMM reduces over more than 256 -- there
+        the doubled workgroup count fills the chip (per launch, same box: the third and fourth layers'
+        forward 15.9 -> 15.3 and 7.5 -> 6.4 us, the deepest backward launch 15.4 -> 11.9, the next 26.2 ->
+        25.4); the wide layers keep 64 rows (their forward 40.0 -> 41.1 us at 32). DUCK_MLP_BM_AUTO = 0: 64."""
+        if os.environ.get("DUCK_MLP_BM_AUTO", "1") == "0":
+            return 64
+        tiles, red = 0, 0
+        for p in probs:
+            if p.kind == 3:
+                tiles += -(-p.M // 64) * -(-(p.R + 1) // 32) * p.splits
+            else:
+                tiles += -(-p.N // 64) * -(-p.M // 32)
+                red = max(red, p.R)
+        return 32 if tiles < 2048 and red <= 256 else 64
 
     @staticmethod
     def _tile_width(probs) -> int:

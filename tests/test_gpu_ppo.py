@@ -495,9 +495,20 @@ def test_mlp_group_equals_separate_launches(gpu):
             check(L.duck_mlp_group_bn(3, (DuckMlpProblem * 3)(*probs), 64, st))
             torch.cuda.synchronize()
             outs["group64"] = (Y, Y2, dX, part)
-    for a, b in zip(outs["separate"], outs["group64"]):
-        assert torch.equal(a, b)
+            # 32-row tiles (duck_mlp_group_tiles): the same bits again
+            Y, Y2, dX = torch.empty(N, M, device=gpu), torch.empty(N, M, device=gpu), torch.empty(N, R, device=gpu)
+            part = torch.zeros(3 * P, device=gpu)
+            probs[0].Y, probs[0].Y2, probs[1].Y, probs[2].partial = Y.data_ptr(), Y2.data_ptr(), dX.data_ptr(), \
+                part.data_ptr()
+            check(L.duck_mlp_group_tiles(3, (DuckMlpProblem * 3)(*probs), 32, 32, st))
+            torch.cuda.synchronize()
+            outs["group32rows"] = (Y, Y2, dX, part)
+    for key in ("group64", "group32rows"):
+        for a, b in zip(outs["separate"], outs[key]):
+            assert torch.equal(a, b), key
     assert L.duck_mlp_group_bn(1, (DuckMlpProblem * 1)(probs[0]), 48, st) < 0
+    assert L.duck_mlp_group_tiles(1, (DuckMlpProblem * 1)(probs[0]), 32, 64, st) < 0
+    assert L.duck_mlp_group_tiles(1, (DuckMlpProblem * 1)(probs[0]), 16, 32, st) < 0
     for a, b in zip(outs["separate"], outs["group"]):
         assert torch.equal(a, b)
     assert L.duck_mlp_group(5, (DuckMlpProblem * 5)(), st) < 0
