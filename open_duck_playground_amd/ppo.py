@@ -491,8 +491,8 @@ class FusedGrad:
     @staticmethod
     def _tile_width(probs) -> int:
         """Output tile width of a grouped launch (duck_mlp_group_bn; bit-identical either way). 32: with 64
-        every launch but the first layer's forward ran slower, and the whole update 1 % slower once the
-        normaliser moved into the gather (profiles/r06_ppo_learner.txt). DUCK_MLP_BN = 64 to try it."""
+        every launch ran slower on the final learner (288 -> 324 us per minibatch,
+        profiles/r06_ppo_tiles_ab.txt). DUCK_MLP_BN = 64 to try it."""
         return 64 if os.environ.get("DUCK_MLP_BN", "32") == "64" else 32
 
     def _backward(self, layers, b, x, norm, dout, n, stream):
