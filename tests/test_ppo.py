@@ -271,3 +271,29 @@ def test_split_k_linear_matches_linear(n, out):
     assert torch.allclose(x1.grad, x2.grad, atol=1e-5)
     assert torch.allclose(a.weight.grad, b.weight.grad, rtol=1e-5, atol=1e-4)
     assert torch.allclose(a.bias.grad, b.bias.grad, rtol=1e-5, atol=1e-4)
+
+
+def test_grouped_launch_row_tiles(monkeypatch):
+    """FusedGrad._row_tile on the learner's grouped launches (5,120-row minibatch, 512-256-128 MLPs, 101 / 172
+    inputs, 14 actions): 64-row tiles where many tiles or a long reduction fill the chip, 32-row tiles for the
+    third / fourth layers and the deepest backward launches (profiles/r06_ppo_tiles_ab.txt)."""
+    from open_duck_playground_amd.native import DuckMlpProblem
+
+    def gemm(kind, n, r, m):
+        return DuckMlpProblem(kind, n, r, m, None, None, None, None, None, None, None, None, 0, 0, 0, 0, None)
+
+    def wgrad(n, r, m, splits):
+        return DuckMlpProblem(3, n, r, m, None, None, None, None, None, None, None, None, splits, 0, 0, 0, None)
+
+    N, Nv = 5120, 5376
+    rt = ppo.FusedGrad._row_tile
+    assert rt([gemm(1, N, 101, 512), gemm(1, Nv, 172, 512)]) == 64            # first layers' forward
+    assert rt([gemm(1, N, 512, 256), gemm(1, Nv, 512, 256)]) == 64            # second layers: long reduction
+    assert rt([gemm(1, N, 256, 128), gemm(1, Nv, 256, 128)]) == 32            # third layers
+    assert rt([gemm(0, N, 128, 28), gemm(0, Nv, 128, 1)]) == 32               # heads
+    assert rt([wgrad(N, 256, 512, 12), gemm(2, N, 256, 512),                   # dgrad of the first layers
+               wgrad(Nv, 256, 512, 12), gemm(2, Nv, 256, 512)]) == 64
+    assert rt([wgrad(N, 128, 256, 16), gemm(2, N, 128, 256),
+               wgrad(Nv, 128, 256, 16), gemm(2, Nv, 128, 256)]) == 32
+    monkeypatch.setenv("DUCK_MLP_BM_AUTO", "0")
+    assert rt([gemm(1, N, 256, 128)]) == 64
